@@ -1,0 +1,329 @@
+#!/usr/bin/env python3
+"""Device-resident FedAvg aggregation throughput on MI355X (BASELINE.json metric).
+
+One step = one pass of the hot path over one round's synthetic client buckets
+already resident in HBM: the ordered weighted-sum reduction of D client buckets
+(pipeline_simulation/aggregator.cpp:59-93 / :112-150, FedAvg semantics) through
+libfa.so's C ABI (fa_reduce_device).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload northstar|c2|c3]
+                  [--layout range|client-rs] [--no-cpu-baseline] [--no-secondary]
+
+N > 1 runs one process per GPU (torch.distributed.run sets RANK/LOCAL_RANK/
+WORLD_SIZE).  Layout "range" (default) shards every bucket by element range:
+each rank reduces its own 256 MiB slice of all D clients, no collective
+(weak scaling).  Layout "client-rs" gives each rank 32 whole clients and
+combines the fp32 partials with an RCCL reduce-scatter over xGMI.
+
+value = bytes of client input reduced by all ranks / max-over-ranks wall time,
+in GiB/s (D * N * sizeof(in) / t / 2^30).  roofline.achieved = algorithmic HBM
+bytes per launch ((D+1) * N * sizeof for f32->f32) / average launch duration
+from HIP events on the launch stream.
+"""
+import argparse
+import importlib.util
+import json
+import os
+import statistics
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.join(ROOT, "multihop-federeated-split-learning_amd")
+HBM_PEAK_GBS = 8000.0  # MI355X spec HBM3E bandwidth (MI355X_MICROARCH.md chip table)
+
+WORKLOADS = {
+    # name: (clients per rank, elements per client per rank, in dtype, out dtype, description)
+    "northstar": (32, 64 << 20, "f32", "f32", "256 MiB fp32 bucket x 32 clients (north-star target)"),
+    "c2": (8, 12_557_962, "f32", "f32", "ResNet-18 full model buckets (reference build), 8 data owners, fp32"),
+    "c3": (32, 42_737_546, "bf16", "bf16", "ResNet-101 full model buckets (basic-block build), 32 owners, bf16"),
+}
+ROTATE_MIN_BYTES = 1 << 30  # rotate input sets until a step's working set no longer fits the 256 MiB MALL
+
+
+def load_pkg():
+    if "mhfsl_amd" in sys.modules:
+        return sys.modules["mhfsl_amd"]
+    spec = importlib.util.spec_from_file_location("mhfsl_amd", os.path.join(PKG_DIR, "__init__.py"),
+                                                  submodule_search_locations=[PKG_DIR])
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["mhfsl_amd"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+# ------------------------------------------------------------------ CPU baseline (rank 0, N = 1)
+
+def cpu_threads():
+    n = len(os.sched_getaffinity(0))
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(n, cap) if cap > 0 else n)
+
+
+def cpu_baseline(D, sample_elems, reps):
+    """libtorch CPU FedAvg (acc.add_(x_k, w_k) in client order) on a bounded sample of the workload.
+
+    Preferred: oracle/_ref/ref_harness (built from the reference's sources, linked with libtorch, the
+    library the reference's arithmetic runs in) -> kind "reference".  Fallback: the C oracle -> "port".
+    Run BEFORE the GPU is initialised: the baseline is a child process.
+    """
+    threads = cpu_threads()
+    harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    sample = "D=%d clients x %d fp32 elements (%.0f MiB per client), %d timed reps after 1 warm-up" % (
+        D, sample_elems, sample_elems * 4 / 2**20, reps)
+    if os.access(harness, os.X_OK):
+        try:
+            out = subprocess.run([harness, "bench-fedavg", str(sample_elems), str(D), str(threads), str(reps)],
+                                 capture_output=True, text=True, timeout=600, check=True).stdout
+            r = json.loads(out.strip().splitlines()[-1])
+            return {"value": round(r["gib_s"], 3), "unit": "GiB/s", "cores": threads, "kind": "reference",
+                    "sample": sample + "; libtorch at::set_num_threads(%d)" % threads}
+        except Exception as e:  # noqa: BLE001 -- fall through to the port
+            print("cpu baseline: ref_harness failed (%s), timing the oracle port" % e, file=sys.stderr)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    xs = [oracle.gen(0x5EED, k, sample_elems) for k in range(D)]
+    w = oracle.weights(D)
+    oracle.fedavg(xs, w, threads=threads)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        oracle.fedavg(xs, w, threads=threads)
+    dt = (time.perf_counter() - t0) / reps
+    return {"value": round(D * sample_elems * 4 / dt / 2**30, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": sample + "; C oracle fmaf chain, %d threads" % threads}
+
+
+# ------------------------------------------------------------------ device measurement
+
+def traffic_from_profile(workload, n_gpus):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), if present."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if n_gpus != 1 or not os.path.exists(p):
+        return None, None
+    with open(p) as f:
+        d = json.load(f)
+    rec = d.get(workload)
+    if not rec:
+        return None, None
+    return rec.get("hbm_bytes_per_launch"), rec.get("source")
+
+
+class Setup:
+    """Device buffers of one workload on the current GPU: `sets` rotated input sets of D clients."""
+
+    def __init__(self, fa, torch, D, n, in_dt, out_dt, rank, seed=0x5EED, min_rotate_bytes=ROTATE_MIN_BYTES):
+        self.fa, self.torch = fa, torch
+        self.D, self.n = D, n
+        self.in_dt = fa.F32 if in_dt == "f32" else fa.BF16
+        self.out_dt = fa.F32 if out_dt == "f32" else fa.BF16
+        self.s_in = 4 if in_dt == "f32" else 2
+        self.s_out = 4 if out_dt == "f32" else 2
+        set_bytes = D * n * self.s_in
+        self.nsets = max(1, -(-min_rotate_bytes // set_bytes))
+        tdt = torch.float32 if in_dt == "f32" else torch.int16
+        self.sets = []
+        for s in range(self.nsets):
+            clients = []
+            for k in range(D):
+                t = torch.empty(n, dtype=tdt, device="cuda")
+                # element index offset by the rank's range so ranks hold disjoint slices of one bucket
+                fa.fill_uniform(t, n, self.in_dt, seed + s, k, idx0=rank * n)
+                clients.append(t)
+            self.sets.append(clients)
+        self.out = torch.empty(n, dtype=torch.float32 if out_dt == "f32" else torch.int16, device="cuda")
+        self.w = self._weights(D)
+
+    @staticmethod
+    def _weights(D):
+        # same as oracle.weights(D) (splitmix64-derived n_k in [500,1500], w_k = n_k / sum n), computed here
+        # so the product path does not import the oracle.
+        import numpy as np
+        M = (1 << 64) - 1
+
+        def sm(z):
+            z = (z + 0x9E3779B97F4A7C15) & M
+            z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+            z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+            return z ^ (z >> 31)
+        nk = [500 + sm(7 ^ (k << 32)) % 1001 for k in range(D)]
+        tot = float(sum(nk))
+        return np.array([float(x) / tot for x in nk], np.float32)
+
+    def launch(self, step, stream):
+        self.fa.reduce_device(self.sets[step % self.nsets], self.w, self.n, self.in_dt, self.out, self.out_dt,
+                              self.fa.FEDAVG, stream=stream)
+
+    def algo_bytes(self):
+        return self.D * self.n * self.s_in + self.n * self.s_out
+
+    def input_bytes(self):
+        return self.D * self.n * self.s_in
+
+
+def timed_loop(torch, setup, steps, warmup, stream, dist, barrier):
+    for i in range(warmup):
+        setup.launch(i, stream)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for i in range(steps):
+        evs[i][0].record(stream)
+        setup.launch(warmup + i, stream)
+        evs[i][1].record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in evs]
+    return wall, kern_ms
+
+
+def run_rs_step(fa, torch, setup, partial, shard, stream, dist):
+    """client-rs: local chain over this rank's clients into fp32 partials, then RCCL reduce-scatter."""
+    fa.reduce_device(setup.sets[0], setup.w, setup.n, setup.in_dt, partial, fa.F32, fa.FEDAVG, stream=stream)
+    with torch.cuda.stream(stream):
+        dist.reduce_scatter_tensor(shard, partial, op=dist.ReduceOp.SUM)
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="northstar", choices=sorted(WORKLOADS))
+    ap.add_argument("--layout", default="range", choices=["range", "client-rs"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--tune", default="", help="block,max_blocks,unroll,nontemporal")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world), file=sys.stderr)
+    D, n, in_dt, out_dt, desc = WORKLOADS[args.workload]
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(D, 16 << 20, 10)
+
+    import torch
+    import torch.distributed as dist
+    fa = load_pkg()
+    torch.cuda.set_device(local_rank)
+    fa.lib()
+    if args.tune:
+        b, mb, u, nt = [int(x) for x in args.tune.split(",")]
+        fa.set_tuning(block=b, max_blocks=mb, unroll=u, nontemporal=nt)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+        def barrier():
+            dist.barrier()
+    else:
+        def barrier():
+            pass
+
+    stream = torch.cuda.Stream()
+    setup = Setup(fa, torch, D, n, in_dt, out_dt, rank)
+    torch.cuda.synchronize()
+
+    if args.layout == "range":
+        wall, kern_ms = timed_loop(torch, setup, args.steps, args.warmup, stream, dist, barrier)
+        units_bytes = setup.input_bytes() * world
+        layout_desc = "range-sharded: each rank owns %d of %d elements of every bucket, no collective" % (
+            n, n * world)
+    else:
+        partial = torch.empty(n, dtype=torch.float32, device="cuda")
+        shard = torch.empty(n // world, dtype=torch.float32, device="cuda")
+        for _ in range(args.warmup):
+            run_rs_step(fa, torch, setup, partial, shard, stream, dist)
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            evs[i][0].record(stream)
+            fa.reduce_device(setup.sets[0], setup.w, n, setup.in_dt, partial, fa.F32, fa.FEDAVG, stream=stream)
+            evs[i][1].record(stream)
+            with torch.cuda.stream(stream):
+                if world > 1:
+                    dist.reduce_scatter_tensor(shard, partial, op=dist.ReduceOp.SUM)
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        kern_ms = [a.elapsed_time(b) for a, b in evs]
+        units_bytes = setup.input_bytes() * world
+        layout_desc = "client-sharded: each rank reduces %d whole clients into fp32 partials, RCCL reduce-scatter" % D
+
+    if world > 1:
+        t = torch.tensor([wall], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+
+    kavg = statistics.mean(kern_ms)
+    achieved = setup.algo_bytes() / (kavg * 1e-3) / 1e9
+    traffic, traffic_src = traffic_from_profile(args.workload, world)
+    line = {
+        "metric": "GiB/s aggregated (device-resident), D-client fp32 bucket FedAvg reduce",
+        "value": round(units_bytes * args.steps / wall / 2**30, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": in_dt,
+        "data": "synthetic (counter-based splitmix64 uniform[-1,1), generated in HBM)",
+        "config": {"workload": args.workload, "description": desc, "clients": D * (world if args.layout ==
+                                                                                     "client-rs" else 1),
+                   "elems_per_client": n * (world if args.layout == "range" else 1), "in_dtype": in_dt,
+                   "out_dtype": out_dt, "layout": layout_desc, "parallelism": "%s%d" % (
+                       "range" if args.layout == "range" else "rs", world),
+                   "tuning": fa.get_tuning(), "input_sets_rotated": setup.nsets},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": setup.algo_bytes(),
+                     "kernel_ms_avg": round(kavg, 4), "kernel_ms_min": round(min(kern_ms), 4),
+                     "kernel_ms_median": round(statistics.median(kern_ms), 4)},
+        "cpu_baseline": cpu,
+    }
+
+    if rank == 0 and world == 1 and not args.no_secondary:
+        sec = {}
+        del setup
+        torch.cuda.empty_cache()
+        for name in sorted(WORKLOADS):
+            if name == args.workload:
+                continue
+            sD, sn, si, so, sdesc = WORKLOADS[name]
+            s = Setup(fa, torch, sD, sn, si, so, 0)
+            torch.cuda.synchronize()
+            w2, km = timed_loop(torch, s, max(10, args.steps), 3, stream, dist, barrier)
+            ka = statistics.mean(km)
+            sec[name] = {"description": sdesc, "gib_s": round(s.input_bytes() * max(10, args.steps) / w2 / 2**30, 1),
+                         "kernel_ms_avg": round(ka, 4),
+                         "achieved_GBs": round(s.algo_bytes() / (ka * 1e-3) / 1e9, 1),
+                         "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "input_sets_rotated": s.nsets}
+            del s
+            torch.cuda.empty_cache()
+        line["secondary"] = sec
+
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

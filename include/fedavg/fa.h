@@ -1,0 +1,124 @@
+/*
+ * fa.h -- C ABI of the MI355X FedAvg aggregation path (libfa.so).
+ *
+ * The reference has no plugin/FFI seam: the reduction is inline in the
+ * aggregator's main() (pipeline_simulation/aggregator.cpp:55-167).  These
+ * entry points replace that inline code; each declaration names the reference
+ * lines it stands in for.  Plain pointers and sizes only, no torch types, no
+ * C++ exceptions across the boundary.  Every call returns FA_OK (0) or a
+ * negative fa_status; fa_last_error() gives a thread-local message.
+ *
+ * Threading: one fa_ctx per aggregator; calls on one ctx are serialized by the
+ * caller (the reference's single consumer main thread, aggregator.cpp:60/:113).
+ * Device work runs on ctx-owned HIP streams (one compute + one copy stream per
+ * GPU) or on the caller's stream for fa_reduce_device.
+ *
+ * Numerics (tests/, DESIGN.md "Parity"):
+ *   FA_FEDAVG  out_i = sum_k w_k x_{k,i} as an ordered fp32 FMA chain in client
+ *              order starting from +0 (== libtorch acc.add_(x_k, w_k)),
+ *              bf16 inputs widened exactly, bf16 output rounded to nearest-even
+ *              once at the end.  Bit-exact vs oracle/ on every GPU layout
+ *              except FA_SHARD_CLIENT_RS (summation order changes, <=1e-6
+ *              relative to sum_k |w_k x_k|).
+ *   FA_LITERAL out_i = fl(fl(x_i + x_i) / divisor), x = the LAST client
+ *              submitted (aggregator.cpp:63-88 with parts/parts_ aliased,
+ *              systemAPI.cpp:34-37); divisor defaults to kTrainSize_10 = 1000
+ *              (aggregator.cpp:48).  Correctly rounded division.
+ */
+#ifndef FEDAVG_FA_H_
+#define FEDAVG_FA_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FA_ABI_VERSION 1
+
+typedef struct fa_ctx fa_ctx; /* opaque: device slots, streams, pinned staging */
+
+typedef enum { FA_F32 = 0, FA_BF16 = 1 } fa_dtype;
+typedef enum { FA_FEDAVG = 0, FA_LITERAL = 1 } fa_mode;
+
+typedef enum {
+    FA_OK = 0,
+    FA_ERR_ARG = -1,     /* bad argument (null pointer, size, dtype, slot) */
+    FA_ERR_HIP = -2,     /* a HIP runtime call failed */
+    FA_ERR_NOMEM = -3,   /* device or pinned allocation failed */
+    FA_ERR_STATE = -4,   /* call out of order (e.g. finalize before any submit) */
+    FA_ERR_NODEV = -5,   /* no usable gfx950 device */
+    FA_ERR_ALIGN = -6    /* pointer not 4-byte (f32) / 2-byte (bf16) aligned */
+} fa_status;
+
+/* fa_create flags */
+#define FA_SHARD_RANGE 0x1 /* n_gpus > 1: GPU g owns elements [g*n/G, (g+1)*n/G) of every bucket */
+
+int fa_version(void);
+const char* fa_last_error(void); /* thread-local; "" when the last call succeeded */
+int fa_device_count(int* out);   /* visible HIP devices */
+
+/* Replaces the aggregator's state construction: systemAPI sys_(true, -1, ...)
+ * + refactor() -> init_model_sate (aggregator.cpp:47,53; systemAPI.cpp:17-38).
+ * Uses devices 0..n_gpus-1. */
+int fa_create(fa_ctx** out, int n_gpus, int flags);
+void fa_destroy(fa_ctx* ctx);
+
+/* One reduced bucket = the flattened named_parameters() of one model part
+ * (model_part 1 -> parts[0].layers[0], aggregator.cpp:64; model_part m >= 2 ->
+ * parts[1].layers[m-2], :118).  Allocates n_clients device slots per GPU. */
+int fa_bucket_define(fa_ctx* ctx, int part_id, size_t n_elems, fa_dtype in, fa_dtype out, int n_clients,
+                     fa_mode mode);
+/* kTrainSize_10 of aggregator.cpp:48 for FA_LITERAL buckets (default 1000). */
+int fa_set_literal_divisor(fa_ctx* ctx, int part_id, float divisor);
+
+/* Replaces one receipt: torch::load into the global module + the per-parameter
+ * update (aggregator.cpp:63-88 / :117-142).  Copies host_src (n_elems of the
+ * bucket dtype, caller-owned, reusable on return) through ctx pinned staging
+ * to the device slot asynchronously.  weight = w_k for FA_FEDAVG (ignored for
+ * FA_LITERAL).  Submitting a slot twice in one round overwrites it. */
+int fa_submit(fa_ctx* ctx, int part_id, int client_slot, const void* host_src, float weight);
+/* Same, but host_src is pinned (hipHostMalloc'd / registered) memory that the
+ * caller keeps unchanged until fa_finalize returns: no staging copy. */
+int fa_submit_pinned(fa_ctx* ctx, int part_id, int client_slot, const void* host_src, float weight);
+
+/* Replaces the end of a phase: the reduced module handed to new_message()
+ * (aggregator.cpp:96-106 / :153-166).  Waits for the submits, reduces on every
+ * GPU, copies the result (out dtype) to host_dst and resets the round. */
+int fa_finalize(fa_ctx* ctx, int part_id, void* host_dst);
+
+/* Raw device entry for benches and device-resident callers: reduce D client
+ * buckets already resident on device `gpu` into d_out.  d_clients[k] are device
+ * pointers, h_weights a host array of D floats (copied into kernel arguments,
+ * any D >= 1).  d_init (nullable, fp32, n) continues an earlier chain: acc
+ * starts at d_init[i] instead of +0 (used to split clients across launches or
+ * GPUs bit-exactly).  Enqueued on hip_stream (a hipStream_t; NULL = the
+ * ctx's compute stream of `gpu`); returns without synchronizing.  ctx may be
+ * NULL except for bf16 output with D > 64 (needs ctx scratch). */
+int fa_reduce_device(fa_ctx* ctx, int gpu, const void* const* d_clients, const float* h_weights, int D, size_t n,
+                     fa_dtype in, void* d_out, fa_dtype out, fa_mode mode, const float* d_init, void* hip_stream);
+
+/* Literal mode divisor used by fa_reduce_device when ctx == NULL. */
+#define FA_DEFAULT_DIVISOR 1000.0f
+
+/* Synthetic input generator on device, identical to oracle/fa_oracle.c:
+ * element i = uniform[-1,1) from splitmix64(seed ^ client<<40 ^ (idx0+i)),
+ * bf16 = round-to-nearest-even of that value. */
+int fa_fill_uniform(void* d_dst, size_t n, fa_dtype dt, uint64_t seed, uint32_t client, uint64_t idx0,
+                    void* hip_stream);
+
+/* Kernel tuning knobs for benches (0 = library default). */
+typedef struct {
+    int block;       /* threads per workgroup (multiple of 64) */
+    int max_blocks;  /* grid cap; grid-stride beyond it */
+    int unroll;      /* clients loaded per FMA group: 4, 8 or 16 */
+    int nontemporal; /* 1: nt loads/stores, 0: default cache policy, -1: library default */
+} fa_tuning;
+int fa_set_tuning(const fa_tuning* t);
+int fa_get_tuning(fa_tuning* t);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FEDAVG_FA_H_ */

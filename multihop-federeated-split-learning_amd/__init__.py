@@ -1,0 +1,196 @@
+"""MI355X FedAvg aggregation path -- Python view of the C ABI in include/fedavg/fa.h.
+
+The product is ``lib/libfa.so`` (HIP kernels + C ABI, built by this directory's
+Makefile).  This module only binds it with ctypes so tests, bench.py and the
+multi-GPU driver (``shard.py``) can call it; there is no CPU fallback: if the
+library or a gfx950 device is missing, calls raise ``FaError``.
+
+Names mirror the reference aggregator (pipeline_simulation/aggregator.cpp):
+a *part* is one model part bucket (``model_part`` 1 = parts[0].layers[0],
+m >= 2 = parts[1].layers[m-2]), a *client slot* is one data owner's receipt.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libfa.so")
+
+F32, BF16 = 0, 1
+FEDAVG, LITERAL = 0, 1
+SHARD_RANGE = 0x1
+OK, ERR_ARG, ERR_HIP, ERR_NOMEM, ERR_STATE, ERR_NODEV, ERR_ALIGN = 0, -1, -2, -3, -4, -5, -6
+DTYPE_SIZE = {F32: 4, BF16: 2}
+
+_lib = None
+
+
+class FaError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("fa error %d: %s" % (code, msg))
+        self.code = code
+
+
+class _Tuning(ctypes.Structure):
+    _fields_ = [("block", ctypes.c_int), ("max_blocks", ctypes.c_int), ("unroll", ctypes.c_int),
+                ("nontemporal", ctypes.c_int)]
+
+
+def build():
+    """Compile libfa.so in-tree (hipcc, gfx950)."""
+    import subprocess
+    subprocess.run(["make", "-C", PKG_DIR, "-j8"], check=True)
+    return LIB_PATH
+
+
+def lib():
+    """Load libfa.so (torch, when used, must be imported first: both share libamdhip64.so.7)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FaError(ERR_NODEV, "libfa.so not built at %s (run make -C %s)" % (LIB_PATH, PKG_DIR))
+    L = ctypes.CDLL(LIB_PATH)
+    P, S, I, F, U64, U32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_float, ctypes.c_uint64, ctypes.c_uint32
+    sig = {
+        "fa_version": (I, []),
+        "fa_last_error": (ctypes.c_char_p, []),
+        "fa_device_count": (I, [ctypes.POINTER(I)]),
+        "fa_create": (I, [ctypes.POINTER(P), I, I]),
+        "fa_destroy": (None, [P]),
+        "fa_bucket_define": (I, [P, I, S, I, I, I, I]),
+        "fa_set_literal_divisor": (I, [P, I, F]),
+        "fa_submit": (I, [P, I, I, P, F]),
+        "fa_submit_pinned": (I, [P, I, I, P, F]),
+        "fa_finalize": (I, [P, I, P]),
+        "fa_reduce_device": (I, [P, I, P, P, I, S, I, P, I, I, P, P]),
+        "fa_fill_uniform": (I, [P, S, I, U64, U32, U64, P]),
+        "fa_set_tuning": (I, [ctypes.POINTER(_Tuning)]),
+        "fa_get_tuning": (I, [ctypes.POINTER(_Tuning)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != OK:
+        raise FaError(rc, lib().fa_last_error().decode(errors="replace"))
+    return rc
+
+
+def last_error():
+    return lib().fa_last_error().decode(errors="replace")
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    check(lib().fa_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def _addr(x):
+    """Device/host address of a torch tensor, numpy array or raw int."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data
+    raise TypeError("need a tensor, array or int address, got %r" % type(x))
+
+
+def _stream(stream):
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream  # torch.cuda.Stream on ROCm wraps a hipStream_t
+
+
+def reduce_device(clients, weights, n, in_dtype, out, out_dtype=F32, mode=FEDAVG, init=None, stream=None, gpu=0,
+                  ctx=None):
+    """fa_reduce_device: D device-resident client buckets -> out (enqueued, not synchronized)."""
+    D = len(clients)
+    arr = (ctypes.c_void_p * D)(*[_addr(c) for c in clients])
+    w = np.ascontiguousarray(np.asarray(weights, np.float32).reshape(-1))
+    if w.size != D:
+        raise ValueError("need one weight per client")
+    check(lib().fa_reduce_device(ctx.handle if ctx is not None else None, gpu, arr, w.ctypes.data, D, n, in_dtype,
+                                 _addr(out), out_dtype, mode, _addr(init), _stream(stream)))
+
+
+def fill_uniform(dst, n, dtype, seed, client, idx0=0, stream=None):
+    check(lib().fa_fill_uniform(_addr(dst), n, dtype, seed, client, idx0, _stream(stream)))
+
+
+def get_tuning():
+    t = _Tuning()
+    check(lib().fa_get_tuning(ctypes.byref(t)))
+    return {"block": t.block, "max_blocks": t.max_blocks, "unroll": t.unroll, "nontemporal": t.nontemporal}
+
+
+def set_tuning(block=0, max_blocks=0, unroll=0, nontemporal=-1):
+    t = _Tuning(block, max_blocks, unroll, nontemporal)
+    check(lib().fa_set_tuning(ctypes.byref(t)))
+
+
+class Aggregator:
+    """fa_ctx: the aggregator's global parts on 1..G GPUs (range-sharded when G > 1).
+
+    Usage mirrors one aggregation phase of aggregator.cpp: define the bucket
+    once (refactor), submit every receipt, finalize to obtain the reduced part.
+    """
+
+    def __init__(self, n_gpus=1, flags=None):
+        if flags is None:
+            flags = SHARD_RANGE if n_gpus > 1 else 0
+        h = ctypes.c_void_p()
+        check(lib().fa_create(ctypes.byref(h), n_gpus, flags))
+        self.handle = h
+        self.parts = {}
+
+    def define(self, part_id, n, in_dtype=F32, out_dtype=F32, n_clients=1, mode=FEDAVG):
+        check(lib().fa_bucket_define(self.handle, part_id, n, in_dtype, out_dtype, n_clients, mode))
+        self.parts[part_id] = (n, in_dtype, out_dtype, n_clients, mode)
+
+    def set_divisor(self, divisor, part_id=-1):
+        check(lib().fa_set_literal_divisor(self.handle, part_id, divisor))
+
+    def submit(self, part_id, slot, host, weight=1.0, pinned=False):
+        host = np.ascontiguousarray(host)
+        n, in_dtype = self.parts[part_id][:2]
+        if host.nbytes != n * DTYPE_SIZE[in_dtype]:
+            raise ValueError("bucket %d expects %d bytes, got %d" % (part_id, n * DTYPE_SIZE[in_dtype], host.nbytes))
+        fn = lib().fa_submit_pinned if pinned else lib().fa_submit
+        check(fn(self.handle, part_id, slot, host.ctypes.data, float(weight)))
+
+    def finalize(self, part_id, out=None):
+        n, _, out_dtype = self.parts[part_id][:3]
+        if out is None:
+            out = np.empty(n, np.float32 if out_dtype == F32 else np.uint16)
+        check(lib().fa_finalize(self.handle, part_id, out.ctypes.data))
+        return out
+
+    def close(self):
+        if self.handle:
+            lib().fa_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

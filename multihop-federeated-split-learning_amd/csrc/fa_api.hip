@@ -1,0 +1,478 @@
+// fa_api.hip -- the C ABI (include/fedavg/fa.h): aggregation context, device
+// slots, pinned staging, multi-GPU range sharding, and the raw device entry.
+//
+// What it replaces in the reference (paths relative to the reference root):
+//   fa_create / fa_bucket_define  <- systemAPI(true,-1,..) + refactor() ->
+//       init_model_sate (aggregator.cpp:47,53; systemAPI.cpp:17-38): the global
+//       model parts the aggregator owns.
+//   fa_submit                     <- one receipt: torch::load of Task.model_parts
+//       into parts_[..] and the per-parameter update (aggregator.cpp:60-92,
+//       :113-149).  Here the bytes are staged to HBM; the arithmetic is deferred
+//       to finalize so that it runs as one ordered chain over all clients.
+//   fa_finalize                   <- the reduced module handed to new_message()
+//       (aggregator.cpp:96-106, :153-166).
+// No CPU fallback exists: without a gfx950 device every entry that needs one
+// returns FA_ERR_NODEV.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "fa_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+fa::Tuning g_tuning{256, 0, 8, 1};
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define FA_HIP(call)                                                                               \
+    do {                                                                                           \
+        hipError_t e_ = (call);                                                                    \
+        if (e_ != hipSuccess) return fail(FA_ERR_HIP, "%s: %s (%s:%d)", #call, hipGetErrorString(e_), \
+                                          __FILE__, __LINE__);                                     \
+    } while (0)
+
+inline size_t dsize(fa_dtype t) { return t == FA_F32 ? 4 : 2; }
+inline bool dvalid(int t) { return t == FA_F32 || t == FA_BF16; }
+
+// Restores the caller's current device on scope exit.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (dev >= 0 && dev != prev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+constexpr size_t kStageBytes = 32u << 20;  // pinned staging chunk per buffer
+
+struct GpuRes {
+    int dev = 0;
+    hipStream_t compute = nullptr, copy = nullptr;
+    char* stage[2] = {nullptr, nullptr};
+    hipEvent_t stage_ev[2] = {nullptr, nullptr};
+    int stage_i = 0;
+    void* scratch = nullptr;  // fp32 chain accumulator for bf16-out, D > kMaxClients
+    size_t scratch_bytes = 0;
+};
+
+struct Part {
+    size_t n = 0;
+    fa_dtype in = FA_F32, out = FA_F32;
+    int D = 0;
+    fa_mode mode = FA_FEDAVG;
+    float divisor = FA_DEFAULT_DIVISOR;
+    std::vector<size_t> off, cnt;  // per-GPU element range
+    std::vector<char*> slots;      // per GPU: D * cnt * dsize(in)
+    std::vector<void*> dout;       // per GPU: cnt * dsize(out)
+    std::vector<float> w;
+    std::vector<char> submitted;
+    int n_submitted = 0;
+    int last_slot = -1;
+};
+
+}  // namespace
+
+struct fa_ctx {
+    int G = 1;
+    int flags = 0;
+    float divisor = FA_DEFAULT_DIVISOR;
+    std::vector<GpuRes> gpu;
+    std::map<int, Part> parts;
+};
+
+namespace {
+
+// Scratch of at least `bytes` on GPU g (only used by bf16 output with D > kMaxClients).
+int ensure_scratch(fa_ctx* ctx, int g, size_t bytes) {
+    GpuRes& r = ctx->gpu[g];
+    if (r.scratch_bytes >= bytes) return FA_OK;
+    DeviceGuard dg(r.dev);
+    if (r.scratch) FA_HIP(hipFree(r.scratch));
+    r.scratch = nullptr;
+    r.scratch_bytes = 0;
+    if (hipMalloc(&r.scratch, bytes) != hipSuccess) return fail(FA_ERR_NOMEM, "scratch alloc of %zu B failed", bytes);
+    r.scratch_bytes = bytes;
+    return FA_OK;
+}
+
+bool aligned(const void* p, size_t a) { return ((uintptr_t)p % a) == 0; }
+
+// The device reduction for one GPU, shared by fa_reduce_device and fa_finalize.
+int reduce_on(fa_ctx* ctx, int g, const void* const* clients, const float* w, int D, size_t n, fa_dtype in,
+              void* dst, fa_dtype out, fa_mode mode, float divisor, const float* init, hipStream_t s) {
+    if (n == 0) return FA_OK;
+    const size_t si = dsize(in), so = dsize(out);
+    const int V = (int)(16 / si);
+    for (int k = 0; k < D; ++k)
+        if (!clients[k]) return fail(FA_ERR_ARG, "client pointer %d is null", k);
+    if (!dst) return fail(FA_ERR_ARG, "output pointer is null");
+    for (int k = 0; k < D; ++k)
+        if (!aligned(clients[k], si)) return fail(FA_ERR_ALIGN, "client %d not %zu-byte aligned", k, si);
+    if (!aligned(dst, so)) return fail(FA_ERR_ALIGN, "output not %zu-byte aligned", so);
+    if (init && !aligned(init, 4)) return fail(FA_ERR_ALIGN, "init not 4-byte aligned");
+
+    // Vector path: every input shares one 16-byte phase; head elements bring it to 0.
+    const size_t phase = ((uintptr_t)clients[mode == FA_LITERAL ? D - 1 : 0] % 16) / si;
+    int64_t head = (int64_t)((V - phase) % V);
+    if ((size_t)head > n) head = (int64_t)n;
+    const int64_t nvec = (int64_t)(n - (size_t)head) / V;
+    bool vec = true;
+    if (mode == FA_FEDAVG)
+        for (int k = 0; k < D; ++k) vec = vec && (((uintptr_t)clients[k] % 16) / si == phase);
+    const size_t out_vec_bytes = (size_t)V * so;  // 16 or 32 (f32 out of bf16) or 8 (bf16 out of f32)
+    vec = vec && ((uintptr_t)dst + (size_t)head * so) % std::min<size_t>(16, out_vec_bytes) == 0;
+    if (init) vec = vec && ((uintptr_t)init + (size_t)head * 4) % 16 == 0;
+
+    if (mode == FA_LITERAL) {
+        FA_HIP(fa::launch_literal(clients[D - 1], in, dst, out, divisor, head, nvec, (int64_t)n, vec, g_tuning, s));
+        return FA_OK;
+    }
+
+    const int passes = (D + fa::kMaxClients - 1) / fa::kMaxClients;
+    float* acc = nullptr;  // fp32 accumulator between passes
+    if (passes > 1) {
+        if (out == FA_F32) {
+            acc = static_cast<float*>(dst);
+        } else {
+            if (!ctx) return fail(FA_ERR_ARG, "bf16 output with D > %d needs a ctx for scratch", fa::kMaxClients);
+            int rc = ensure_scratch(ctx, g, n * 4);
+            if (rc) return rc;
+            acc = static_cast<float*>(ctx->gpu[g].scratch);
+            vec = vec && ((uintptr_t)acc + (size_t)head * 4) % 16 == 0;
+        }
+    }
+    for (int p = 0; p < passes; ++p) {
+        fa::ClientTable t;
+        const int k0 = p * fa::kMaxClients, nc = std::min(fa::kMaxClients, D - k0);
+        for (int k = 0; k < nc; ++k) {
+            t.src[k] = clients[k0 + k];
+            t.w[k] = w[k0 + k];
+        }
+        const float* pin = p == 0 ? init : acc;
+        const bool last = p == passes - 1;
+        void* pdst = last ? dst : acc;
+        FA_HIP(fa::launch_chain(t, nc, in, last ? out : FA_F32, pin, pdst, head, nvec, (int64_t)n, vec, g_tuning, s));
+    }
+    return FA_OK;
+}
+
+int check_part(fa_ctx* ctx, int part_id, Part** out) {
+    if (!ctx) return fail(FA_ERR_ARG, "ctx is null");
+    auto it = ctx->parts.find(part_id);
+    if (it == ctx->parts.end()) return fail(FA_ERR_ARG, "part %d not defined", part_id);
+    *out = &it->second;
+    return FA_OK;
+}
+
+void free_part(fa_ctx* ctx, Part& p) {
+    for (size_t g = 0; g < p.slots.size(); ++g) {
+        DeviceGuard dg(ctx->gpu[g].dev);
+        if (p.slots[g]) (void)hipFree(p.slots[g]);
+        if (p.dout[g]) (void)hipFree(p.dout[g]);
+    }
+    p.slots.clear();
+    p.dout.clear();
+}
+
+int submit_impl(fa_ctx* ctx, int part_id, int slot, const void* src, float weight, bool pinned) {
+    Part* p;
+    int rc = check_part(ctx, part_id, &p);
+    if (rc) return rc;
+    if (slot < 0 || slot >= p->D) return fail(FA_ERR_ARG, "client slot %d out of range [0,%d)", slot, p->D);
+    if (!src && p->n) return fail(FA_ERR_ARG, "host_src is null");
+    const size_t si = dsize(p->in);
+    for (int g = 0; g < ctx->G; ++g) {
+        GpuRes& r = ctx->gpu[g];
+        DeviceGuard dg(r.dev);
+        const char* hs = static_cast<const char*>(src) + p->off[g] * si;
+        char* ds = p->slots[g] + (size_t)slot * p->cnt[g] * si;
+        size_t bytes = p->cnt[g] * si;
+        if (pinned) {
+            if (bytes) FA_HIP(hipMemcpyAsync(ds, hs, bytes, hipMemcpyHostToDevice, r.copy));
+            continue;
+        }
+        // Double-buffered staging: fill one pinned chunk while the other is in flight.
+        for (size_t o = 0; o < bytes; o += kStageBytes) {
+            const size_t b = std::min(kStageBytes, bytes - o);
+            const int i = r.stage_i;
+            r.stage_i ^= 1;
+            FA_HIP(hipEventSynchronize(r.stage_ev[i]));
+            std::memcpy(r.stage[i], hs + o, b);
+            FA_HIP(hipMemcpyAsync(ds + o, r.stage[i], b, hipMemcpyHostToDevice, r.copy));
+            FA_HIP(hipEventRecord(r.stage_ev[i], r.copy));
+        }
+    }
+    if (!p->submitted[slot]) {
+        p->submitted[slot] = 1;
+        ++p->n_submitted;
+    }
+    p->w[slot] = weight;
+    p->last_slot = slot;
+    return FA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fa_version(void) { return FA_ABI_VERSION; }
+
+const char* fa_last_error(void) { return g_err.c_str(); }
+
+int fa_device_count(int* out) {
+    g_err.clear();
+    if (!out) return fail(FA_ERR_ARG, "out is null");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *out = n;
+    return FA_OK;
+}
+
+int fa_set_tuning(const fa_tuning* t) {
+    g_err.clear();
+    if (!t) return fail(FA_ERR_ARG, "tuning is null");
+    fa::Tuning nt = g_tuning;
+    if (t->block) {
+        if (t->block != 64 && t->block != 128 && t->block != 256) return fail(FA_ERR_ARG, "block must be 64/128/256");
+        nt.block = t->block;
+    }
+    if (t->max_blocks) nt.max_blocks = t->max_blocks < 0 ? 0 : t->max_blocks;
+    if (t->unroll) {
+        if (t->unroll != 4 && t->unroll != 8 && t->unroll != 16) return fail(FA_ERR_ARG, "unroll must be 4/8/16");
+        nt.unroll = t->unroll;
+    }
+    if (t->nontemporal >= 0) nt.nontemporal = t->nontemporal ? 1 : 0;
+    g_tuning = nt;
+    return FA_OK;
+}
+
+int fa_get_tuning(fa_tuning* t) {
+    g_err.clear();
+    if (!t) return fail(FA_ERR_ARG, "tuning is null");
+    t->block = g_tuning.block;
+    t->max_blocks = g_tuning.max_blocks;
+    t->unroll = g_tuning.unroll;
+    t->nontemporal = g_tuning.nontemporal;
+    return FA_OK;
+}
+
+int fa_create(fa_ctx** out, int n_gpus, int flags) {
+    g_err.clear();
+    if (!out) return fail(FA_ERR_ARG, "out is null");
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return fail(FA_ERR_NODEV, "no HIP device visible");
+    if (n_gpus < 1 || n_gpus > count) return fail(FA_ERR_ARG, "n_gpus=%d but %d device(s) visible", n_gpus, count);
+    if (n_gpus > 1 && !(flags & FA_SHARD_RANGE)) return fail(FA_ERR_ARG, "n_gpus > 1 needs FA_SHARD_RANGE");
+    for (int g = 0; g < n_gpus; ++g) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, g) != hipSuccess) return fail(FA_ERR_NODEV, "device %d unreadable", g);
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+            return fail(FA_ERR_NODEV, "device %d is %s; libfa.so is built for gfx950 only", g, prop.gcnArchName);
+    }
+    fa_ctx* ctx = new fa_ctx();
+    ctx->G = n_gpus;
+    ctx->flags = flags;
+    ctx->gpu.resize(n_gpus);
+    for (int g = 0; g < n_gpus; ++g) {
+        GpuRes& r = ctx->gpu[g];
+        r.dev = g;
+        DeviceGuard dg(g);
+        bool ok = hipStreamCreateWithFlags(&r.compute, hipStreamNonBlocking) == hipSuccess &&
+                  hipStreamCreateWithFlags(&r.copy, hipStreamNonBlocking) == hipSuccess;
+        for (int i = 0; ok && i < 2; ++i)
+            ok = hipHostMalloc((void**)&r.stage[i], kStageBytes, hipHostMallocDefault) == hipSuccess &&
+                 hipEventCreateWithFlags(&r.stage_ev[i], hipEventDisableTiming) == hipSuccess;
+        if (!ok) {
+            fa_destroy(ctx);
+            return fail(FA_ERR_NOMEM, "stream/staging setup failed on device %d", g);
+        }
+    }
+    *out = ctx;
+    return FA_OK;
+}
+
+void fa_destroy(fa_ctx* ctx) {
+    if (!ctx) return;
+    for (auto& kv : ctx->parts) free_part(ctx, kv.second);
+    for (auto& r : ctx->gpu) {
+        DeviceGuard dg(r.dev);
+        if (r.compute) (void)hipStreamSynchronize(r.compute);
+        if (r.copy) (void)hipStreamSynchronize(r.copy);
+        for (int i = 0; i < 2; ++i) {
+            if (r.stage[i]) (void)hipHostFree(r.stage[i]);
+            if (r.stage_ev[i]) (void)hipEventDestroy(r.stage_ev[i]);
+        }
+        if (r.scratch) (void)hipFree(r.scratch);
+        if (r.compute) (void)hipStreamDestroy(r.compute);
+        if (r.copy) (void)hipStreamDestroy(r.copy);
+    }
+    delete ctx;
+}
+
+int fa_bucket_define(fa_ctx* ctx, int part_id, size_t n_elems, fa_dtype in, fa_dtype out, int n_clients,
+                     fa_mode mode) {
+    g_err.clear();
+    if (!ctx) return fail(FA_ERR_ARG, "ctx is null");
+    if (!dvalid(in) || !dvalid(out)) return fail(FA_ERR_ARG, "bad dtype");
+    if (mode != FA_FEDAVG && mode != FA_LITERAL) return fail(FA_ERR_ARG, "bad mode");
+    if (n_clients < 1) return fail(FA_ERR_ARG, "n_clients must be >= 1");
+    auto it = ctx->parts.find(part_id);
+    if (it != ctx->parts.end()) {
+        free_part(ctx, it->second);
+        ctx->parts.erase(it);
+    }
+    Part p;
+    p.n = n_elems;
+    p.in = in;
+    p.out = out;
+    p.D = n_clients;
+    p.mode = mode;
+    p.divisor = ctx->divisor;
+    p.w.assign(n_clients, 0.0f);
+    p.submitted.assign(n_clients, 0);
+    // Range shards: multiples of 64 elements so every shard keeps 16-B phase 0.
+    const size_t G = (size_t)ctx->G, unit = 64;
+    size_t per = ((n_elems + G - 1) / G + unit - 1) / unit * unit;
+    for (size_t g = 0; g < G; ++g) {
+        size_t lo = std::min(n_elems, g * per), hi = std::min(n_elems, lo + per);
+        p.off.push_back(lo);
+        p.cnt.push_back(hi - lo);
+    }
+    p.slots.assign(G, nullptr);
+    p.dout.assign(G, nullptr);
+    for (size_t g = 0; g < G; ++g) {
+        DeviceGuard dg(ctx->gpu[g].dev);
+        size_t sb = std::max<size_t>(1, (size_t)n_clients * p.cnt[g] * dsize(in));
+        size_t ob = std::max<size_t>(1, p.cnt[g] * dsize(out));
+        if (hipMalloc((void**)&p.slots[g], sb) != hipSuccess || hipMalloc(&p.dout[g], ob) != hipSuccess) {
+            free_part(ctx, p);
+            return fail(FA_ERR_NOMEM, "device alloc for part %d (%zu B slots) failed on GPU %zu", part_id, sb, g);
+        }
+    }
+    ctx->parts.emplace(part_id, std::move(p));
+    return FA_OK;
+}
+
+int fa_set_literal_divisor(fa_ctx* ctx, int part_id, float divisor) {
+    g_err.clear();
+    if (!ctx) return fail(FA_ERR_ARG, "ctx is null");
+    if (!(divisor != 0.0f)) return fail(FA_ERR_ARG, "divisor must be non-zero");
+    if (part_id < 0) {
+        ctx->divisor = divisor;
+        return FA_OK;
+    }
+    Part* p;
+    int rc = check_part(ctx, part_id, &p);
+    if (rc) return rc;
+    p->divisor = divisor;
+    return FA_OK;
+}
+
+int fa_submit(fa_ctx* ctx, int part_id, int client_slot, const void* host_src, float weight) {
+    g_err.clear();
+    return submit_impl(ctx, part_id, client_slot, host_src, weight, false);
+}
+
+int fa_submit_pinned(fa_ctx* ctx, int part_id, int client_slot, const void* host_src, float weight) {
+    g_err.clear();
+    return submit_impl(ctx, part_id, client_slot, host_src, weight, true);
+}
+
+int fa_finalize(fa_ctx* ctx, int part_id, void* host_dst) {
+    g_err.clear();
+    Part* p;
+    int rc = check_part(ctx, part_id, &p);
+    if (rc) return rc;
+    if (p->mode == FA_FEDAVG && p->n_submitted != p->D)
+        return fail(FA_ERR_STATE, "part %d: %d of %d clients submitted", part_id, p->n_submitted, p->D);
+    if (p->n_submitted == 0) return fail(FA_ERR_STATE, "part %d: nothing submitted", part_id);
+    if (!host_dst && p->n) return fail(FA_ERR_ARG, "host_dst is null");
+    const size_t si = dsize(p->in), so = dsize(p->out);
+    std::vector<const void*> ptrs(p->D);
+    for (int g = 0; g < ctx->G; ++g) {
+        GpuRes& r = ctx->gpu[g];
+        DeviceGuard dg(r.dev);
+        hipEvent_t ev;
+        FA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        FA_HIP(hipEventRecord(ev, r.copy));
+        FA_HIP(hipStreamWaitEvent(r.compute, ev, 0));
+        FA_HIP(hipEventDestroy(ev));
+        for (int k = 0; k < p->D; ++k) ptrs[k] = p->slots[g] + (size_t)k * p->cnt[g] * si;
+        if (p->mode == FA_LITERAL) {
+            const void* last = ptrs[p->last_slot];
+            rc = reduce_on(ctx, g, &last, p->w.data(), 1, p->cnt[g], p->in, p->dout[g], p->out, p->mode, p->divisor,
+                           nullptr, r.compute);
+        } else {
+            rc = reduce_on(ctx, g, ptrs.data(), p->w.data(), p->D, p->cnt[g], p->in, p->dout[g], p->out, p->mode,
+                           p->divisor, nullptr, r.compute);
+        }
+        if (rc) return rc;
+    }
+    // D2H through the pinned chunks (the result leaves for new_message()).
+    for (int g = 0; g < ctx->G; ++g) {
+        GpuRes& r = ctx->gpu[g];
+        DeviceGuard dg(r.dev);
+        const char* src = static_cast<const char*>(p->dout[g]);
+        char* dst = static_cast<char*>(host_dst) + p->off[g] * so;
+        const size_t bytes = p->cnt[g] * so;
+        for (size_t o = 0; o < bytes; o += kStageBytes) {
+            const size_t b = std::min(kStageBytes, bytes - o);
+            FA_HIP(hipMemcpyAsync(r.stage[0], src + o, b, hipMemcpyDeviceToHost, r.compute));
+            FA_HIP(hipStreamSynchronize(r.compute));
+            std::memcpy(dst + o, r.stage[0], b);
+        }
+        FA_HIP(hipStreamSynchronize(r.compute));
+    }
+    std::fill(p->submitted.begin(), p->submitted.end(), 0);
+    p->n_submitted = 0;
+    p->last_slot = -1;
+    return FA_OK;
+}
+
+int fa_reduce_device(fa_ctx* ctx, int gpu, const void* const* d_clients, const float* h_weights, int D, size_t n,
+                     fa_dtype in, void* d_out, fa_dtype out, fa_mode mode, const float* d_init, void* hip_stream) {
+    g_err.clear();
+    if (!d_clients || !h_weights) return fail(FA_ERR_ARG, "client or weight array is null");
+    if (D < 1) return fail(FA_ERR_ARG, "D must be >= 1");
+    if (!dvalid(in) || !dvalid(out)) return fail(FA_ERR_ARG, "bad dtype");
+    if (mode != FA_FEDAVG && mode != FA_LITERAL) return fail(FA_ERR_ARG, "bad mode");
+    if (ctx && (gpu < 0 || gpu >= ctx->G)) return fail(FA_ERR_ARG, "gpu %d out of range", gpu);
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    int dev = ctx ? ctx->gpu[gpu].dev : gpu;
+    if (!s && ctx) s = ctx->gpu[gpu].compute;
+    DeviceGuard dg(dev);
+    return reduce_on(ctx, ctx ? gpu : 0, d_clients, h_weights, D, n, in, d_out, out, mode,
+                     ctx ? ctx->divisor : FA_DEFAULT_DIVISOR, d_init, s);
+}
+
+int fa_fill_uniform(void* d_dst, size_t n, fa_dtype dt, uint64_t seed, uint32_t client, uint64_t idx0,
+                    void* hip_stream) {
+    g_err.clear();
+    if (!dvalid(dt)) return fail(FA_ERR_ARG, "bad dtype");
+    if (n == 0) return FA_OK;
+    if (!d_dst) return fail(FA_ERR_ARG, "dst is null");
+    FA_HIP(fa::launch_fill(d_dst, (int64_t)n, dt, seed, client, idx0, static_cast<hipStream_t>(hip_stream)));
+    return FA_OK;
+}
+
+}  // extern "C"

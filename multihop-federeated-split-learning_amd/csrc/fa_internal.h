@@ -1,0 +1,33 @@
+// fa_internal.h -- shared declarations between the kernel TU and the C-ABI TU.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fedavg/fa.h"
+
+namespace fa {
+
+// Clients per launch.  Pointers + weights travel in the kernel-argument segment
+// (768 B), read with scalar loads; more clients continue the chain in another pass.
+constexpr int kMaxClients = 64;
+
+struct ClientTable {
+    const void* src[kMaxClients];
+    float w[kMaxClients];
+};
+
+struct Tuning {
+    int block;       // threads per workgroup: 64, 128 or 256
+    int max_blocks;  // grid cap (grid-stride beyond it), <= 0: uncapped
+    int unroll;      // clients per load group: 4, 8, 16
+    int nontemporal; // nt loads/stores
+};
+
+hipError_t launch_chain(const ClientTable& t, int nc, fa_dtype in, fa_dtype out, const float* init, void* dst,
+                        int64_t head, int64_t nvec, int64_t n, bool vector_ok, const Tuning& tu, hipStream_t s);
+hipError_t launch_literal(const void* x, fa_dtype in, void* dst, fa_dtype out, float divisor, int64_t head,
+                          int64_t nvec, int64_t n, bool vector_ok, const Tuning& tu, hipStream_t s);
+hipError_t launch_fill(void* dst, int64_t n, fa_dtype dt, uint64_t seed, uint32_t client, uint64_t idx0,
+                       hipStream_t s);
+
+}  // namespace fa

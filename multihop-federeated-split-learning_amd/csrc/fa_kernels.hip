@@ -1,0 +1,348 @@
+// fa_kernels.hip -- CDNA4 (gfx950) kernels of the FedAvg aggregation path.
+//
+// The reduction replaces the per-parameter loop of the reference aggregator
+// (pipeline_simulation/aggregator.cpp:72-88 and :126-142).  It is pure
+// element-wise, HBM-bound work: per element, D client reads and one write, two
+// flops per client.  No MFMA, no LDS reuse to exploit -- what matters is the
+// number of 16-byte loads in flight per CU.
+//
+// Layout: each client bucket is one contiguous array in HBM (the flattened
+// named_parameters() of a model part).  A wave reads 1 KiB contiguous from U
+// client buckets (16 B per lane, one global_load_dwordx4 each), then runs the
+// ordered FMA chain acc = fma(x_k, w_k, acc) in client order for the 4 (f32)
+// or 8 (bf16) elements it owns, and writes the result once.  Client pointers
+// and weights sit in the kernel-argument segment (scalar loads, uniform per
+// wave); more than kMaxClients clients are handled by further passes that
+// continue the chain from the fp32 accumulator (bit-identical to one chain).
+//
+// Numerics follow oracle/fa_oracle.c exactly: fmaf chain from +0, exact bf16
+// widening, one round-to-nearest-even at the end; literal mode uses IEEE
+// division (hipcc's default correctly rounded f32 divide).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fa_internal.h"
+
+namespace fa {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// ---------------------------------------------------------------- helpers
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(const void* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    else return *reinterpret_cast<const u32x4*>(p);
+}
+template <bool NT>
+__device__ __forceinline__ void st16(void* p, u32x4 v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+    else *reinterpret_cast<u32x4*>(p) = v;
+}
+template <bool NT>
+__device__ __forceinline__ void st8(void* p, u32x2 v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x2*>(p));
+    else *reinterpret_cast<u32x2*>(p) = v;
+}
+
+__device__ __forceinline__ float bf16_to_f32(uint32_t h) { return __uint_as_float(h << 16); }
+
+// Same integer rounding as oracle fa_oracle_f32_to_bf16 (NaN kept a quiet NaN).
+__device__ __forceinline__ uint32_t f32_to_bf16(float f) {
+    uint32_t u = __float_as_uint(f);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40u;
+    return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+
+// Element-type traits: a lane owns 16 bytes of every input bucket.
+template <typename T> struct In;
+template <> struct In<float> {
+    static constexpr int kVec = 4;
+    __device__ static __forceinline__ void widen(u32x4 r, float* x) {
+        x[0] = __uint_as_float(r.x); x[1] = __uint_as_float(r.y);
+        x[2] = __uint_as_float(r.z); x[3] = __uint_as_float(r.w);
+    }
+    __device__ static __forceinline__ float scalar(const void* p, int64_t i) {
+        return reinterpret_cast<const float*>(p)[i];
+    }
+};
+template <> struct In<uint16_t> {
+    static constexpr int kVec = 8;
+    __device__ static __forceinline__ void widen(u32x4 r, float* x) {
+        x[0] = __uint_as_float(r.x << 16); x[1] = __uint_as_float(r.x & 0xffff0000u);
+        x[2] = __uint_as_float(r.y << 16); x[3] = __uint_as_float(r.y & 0xffff0000u);
+        x[4] = __uint_as_float(r.z << 16); x[5] = __uint_as_float(r.z & 0xffff0000u);
+        x[6] = __uint_as_float(r.w << 16); x[7] = __uint_as_float(r.w & 0xffff0000u);
+    }
+    __device__ static __forceinline__ float scalar(const void* p, int64_t i) {
+        return bf16_to_f32(reinterpret_cast<const uint16_t*>(p)[i]);
+    }
+};
+
+template <typename T> struct Out;
+template <> struct Out<float> {
+    template <int V, bool NT>
+    __device__ static __forceinline__ void store(void* base, int64_t e, const float* a) {
+        float* p = reinterpret_cast<float*>(base) + e;
+#pragma unroll
+        for (int j = 0; j < V; j += 4)
+            st16<NT>(p + j, u32x4{__float_as_uint(a[j]), __float_as_uint(a[j + 1]), __float_as_uint(a[j + 2]),
+                                  __float_as_uint(a[j + 3])});
+    }
+    __device__ static __forceinline__ void scalar(void* base, int64_t i, float a) {
+        reinterpret_cast<float*>(base)[i] = a;
+    }
+};
+template <> struct Out<uint16_t> {
+    template <int V, bool NT>
+    __device__ static __forceinline__ void store(void* base, int64_t e, const float* a) {
+        uint16_t* p = reinterpret_cast<uint16_t*>(base) + e;
+        if constexpr (V == 8) {
+            st16<NT>(p, u32x4{f32_to_bf16(a[0]) | (f32_to_bf16(a[1]) << 16), f32_to_bf16(a[2]) | (f32_to_bf16(a[3]) << 16),
+                              f32_to_bf16(a[4]) | (f32_to_bf16(a[5]) << 16), f32_to_bf16(a[6]) | (f32_to_bf16(a[7]) << 16)});
+        } else {
+            st8<NT>(p, u32x2{f32_to_bf16(a[0]) | (f32_to_bf16(a[1]) << 16), f32_to_bf16(a[2]) | (f32_to_bf16(a[3]) << 16)});
+        }
+    }
+    __device__ static __forceinline__ void scalar(void* base, int64_t i, float a) {
+        reinterpret_cast<uint16_t*>(base)[i] = (uint16_t)f32_to_bf16(a);
+    }
+};
+
+// ---------------------------------------------------------------- FedAvg chain
+
+// Scalar elements [0, head) and [tail0, n): handled by the first workgroup.
+template <typename IN, typename OUT, bool INIT>
+__device__ __forceinline__ void chain_scalar_edges(const ClientTable& t, int nc, const float* init, void* out,
+                                                   int64_t head, int64_t tail0, int64_t n) {
+    if (blockIdx.x != 0) return;
+    const int64_t n_tail = n - tail0;
+    for (int64_t s = threadIdx.x; s < head + n_tail; s += blockDim.x) {
+        const int64_t i = s < head ? s : tail0 + (s - head);
+        float acc = INIT ? init[i] : 0.0f;
+        for (int k = 0; k < nc; ++k) acc = __builtin_fmaf(In<IN>::scalar(t.src[k], i), t.w[k], acc);
+        Out<OUT>::scalar(out, i, acc);
+    }
+}
+
+// Vector body over nvec lane-vectors starting at element `head`.
+template <typename IN, typename OUT, int U, bool NT, bool INIT>
+__global__ __launch_bounds__(256) void fedavg_chain_kernel(const ClientTable t, int nc, const float* init, void* out,
+                                                           int64_t head, int64_t nvec, int64_t n) {
+    constexpr int V = In<IN>::kVec;
+    chain_scalar_edges<IN, OUT, INIT>(t, nc, init, out, head, head + nvec * V, n);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+        const int64_t e = head + v * V;  // first element owned by this lane
+        float acc[V];
+        if constexpr (INIT) {
+#pragma unroll
+            for (int j = 0; j < V; j += 4) {
+                u32x4 r = ld16<NT>(init + e + j);
+                acc[j] = __uint_as_float(r.x); acc[j + 1] = __uint_as_float(r.y);
+                acc[j + 2] = __uint_as_float(r.z); acc[j + 3] = __uint_as_float(r.w);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < V; ++j) acc[j] = 0.0f;
+        }
+        int k = 0;
+        for (; k + U <= nc; k += U) {
+            u32x4 raw[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) raw[u] = ld16<NT>(reinterpret_cast<const IN*>(t.src[k + u]) + e);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                float x[V];
+                In<IN>::widen(raw[u], x);
+                const float w = t.w[k + u];
+#pragma unroll
+                for (int j = 0; j < V; ++j) acc[j] = __builtin_fmaf(x[j], w, acc[j]);
+            }
+        }
+        for (; k < nc; ++k) {
+            float x[V];
+            In<IN>::widen(ld16<NT>(reinterpret_cast<const IN*>(t.src[k]) + e), x);
+            const float w = t.w[k];
+#pragma unroll
+            for (int j = 0; j < V; ++j) acc[j] = __builtin_fmaf(x[j], w, acc[j]);
+        }
+        Out<OUT>::template store<V, NT>(out, e, acc);
+    }
+}
+
+// Fully general path (pointers whose 16-byte phases differ): one element per lane.
+template <typename IN, typename OUT, bool INIT>
+__global__ __launch_bounds__(256) void fedavg_chain_scalar_kernel(const ClientTable t, int nc, const float* init,
+                                                                  void* out, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        float acc = INIT ? init[i] : 0.0f;
+        for (int k = 0; k < nc; ++k) acc = __builtin_fmaf(In<IN>::scalar(t.src[k], i), t.w[k], acc);
+        Out<OUT>::scalar(out, i, acc);
+    }
+}
+
+// ---------------------------------------------------------------- literal mode
+
+template <typename IN, typename OUT, bool NT>
+__global__ __launch_bounds__(256) void literal_kernel(const void* x, void* out, float divisor, int64_t head,
+                                                      int64_t nvec, int64_t n) {
+    constexpr int V = In<IN>::kVec;
+    if (blockIdx.x == 0) {
+        const int64_t tail0 = head + nvec * V, n_tail = n - tail0;
+        for (int64_t s = threadIdx.x; s < head + n_tail; s += blockDim.x) {
+            const int64_t i = s < head ? s : tail0 + (s - head);
+            const float xi = In<IN>::scalar(x, i);
+            Out<OUT>::scalar(out, i, (xi + xi) / divisor);
+        }
+    }
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+        const int64_t e = head + v * V;
+        float xv[V], r[V];
+        In<IN>::widen(ld16<NT>(reinterpret_cast<const IN*>(x) + e), xv);
+#pragma unroll
+        for (int j = 0; j < V; ++j) r[j] = (xv[j] + xv[j]) / divisor;
+        Out<OUT>::template store<V, NT>(out, e, r);
+    }
+}
+
+template <typename IN, typename OUT>
+__global__ __launch_bounds__(256) void literal_scalar_kernel(const void* x, void* out, float divisor, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const float xi = In<IN>::scalar(x, i);
+        Out<OUT>::scalar(out, i, (xi + xi) / divisor);
+    }
+}
+
+// ---------------------------------------------------------------- generator
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ float gen_value(uint64_t seed, uint32_t client, uint64_t idx) {
+    const uint64_t h = splitmix64(seed ^ ((uint64_t)client << 40) ^ idx);
+    return (float)(uint32_t)(h >> 40) * 0x1p-23f - 1.0f;
+}
+
+template <typename OUT>
+__global__ __launch_bounds__(256) void fill_kernel(void* dst, int64_t n, uint64_t seed, uint32_t client,
+                                                   uint64_t idx0) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        Out<OUT>::scalar(dst, i, gen_value(seed, client, idx0 + (uint64_t)i));
+}
+
+// ---------------------------------------------------------------- launchers
+
+namespace {
+
+inline int64_t grid_for(int64_t work, const Tuning& tu) {
+    int64_t g = (work + tu.block - 1) / tu.block;
+    if (g < 1) g = 1;
+    if (tu.max_blocks > 0 && g > tu.max_blocks) g = tu.max_blocks;
+    return g;
+}
+
+template <typename IN, typename OUT, int U, bool NT>
+hipError_t launch_chain_u(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
+                          int64_t n, const Tuning& tu, hipStream_t s) {
+    const int64_t g = grid_for(nvec > 0 ? nvec : 1, tu);
+    if (init)
+        hipLaunchKernelGGL((fedavg_chain_kernel<IN, OUT, U, NT, true>), dim3((unsigned)g), dim3(tu.block), 0, s, t,
+                           nc, init, out, head, nvec, n);
+    else
+        hipLaunchKernelGGL((fedavg_chain_kernel<IN, OUT, U, NT, false>), dim3((unsigned)g), dim3(tu.block), 0, s, t,
+                           nc, init, out, head, nvec, n);
+    return hipGetLastError();
+}
+
+template <typename IN, typename OUT, bool NT>
+hipError_t launch_chain_nt(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
+                           int64_t n, const Tuning& tu, hipStream_t s) {
+    switch (tu.unroll) {
+        case 4: return launch_chain_u<IN, OUT, 4, NT>(t, nc, init, out, head, nvec, n, tu, s);
+        case 16: return launch_chain_u<IN, OUT, 16, NT>(t, nc, init, out, head, nvec, n, tu, s);
+        default: return launch_chain_u<IN, OUT, 8, NT>(t, nc, init, out, head, nvec, n, tu, s);
+    }
+}
+
+template <typename IN, typename OUT>
+hipError_t launch_chain_t(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
+                          int64_t n, bool vector_ok, const Tuning& tu, hipStream_t s) {
+    if (!vector_ok) {
+        const int64_t g = grid_for(n, tu);
+        if (init)
+            hipLaunchKernelGGL((fedavg_chain_scalar_kernel<IN, OUT, true>), dim3((unsigned)g), dim3(tu.block), 0, s,
+                               t, nc, init, out, n);
+        else
+            hipLaunchKernelGGL((fedavg_chain_scalar_kernel<IN, OUT, false>), dim3((unsigned)g), dim3(tu.block), 0,
+                               s, t, nc, init, out, n);
+        return hipGetLastError();
+    }
+    if (tu.nontemporal) return launch_chain_nt<IN, OUT, true>(t, nc, init, out, head, nvec, n, tu, s);
+    return launch_chain_nt<IN, OUT, false>(t, nc, init, out, head, nvec, n, tu, s);
+}
+
+}  // namespace
+
+hipError_t launch_chain(const ClientTable& t, int nc, fa_dtype in, fa_dtype outdt, const float* init, void* out,
+                        int64_t head, int64_t nvec, int64_t n, bool vector_ok, const Tuning& tu, hipStream_t s) {
+    if (in == FA_F32 && outdt == FA_F32)
+        return launch_chain_t<float, float>(t, nc, init, out, head, nvec, n, vector_ok, tu, s);
+    if (in == FA_F32 && outdt == FA_BF16)
+        return launch_chain_t<float, uint16_t>(t, nc, init, out, head, nvec, n, vector_ok, tu, s);
+    if (in == FA_BF16 && outdt == FA_F32)
+        return launch_chain_t<uint16_t, float>(t, nc, init, out, head, nvec, n, vector_ok, tu, s);
+    return launch_chain_t<uint16_t, uint16_t>(t, nc, init, out, head, nvec, n, vector_ok, tu, s);
+}
+
+namespace {
+template <typename IN, typename OUT>
+hipError_t launch_literal_t(const void* x, void* out, float divisor, int64_t head, int64_t nvec, int64_t n,
+                            bool vector_ok, const Tuning& tu, hipStream_t s) {
+    if (!vector_ok) {
+        hipLaunchKernelGGL((literal_scalar_kernel<IN, OUT>), dim3((unsigned)grid_for(n, tu)), dim3(tu.block), 0, s,
+                           x, out, divisor, n);
+    } else if (tu.nontemporal) {
+        hipLaunchKernelGGL((literal_kernel<IN, OUT, true>), dim3((unsigned)grid_for(nvec > 0 ? nvec : 1, tu)),
+                           dim3(tu.block), 0, s, x, out, divisor, head, nvec, n);
+    } else {
+        hipLaunchKernelGGL((literal_kernel<IN, OUT, false>), dim3((unsigned)grid_for(nvec > 0 ? nvec : 1, tu)),
+                           dim3(tu.block), 0, s, x, out, divisor, head, nvec, n);
+    }
+    return hipGetLastError();
+}
+}  // namespace
+
+hipError_t launch_literal(const void* x, fa_dtype in, void* out, fa_dtype outdt, float divisor, int64_t head,
+                          int64_t nvec, int64_t n, bool vector_ok, const Tuning& tu, hipStream_t s) {
+    if (in == FA_F32 && outdt == FA_F32)
+        return launch_literal_t<float, float>(x, out, divisor, head, nvec, n, vector_ok, tu, s);
+    if (in == FA_F32 && outdt == FA_BF16)
+        return launch_literal_t<float, uint16_t>(x, out, divisor, head, nvec, n, vector_ok, tu, s);
+    if (in == FA_BF16 && outdt == FA_F32)
+        return launch_literal_t<uint16_t, float>(x, out, divisor, head, nvec, n, vector_ok, tu, s);
+    return launch_literal_t<uint16_t, uint16_t>(x, out, divisor, head, nvec, n, vector_ok, tu, s);
+}
+
+hipError_t launch_fill(void* dst, int64_t n, fa_dtype dt, uint64_t seed, uint32_t client, uint64_t idx0,
+                       hipStream_t s) {
+    Tuning tu{256, 8192, 8, 0};
+    const int64_t g = grid_for(n, tu);
+    if (dt == FA_F32)
+        hipLaunchKernelGGL((fill_kernel<float>), dim3((unsigned)g), dim3(256), 0, s, dst, n, seed, client, idx0);
+    else
+        hipLaunchKernelGGL((fill_kernel<uint16_t>), dim3((unsigned)g), dim3(256), 0, s, dst, n, seed, client, idx0);
+    return hipGetLastError();
+}
+
+}  // namespace fa

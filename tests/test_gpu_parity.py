@@ -1,0 +1,309 @@
+"""GPU parity: libfa.so kernels vs the oracle (bit-exact) through the C ABI.
+
+Inputs are produced on the device by fa_fill_uniform and on the host by the
+oracle's generator (the two are checked equal first), so both sides reduce the
+same bytes.  Small and ragged sizes are compared whole; the reference configs
+(tests/golden) are compared at full size against the reference-generated
+fixtures (file or SHA-256 + sampled bits); the north-star size is checked by
+sampled elements plus a split-chain consistency property.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def to_np(t, bf16):
+    a = t.cpu().numpy()
+    return a.view(np.uint16) if bf16 else a
+
+
+def dev_buf(torch, n, bf16, offset=0):
+    """Device buffer of n elements starting `offset` elements into a fresh allocation."""
+    base = torch.empty(n + 16, dtype=torch.int16 if bf16 else torch.float32, device="cuda")
+    return base[offset:offset + n]
+
+
+def filled(fa, torch, n, bf16, seed, client, offset=0):
+    t = dev_buf(torch, n, bf16, offset)
+    fa.fill_uniform(t, n, fa.BF16 if bf16 else fa.F32, seed, client)
+    return t
+
+
+def run_fedavg(fa, torch, clients, w, n, bf16_in, bf16_out, init=None, out_offset=0):
+    out = dev_buf(torch, n, bf16_out, out_offset)
+    fa.reduce_device(clients, w, n, fa.BF16 if bf16_in else fa.F32, out, fa.BF16 if bf16_out else fa.F32,
+                     fa.FEDAVG, init=init)
+    torch.cuda.synchronize()
+    return to_np(out, bf16_out)
+
+
+def host_clients(O, seed, D, n, bf16):
+    xs = [O.gen(seed, k, n) for k in range(D)]
+    return [O.f32_to_bf16(x) for x in xs] if bf16 else xs
+
+
+def assert_bits(got, ref):
+    ut = np.uint16 if got.dtype == np.uint16 else np.uint32
+    bad = np.flatnonzero(got.view(ut) != ref.view(ut))
+    assert bad.size == 0, "%d/%d mismatches, first at %s: got %s ref %s" % (
+        bad.size, got.size, bad[:4], got[bad[:4]], ref[bad[:4]])
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_fill_matches_oracle_generator(fa, O, torch_gpu, bf16):
+    torch = torch_gpu
+    for n, client, idx0 in [(1, 0, 0), (4099, 5, 17), (1 << 20, 31, 1 << 33)]:
+        t = dev_buf(torch, n, bf16)
+        fa.fill_uniform(t, n, fa.BF16 if bf16 else fa.F32, 0x5EED, client, idx0)
+        assert_bits(to_np(t, bf16), O.gen(0x5EED, client, n, idx0=idx0, dtype="bf16" if bf16 else "f32"))
+
+
+@pytest.mark.parametrize("D", [1, 2, 3, 8, 33, 64, 65, 130])
+def test_fedavg_f32_bitexact(fa, O, torch_gpu, D):
+    torch = torch_gpu
+    w = O.weights(D)
+    for n in [1, 3, 5, 64, 1000, 4097, 262147]:
+        xs = host_clients(O, 100 + n, D, n, False)
+        clients = [filled(fa, torch, n, False, 100 + n, k) for k in range(D)]
+        assert_bits(run_fedavg(fa, torch, clients, w, n, False, False), O.fedavg(xs, w))
+
+
+def test_fedavg_zero_elements_is_noop(fa, O, torch_gpu):
+    torch = torch_gpu
+    c = [dev_buf(torch, 4, False)]
+    fa.reduce_device(c, [1.0], 0, fa.F32, dev_buf(torch, 4, False), fa.F32)
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("offsets", [(1, 1, 1, 1), (2, 2, 2, 2), (3, 3, 3, 3), (0, 1, 2, 3), (3, 0, 0, 1)])
+def test_fedavg_misaligned_pointers(fa, O, torch_gpu, offsets):
+    """Same 16-B phase -> vector body + scalar head; mixed phases -> general path. Same bits either way."""
+    torch = torch_gpu
+    n, D = 100_003, len(offsets) - 1
+    w = O.weights(D)
+    xs = host_clients(O, 77, D, n, False)
+    clients = [filled(fa, torch, n, False, 77, k, offset=offsets[k]) for k in range(D)]
+    assert_bits(run_fedavg(fa, torch, clients, w, n, False, False, out_offset=offsets[-1]), O.fedavg(xs, w))
+
+
+def test_fedavg_init_continues_the_chain(fa, O, torch_gpu):
+    """Clients split over two launches with d_init == one ordered chain (used for multi-GPU chains)."""
+    torch = torch_gpu
+    n, D = 300_001, 10
+    w = O.weights(D)
+    xs = host_clients(O, 5, D, n, False)
+    clients = [filled(fa, torch, n, False, 5, k) for k in range(D)]
+    acc = dev_buf(torch, n, False)
+    fa.reduce_device(clients[:4], w[:4], n, fa.F32, acc, fa.F32)
+    out = run_fedavg(fa, torch, clients[4:], w[4:], n, False, False, init=acc)
+    assert_bits(out, O.fedavg(xs, w))
+
+
+@pytest.mark.parametrize("out_bf16", [False, True])
+@pytest.mark.parametrize("D", [1, 7, 32, 70])
+def test_fedavg_bf16_inputs(fa, O, torch_gpu, D, out_bf16):
+    torch = torch_gpu
+    n = 100_003
+    w = O.weights(D)
+    xs = host_clients(O, 9, D, n, True)
+    clients = [filled(fa, torch, n, True, 9, k) for k in range(D)]
+    ref = O.fedavg(xs, w, out_dtype="bf16" if out_bf16 else "f32")
+    if out_bf16 and D > 64:
+        ctx = fa.Aggregator(1)  # bf16 output across passes needs ctx scratch
+        out = dev_buf(torch, n, True)
+        fa.reduce_device(clients, w, n, fa.BF16, out, fa.BF16, ctx=ctx)
+        torch.cuda.synchronize()
+        assert_bits(to_np(out, True), ref)
+        ctx.close()
+    else:
+        assert_bits(run_fedavg(fa, torch, clients, w, n, True, out_bf16), ref)
+
+
+def test_fedavg_f32_in_bf16_out(fa, O, torch_gpu):
+    torch = torch_gpu
+    n, D = 65_537, 6
+    w = O.weights(D)
+    xs = host_clients(O, 3, D, n, False)
+    clients = [filled(fa, torch, n, False, 3, k) for k in range(D)]
+    ref = O.f32_to_bf16(O.fedavg(xs, w))
+    assert_bits(run_fedavg(fa, torch, clients, w, n, False, True), ref)
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_literal_mode(fa, O, torch_gpu, bf16):
+    """aggregator.cpp:63-88 semantics: only the last client survives, fl(fl(2x)/1000)."""
+    torch = torch_gpu
+    n, D = 70_001, 4
+    xs = host_clients(O, 21, D, n, bf16)
+    clients = [filled(fa, torch, n, bf16, 21, k, offset=1) for k in range(D)]
+    for out_bf16 in ([False, True] if bf16 else [False]):
+        out = dev_buf(torch, n, out_bf16, offset=1)
+        fa.reduce_device(clients, np.zeros(D), n, fa.BF16 if bf16 else fa.F32, out,
+                         fa.BF16 if out_bf16 else fa.F32, fa.LITERAL)
+        torch.cuda.synchronize()
+        assert_bits(to_np(out, out_bf16), O.literal(xs[-1], out_dtype="bf16" if out_bf16 else "f32"))
+
+
+@pytest.mark.parametrize("tuning", [dict(block=64, unroll=4, nontemporal=0), dict(block=128, unroll=16, nontemporal=1),
+                                    dict(block=256, unroll=8, nontemporal=0, max_blocks=7),
+                                    dict(block=256, unroll=16, nontemporal=1, max_blocks=1)])
+def test_tuning_variants_same_bits(fa, O, torch_gpu, tuning):
+    torch = torch_gpu
+    before = fa.get_tuning()
+    try:
+        fa.set_tuning(**tuning)
+        n, D = 200_003, 19
+        w = O.weights(D)
+        xs = host_clients(O, 8, D, n, False)
+        clients = [filled(fa, torch, n, False, 8, k) for k in range(D)]
+        assert_bits(run_fedavg(fa, torch, clients, w, n, False, False), O.fedavg(xs, w))
+    finally:
+        fa.set_tuning(**before)
+
+
+# ----------------------------------------------------------------- reference golden configs, full size
+
+CONFIGS = ["lenet5_c1", "resnet18_c2", "resnet101_c3", "vgg19_c4"]
+
+
+def check_golden(cfg, rec, got):
+    if "file" in rec:
+        ref = np.fromfile(os.path.join(GOLDEN, cfg, rec["file"]), dtype=got.dtype)
+        assert_bits(got, ref)
+    else:
+        idx = np.asarray(rec["sample_idx"])
+        bits = got.view(np.uint32 if got.dtype == np.float32 else np.uint16)[idx]
+        assert np.array_equal(bits, np.asarray(rec["sample_bits"], bits.dtype))
+        assert hashlib.sha256(got.tobytes()).hexdigest() == rec["sha256"]
+
+
+@pytest.mark.parametrize("cfg", CONFIGS)
+def test_reference_golden_on_gpu(fa, O, torch_gpu, cfg):
+    torch = torch_gpu
+    with open(os.path.join(GOLDEN, cfg, "manifest.json")) as f:
+        m = json.load(f)
+    D = m["D"]
+    w = O.weights(D)
+    for b in m["buckets"]:
+        n, s = b["numel"], b["bucket_seed"]
+        cf = [filled(fa, torch, n, False, s, k) for k in range(D)]
+        check_golden(cfg, b["outputs"]["fedavg.f32"], run_fedavg(fa, torch, cf, w, n, False, False))
+        out = dev_buf(torch, n, False)
+        fa.reduce_device(cf, w, n, fa.F32, out, fa.F32, fa.LITERAL)
+        torch.cuda.synchronize()
+        check_golden(cfg, b["outputs"]["literal.f32"], to_np(out, False))
+        del cf
+        cb = [filled(fa, torch, n, True, s, k) for k in range(D)]
+        check_golden(cfg, b["outputs"]["fedavg_bf16.bf16"], run_fedavg(fa, torch, cb, w, n, True, True))
+        check_golden(cfg, b["outputs"]["fedavg_bf16.f32"], run_fedavg(fa, torch, cb, w, n, True, False))
+        del cb
+
+
+def test_north_star_size_sampled_and_split_consistent(fa, O, torch_gpu):
+    """256 MiB fp32 x 32 clients: sampled elements vs the oracle, and a split chain == one chain."""
+    torch = torch_gpu
+    n, D = 64 << 20, 32
+    w = O.weights(D)
+    clients = [filled(fa, torch, n, False, 0x5EED, k) for k in range(D)]
+    out = dev_buf(torch, n, False)
+    fa.reduce_device(clients, w, n, fa.F32, out, fa.F32)
+    acc = dev_buf(torch, n, False)
+    fa.reduce_device(clients[:13], w[:13], n, fa.F32, acc, fa.F32)
+    fa.reduce_device(clients[13:], w[13:], n, fa.F32, acc, fa.F32, init=acc)
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int32), acc.view(torch.int32))
+    rng = np.random.default_rng(0)
+    idx = np.unique(np.concatenate([[0, 1, 2, 3, n - 4, n - 3, n - 2, n - 1], rng.integers(0, n, 2048)]))
+    got = out[torch.as_tensor(idx, device="cuda")].cpu().numpy()
+    assert_bits(got, O.fedavg_at(0x5EED, w, idx))
+
+
+# ----------------------------------------------------------------- aggregation context (host buckets)
+
+def test_context_fedavg_out_of_order_submits(fa, O, torch_gpu):
+    n, D = 1_000_003, 5
+    w = O.weights(D)
+    xs = host_clients(O, 44, D, n, False)
+    with fa.Aggregator(1) as agg:
+        agg.define(2, n, fa.F32, fa.F32, D, fa.FEDAVG)
+        for k in [3, 0, 4, 1, 2]:
+            agg.submit(2, k, xs[k], w[k])
+        assert_bits(agg.finalize(2), O.fedavg(xs, w))
+        # next round reuses the bucket
+        xs2 = host_clients(O, 45, D, n, False)
+        for k in range(D):
+            agg.submit(2, k, xs2[k], w[k])
+        assert_bits(agg.finalize(2), O.fedavg(xs2, w))
+
+
+def test_context_literal_takes_last_submitted(fa, O, torch_gpu):
+    n, D = 50_000, 3
+    xs = host_clients(O, 46, D, n, False)
+    with fa.Aggregator(1) as agg:
+        agg.define(1, n, fa.F32, fa.F32, D, fa.LITERAL)
+        for k in [2, 0, 1]:
+            agg.submit(1, k, xs[k])
+        assert_bits(agg.finalize(1), O.literal(xs[1]))
+        agg.set_divisor(7.0, part_id=1)
+        agg.submit(1, 2, xs[2])
+        assert_bits(agg.finalize(1), O.literal(xs[2], divisor=7.0))
+
+
+def test_context_large_bucket_multi_chunk_and_bf16(fa, O, torch_gpu):
+    n, D = 20_000_001, 3  # 80 MB per client: several pinned staging chunks
+    w = O.weights(D)
+    xs = host_clients(O, 47, D, n, True)
+    with fa.Aggregator(1) as agg:
+        agg.define(1, n, fa.BF16, fa.BF16, D, fa.FEDAVG)
+        for k in range(D):
+            agg.submit(1, k, xs[k], w[k])
+        assert_bits(agg.finalize(1), O.fedavg(xs, w, out_dtype="bf16", threads=8))
+
+
+def test_context_pinned_submit(fa, O, torch_gpu):
+    torch = torch_gpu
+    n, D = 333_333, 4
+    w = O.weights(D)
+    xs = host_clients(O, 48, D, n, False)
+    pinned = [torch.empty(n, dtype=torch.float32, pin_memory=True) for _ in range(D)]
+    for p, x in zip(pinned, xs):
+        p.numpy()[:] = x
+    with fa.Aggregator(1) as agg:
+        agg.define(1, n, fa.F32, fa.F32, D, fa.FEDAVG)
+        for k in range(D):
+            agg.submit(1, k, pinned[k].numpy(), w[k], pinned=True)
+        assert_bits(agg.finalize(1), O.fedavg(xs, w))
+
+
+def test_context_errors(fa, O, torch_gpu):
+    with fa.Aggregator(1) as agg:
+        agg.define(1, 1000, fa.F32, fa.F32, 3, fa.FEDAVG)
+        agg.submit(1, 0, np.zeros(1000, np.float32), 0.5)
+        with pytest.raises(fa.FaError) as e:
+            agg.finalize(1)
+        assert e.value.code == fa.ERR_STATE
+        with pytest.raises(fa.FaError) as e:
+            agg.submit(1, 3, np.zeros(1000, np.float32), 0.5)
+        assert e.value.code == fa.ERR_ARG
+        with pytest.raises(fa.FaError):
+            agg.finalize(9)
+
+
+def test_context_multi_gpu_range_shards(fa, O, torch_gpu):
+    if fa.device_count() < 2:
+        pytest.skip("needs 2 GPUs in one process")
+    n, D = 1_000_001, 4
+    w = O.weights(D)
+    xs = host_clients(O, 49, D, n, False)
+    with fa.Aggregator(2) as agg:
+        agg.define(1, n, fa.F32, fa.F32, D, fa.FEDAVG)
+        for k in range(D):
+            agg.submit(1, k, xs[k], w[k])
+        assert_bits(agg.finalize(1), O.fedavg(xs, w))

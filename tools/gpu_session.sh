@@ -1,0 +1,46 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, bench, rocprofv3 kernel-trace stats.
+# Every GPU step has its own time limit; a crash, abort or timeout (exit code
+# other than 0, or 1 = "tests failed") ends the session so nothing else runs on
+# a possibly faulted GPU.  Output lands in gpurun_out/<tag>/.
+#   tools/gpu_session.sh <tag> [steps...]   steps: test smoke bench prof pmc
+set -u
+TAG=${1:-r01}
+shift || true
+STEPS=${*:-test smoke bench prof}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+ok_or_fail() {  # rc, step
+    if [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; then
+        echo "step $2 ended with $1 (crash/timeout): stopping" | tee -a "$OUT/session.log"
+        exit "$1"
+    fi
+}
+for s in $STEPS; do
+    echo "== $s $(date +%T)" | tee -a "$OUT/session.log"
+    case $s in
+    test)
+        timeout -k 10 900 python -m pytest tests -m gpu -q -rf > "$OUT/pytest_gpu.log" 2>&1
+        rc=$?; tail -5 "$OUT/pytest_gpu.log"; ok_or_fail $rc test ;;
+    smoke)
+        timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+        rc=$?; tail -3 "$OUT/smoke.log"; ok_or_fail $rc smoke ;;
+    bench)
+        timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
+        rc=$?; cat "$OUT/bench.json"; tail -3 "$OUT/bench.err"; ok_or_fail $rc bench ;;
+    prof)
+        timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
+            python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
+        rc=$?; tail -3 "$OUT/prof.err"; ok_or_fail $rc prof ;;
+    pmc)
+        for c in FETCH_SIZE WRITE_SIZE; do
+            timeout -k 10 600 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$OUT/pmc_$c" -o run -- \
+                python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-secondary > "$OUT/pmc_$c.json" 2> "$OUT/pmc_$c.err"
+            rc=$?; tail -2 "$OUT/pmc_$c.err"; ok_or_fail $rc pmc_$c
+        done ;;
+    *)
+        echo "unknown step $s" ;;
+    esac
+done
+echo "== done $(date +%T)" | tee -a "$OUT/session.log"
