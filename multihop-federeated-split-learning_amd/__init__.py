@@ -165,6 +165,8 @@ class Aggregator:
 
     def submit(self, part_id, slot, host, weight=1.0, pinned=False):
         host = np.ascontiguousarray(host)
+        if part_id not in self.parts:
+            check(lib().fa_submit(self.handle, part_id, slot, host.ctypes.data, float(weight)))
         n, in_dtype = self.parts[part_id][:2]
         if host.nbytes != n * DTYPE_SIZE[in_dtype]:
             raise ValueError("bucket %d expects %d bytes, got %d" % (part_id, n * DTYPE_SIZE[in_dtype], host.nbytes))
@@ -172,6 +174,8 @@ class Aggregator:
         check(fn(self.handle, part_id, slot, host.ctypes.data, float(weight)))
 
     def finalize(self, part_id, out=None):
+        if part_id not in self.parts:  # let the library report it (FA_ERR_ARG)
+            check(lib().fa_finalize(self.handle, part_id, None))
         n, _, out_dtype = self.parts[part_id][:3]
         if out is None:
             out = np.empty(n, np.float32 if out_dtype == F32 else np.uint16)

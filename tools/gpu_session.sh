@@ -31,7 +31,7 @@ for s in $STEPS; do
         rc=$?; cat "$OUT/bench.json"; tail -3 "$OUT/bench.err"; ok_or_fail $rc bench ;;
     prof)
         timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-            python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
+            python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-secondary > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
         rc=$?; tail -3 "$OUT/prof.err"; ok_or_fail $rc prof ;;
     pmc)
         for c in FETCH_SIZE WRITE_SIZE; do
@@ -39,6 +39,15 @@ for s in $STEPS; do
                 python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-secondary > "$OUT/pmc_$c.json" 2> "$OUT/pmc_$c.err"
             rc=$?; tail -2 "$OUT/pmc_$c.err"; ok_or_fail $rc pmc_$c
         done ;;
+    probe)
+        hipcc --offload-arch=gfx950 -O3 tools/hbm_probe.hip -o "$OUT/hbm_probe" > "$OUT/probe_build.log" 2>&1 &&
+        timeout -k 10 300 "$OUT/hbm_probe" > "$OUT/hbm_probe.json" 2> "$OUT/probe.err"
+        rc=$?; cat "$OUT/hbm_probe.json"; ok_or_fail $rc probe ;;
+    sweep)
+        timeout -k 10 600 python tools/sweep.py northstar > "$OUT/sweep_northstar.jsonl" 2> "$OUT/sweep.err"
+        rc=$?; head -5 "$OUT/sweep_northstar.jsonl"; ok_or_fail $rc sweep
+        timeout -k 10 600 python tools/sweep.py c2 > "$OUT/sweep_c2.jsonl" 2>> "$OUT/sweep.err"
+        rc=$?; head -5 "$OUT/sweep_c2.jsonl"; ok_or_fail $rc sweep_c2 ;;
     *)
         echo "unknown step $s" ;;
     esac

@@ -1,0 +1,100 @@
+// hbm_probe.hip -- measured HBM ceilings on this MI355X for the roofline report.
+// Not part of the product: a standalone tool that times a read-only stream, a
+// copy and a write stream over 8 GiB buffers (far beyond the 256 MiB
+// Infinity Cache) with hipEvents and prints one JSON line.
+//   hipcc --offload-arch=gfx950 -O3 tools/hbm_probe.hip -o tools/hbm_probe
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define CHECK(x)                                                               \
+    do {                                                                       \
+        hipError_t e = (x);                                                    \
+        if (e != hipSuccess) {                                                 \
+            fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e));             \
+            return 1;                                                          \
+        }                                                                      \
+    } while (0)
+
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void read_kernel(const f32x4* __restrict__ p, int64_t nvec, float* sink) {
+    f32x4 acc = {0, 0, 0, 0};
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; v + (U - 1) * stride < nvec; v += U * stride) {
+        f32x4 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = NT ? __builtin_nontemporal_load(p + v + u * stride) : p[v + u * stride];
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += x[u];
+    }
+    for (; v < nvec; v += stride) acc += p[v];
+    float s = acc.x + acc.y + acc.z + acc.w;
+    if (s == 12345.678f) sink[threadIdx.x] = s;  // keeps the loads live, never true for the fill below
+}
+
+__global__ __launch_bounds__(256) void copy_kernel(const f32x4* __restrict__ a, f32x4* __restrict__ b, int64_t nvec) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride)
+        __builtin_nontemporal_store(__builtin_nontemporal_load(a + v), b + v);
+}
+
+__global__ __launch_bounds__(256) void write_kernel(f32x4* __restrict__ b, int64_t nvec) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride)
+        __builtin_nontemporal_store(f32x4{1.f, 2.f, 3.f, 4.f}, b + v);
+}
+
+template <typename F>
+double time_ms(F f, int reps) {
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    f();
+    (void)hipDeviceSynchronize();
+    std::vector<float> ms;
+    for (int r = 0; r < reps; ++r) {
+        (void)hipEventRecord(a, 0);
+        f();
+        (void)hipEventRecord(b, 0);
+        (void)hipEventSynchronize(b);
+        float t;
+        (void)hipEventElapsedTime(&t, a, b);
+        ms.push_back(t);
+    }
+    std::sort(ms.begin(), ms.end());
+    return ms[ms.size() / 2];
+}
+
+int main() {
+    const size_t bytes = 8ull << 30;
+    const int64_t nvec = (int64_t)(bytes / 16);
+    f32x4 *a, *b;
+    float* sink;
+    CHECK(hipMalloc(&a, bytes));
+    CHECK(hipMalloc(&b, bytes / 2));
+    CHECK(hipMalloc(&sink, 4096));
+    CHECK(hipMemset(a, 0, bytes));
+    CHECK(hipMemset(b, 0, bytes / 2));
+    printf("{");
+    const int grids[] = {1024, 2048, 4096, 8192, 16384};
+    bool first = true;
+    for (int g : grids) {
+        double r8 = time_ms([&] { read_kernel<8, false><<<g, 256>>>(a, nvec, sink); }, 10);
+        double r8n = time_ms([&] { read_kernel<8, true><<<g, 256>>>(a, nvec, sink); }, 10);
+        double r16 = time_ms([&] { read_kernel<16, true><<<g, 256>>>(a, nvec, sink); }, 10);
+        printf("%s\"read_grid%d\":{\"u8\":%.1f,\"u8_nt\":%.1f,\"u16_nt\":%.1f}", first ? "" : ",", g,
+               bytes / r8 / 1e6, bytes / r8n / 1e6, bytes / r16 / 1e6);
+        first = false;
+    }
+    const int64_t nh = nvec / 2;
+    double c = time_ms([&] { copy_kernel<<<4096, 256>>>(a, b, nh); }, 10);
+    double w = time_ms([&] { write_kernel<<<4096, 256>>>(b, nh); }, 10);
+    printf(",\"copy_GBs\":%.1f,\"write_GBs\":%.1f,\"unit\":\"GB/s (1e9 B/s), median of 10, 8 GiB read / 4 GiB copy+write\"}\n",
+           2.0 * (bytes / 2) / c / 1e6, (bytes / 2) / w / 1e6);
+    return 0;
+}

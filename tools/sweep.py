@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Tuning sweep of the FedAvg kernel on the north-star workload (GPU box tool).
+
+Interleaves every configuration in rounds inside one process (rule: A/B deltas
+come from one process), prints one JSON line per configuration with the median
+and min kernel time over all rounds.
+"""
+import itertools
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+
+def main():
+    import torch
+    fa = bench.load_pkg()
+    fa.lib()
+    workload = sys.argv[1] if len(sys.argv) > 1 else "northstar"
+    D, n, i, o, _ = bench.WORKLOADS[workload]
+    setup = bench.Setup(fa, torch, D, n, i, o, 0)
+    stream = torch.cuda.Stream()
+    grid = list(itertools.product([128, 256], [0, 1024, 2048, 4096, 8192], [4, 8, 16], [0, 1]))
+    times = {g: [] for g in grid}
+    for rnd in range(5):
+        for g in grid:
+            fa.set_tuning(block=g[0], max_blocks=g[1] if g[1] else -1, unroll=g[2], nontemporal=g[3])
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(6)]
+            for a, b in ev:
+                a.record(stream)
+                setup.launch(0, stream)
+                b.record(stream)
+            torch.cuda.synchronize()
+            times[g] += [a.elapsed_time(b) for a, b in ev[1:]]
+    rows = []
+    for g, t in times.items():
+        med = statistics.median(t)
+        rows.append({"block": g[0], "max_blocks": g[1], "unroll": g[2], "nt": g[3], "ms_median": round(med, 4),
+                     "ms_min": round(min(t), 4), "GBs": round(setup.algo_bytes() / med / 1e6, 1)})
+    rows.sort(key=lambda r: r["ms_median"])
+    for r in rows:
+        print(json.dumps(r))
+
+
+if __name__ == "__main__":
+    main()
