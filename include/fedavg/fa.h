@@ -113,7 +113,7 @@ typedef struct {
     int block;       /* threads per workgroup (multiple of 64) */
     int max_blocks;  /* grid cap; grid-stride beyond it */
     int unroll;      /* clients loaded per FMA group: 4, 8 or 16 */
-    int nontemporal; /* 1: nt loads/stores, 0: default cache policy, -1: library default */
+    int nontemporal; /* 0 default policy, 1 nt loads+stores, 2 nt loads only, 3 nt stores only; -1 keep */
 } fa_tuning;
 int fa_set_tuning(const fa_tuning* t);
 int fa_get_tuning(fa_tuning* t);

@@ -260,7 +260,10 @@ int fa_set_tuning(const fa_tuning* t) {
         if (t->unroll != 4 && t->unroll != 8 && t->unroll != 16) return fail(FA_ERR_ARG, "unroll must be 4/8/16");
         nt.unroll = t->unroll;
     }
-    if (t->nontemporal >= 0) nt.nontemporal = t->nontemporal ? 1 : 0;
+    if (t->nontemporal >= 0) {
+        if (t->nontemporal > 3) return fail(FA_ERR_ARG, "nontemporal must be 0..3");
+        nt.nontemporal = t->nontemporal;
+    }
     g_tuning = nt;
     return FA_OK;
 }

@@ -128,7 +128,8 @@ __device__ __forceinline__ void chain_scalar_edges(const ClientTable& t, int nc,
 }
 
 // Vector body over nvec lane-vectors starting at element `head`.
-template <typename IN, typename OUT, int U, bool NT, bool INIT>
+// POL: bit 0 = non-temporal loads, bit 1 = non-temporal stores.
+template <typename IN, typename OUT, int U, int POL, bool INIT>
 __global__ __launch_bounds__(256) void fedavg_chain_kernel(const ClientTable t, int nc, const float* init, void* out,
                                                            int64_t head, int64_t nvec, int64_t n) {
     constexpr int V = In<IN>::kVec;
@@ -140,7 +141,7 @@ __global__ __launch_bounds__(256) void fedavg_chain_kernel(const ClientTable t, 
         if constexpr (INIT) {
 #pragma unroll
             for (int j = 0; j < V; j += 4) {
-                u32x4 r = ld16<NT>(init + e + j);
+                u32x4 r = ld16<(POL & 1) != 0>(init + e + j);
                 acc[j] = __uint_as_float(r.x); acc[j + 1] = __uint_as_float(r.y);
                 acc[j + 2] = __uint_as_float(r.z); acc[j + 3] = __uint_as_float(r.w);
             }
@@ -152,7 +153,7 @@ __global__ __launch_bounds__(256) void fedavg_chain_kernel(const ClientTable t, 
         for (; k + U <= nc; k += U) {
             u32x4 raw[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) raw[u] = ld16<NT>(reinterpret_cast<const IN*>(t.src[k + u]) + e);
+            for (int u = 0; u < U; ++u) raw[u] = ld16<(POL & 1) != 0>(reinterpret_cast<const IN*>(t.src[k + u]) + e);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 float x[V];
@@ -164,12 +165,12 @@ __global__ __launch_bounds__(256) void fedavg_chain_kernel(const ClientTable t, 
         }
         for (; k < nc; ++k) {
             float x[V];
-            In<IN>::widen(ld16<NT>(reinterpret_cast<const IN*>(t.src[k]) + e), x);
+            In<IN>::widen(ld16<(POL & 1) != 0>(reinterpret_cast<const IN*>(t.src[k]) + e), x);
             const float w = t.w[k];
 #pragma unroll
             for (int j = 0; j < V; ++j) acc[j] = __builtin_fmaf(x[j], w, acc[j]);
         }
-        Out<OUT>::template store<V, NT>(out, e, acc);
+        Out<OUT>::template store<V, (POL & 2) != 0>(out, e, acc);
     }
 }
 
@@ -252,26 +253,26 @@ inline int64_t grid_for(int64_t work, const Tuning& tu) {
     return g;
 }
 
-template <typename IN, typename OUT, int U, bool NT>
+template <typename IN, typename OUT, int U, int POL>
 hipError_t launch_chain_u(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
                           int64_t n, const Tuning& tu, hipStream_t s) {
     const int64_t g = grid_for(nvec > 0 ? nvec : 1, tu);
     if (init)
-        hipLaunchKernelGGL((fedavg_chain_kernel<IN, OUT, U, NT, true>), dim3((unsigned)g), dim3(tu.block), 0, s, t,
+        hipLaunchKernelGGL((fedavg_chain_kernel<IN, OUT, U, POL, true>), dim3((unsigned)g), dim3(tu.block), 0, s, t,
                            nc, init, out, head, nvec, n);
     else
-        hipLaunchKernelGGL((fedavg_chain_kernel<IN, OUT, U, NT, false>), dim3((unsigned)g), dim3(tu.block), 0, s, t,
+        hipLaunchKernelGGL((fedavg_chain_kernel<IN, OUT, U, POL, false>), dim3((unsigned)g), dim3(tu.block), 0, s, t,
                            nc, init, out, head, nvec, n);
     return hipGetLastError();
 }
 
-template <typename IN, typename OUT, bool NT>
-hipError_t launch_chain_nt(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
+template <typename IN, typename OUT, int POL>
+hipError_t launch_chain_pol(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
                            int64_t n, const Tuning& tu, hipStream_t s) {
     switch (tu.unroll) {
-        case 4: return launch_chain_u<IN, OUT, 4, NT>(t, nc, init, out, head, nvec, n, tu, s);
-        case 16: return launch_chain_u<IN, OUT, 16, NT>(t, nc, init, out, head, nvec, n, tu, s);
-        default: return launch_chain_u<IN, OUT, 8, NT>(t, nc, init, out, head, nvec, n, tu, s);
+        case 4: return launch_chain_u<IN, OUT, 4, POL>(t, nc, init, out, head, nvec, n, tu, s);
+        case 16: return launch_chain_u<IN, OUT, 16, POL>(t, nc, init, out, head, nvec, n, tu, s);
+        default: return launch_chain_u<IN, OUT, 8, POL>(t, nc, init, out, head, nvec, n, tu, s);
     }
 }
 
@@ -288,8 +289,13 @@ hipError_t launch_chain_t(const ClientTable& t, int nc, const float* init, void*
                                s, t, nc, init, out, n);
         return hipGetLastError();
     }
-    if (tu.nontemporal) return launch_chain_nt<IN, OUT, true>(t, nc, init, out, head, nvec, n, tu, s);
-    return launch_chain_nt<IN, OUT, false>(t, nc, init, out, head, nvec, n, tu, s);
+    // nontemporal knob: 0 none, 1 loads + stores, 2 loads only, 3 stores only
+    switch (tu.nontemporal) {
+        case 1: return launch_chain_pol<IN, OUT, 3>(t, nc, init, out, head, nvec, n, tu, s);
+        case 2: return launch_chain_pol<IN, OUT, 1>(t, nc, init, out, head, nvec, n, tu, s);
+        case 3: return launch_chain_pol<IN, OUT, 2>(t, nc, init, out, head, nvec, n, tu, s);
+        default: return launch_chain_pol<IN, OUT, 0>(t, nc, init, out, head, nvec, n, tu, s);
+    }
 }
 
 }  // namespace

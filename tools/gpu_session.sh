@@ -48,6 +48,9 @@ for s in $STEPS; do
         rc=$?; head -5 "$OUT/sweep_northstar.jsonl"; ok_or_fail $rc sweep
         timeout -k 10 600 python tools/sweep.py c2 > "$OUT/sweep_c2.jsonl" 2>> "$OUT/sweep.err"
         rc=$?; head -5 "$OUT/sweep_c2.jsonl"; ok_or_fail $rc sweep_c2 ;;
+    layout)
+        timeout -k 10 600 python tools/exp_layout.py > "$OUT/exp_layout.jsonl" 2> "$OUT/exp_layout.err"
+        rc=$?; head -8 "$OUT/exp_layout.jsonl"; tail -3 "$OUT/exp_layout.err"; ok_or_fail $rc layout ;;
     *)
         echo "unknown step $s" ;;
     esac

@@ -49,6 +49,28 @@ __global__ __launch_bounds__(256) void write_kernel(f32x4* __restrict__ b, int64
         __builtin_nontemporal_store(f32x4{1.f, 2.f, 3.f, 4.f}, b + v);
 }
 
+struct Table {
+    const f32x4* p[32];
+};
+
+// 32-stream read with the FedAvg kernel's structure (8 clients per load group, one float4 per lane) but no
+// store: the read-only ceiling of the aggregation access pattern.
+__global__ __launch_bounds__(256) void mstream_read_kernel(Table t, int64_t nvec, float* sink) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+        f32x4 acc = {0, 0, 0, 0};
+        for (int k = 0; k < 32; k += 8) {
+            f32x4 x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) x[u] = __builtin_nontemporal_load(t.p[k + u] + v);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc += x[u];
+        }
+        float s = acc.x + acc.y + acc.z + acc.w;
+        if (s == 12345.678f) sink[threadIdx.x] = s;
+    }
+}
+
 template <typename F>
 double time_ms(F f, int reps) {
     hipEvent_t a, b;
@@ -94,6 +116,12 @@ int main() {
     const int64_t nh = nvec / 2;
     double c = time_ms([&] { copy_kernel<<<4096, 256>>>(a, b, nh); }, 10);
     double w = time_ms([&] { write_kernel<<<4096, 256>>>(b, nh); }, 10);
+    // 32 streams of 256 MiB inside the 8 GiB buffer, one-shot grid like the FedAvg kernel
+    Table t;
+    const int64_t per = nvec / 32;
+    for (int k = 0; k < 32; ++k) t.p[k] = a + k * per;
+    double m = time_ms([&] { mstream_read_kernel<<<(unsigned)(per / 256), 256>>>(t, per, sink); }, 10);
+    printf(",\"mstream32_read_GBs\":%.1f", bytes / m / 1e6);
     printf(",\"copy_GBs\":%.1f,\"write_GBs\":%.1f,\"unit\":\"GB/s (1e9 B/s), median of 10, 8 GiB read / 4 GiB copy+write\"}\n",
            2.0 * (bytes / 2) / c / 1e6, (bytes / 2) / w / 1e6);
     return 0;
