@@ -110,9 +110,15 @@ def traffic_from_profile(workload, n_gpus):
 
 
 class Setup:
-    """Device buffers of one workload on the current GPU: `sets` rotated input sets of D clients."""
+    """One workload on the current GPU through the product's own context (fa_ctx).
 
-    def __init__(self, fa, torch, D, n, in_dt, out_dt, rank, seed=0x5EED, min_rotate_bytes=ROTATE_MIN_BYTES):
+    Each rotated input set is one bucket (part) of the context: its D client
+    slots live in one HBM pool with the library's per-slot skew, the inputs are
+    generated in place (fa_fill_uniform on the slot pointers) and a step is
+    fa_reduce_part -- the device-resident round of the aggregator.
+    """
+
+    def __init__(self, fa, torch, D, n, in_dt, out_dt, rank, device, seed=0x5EED, min_rotate_bytes=ROTATE_MIN_BYTES):
         self.fa, self.torch = fa, torch
         self.D, self.n = D, n
         self.in_dt = fa.F32 if in_dt == "f32" else fa.BF16
@@ -121,17 +127,13 @@ class Setup:
         self.s_out = 4 if out_dt == "f32" else 2
         set_bytes = D * n * self.s_in
         self.nsets = max(1, -(-min_rotate_bytes // set_bytes))
-        tdt = torch.float32 if in_dt == "f32" else torch.int16
-        self.sets = []
+        self.agg = fa.Aggregator(devices=[device])
         for s in range(self.nsets):
-            clients = []
+            self.agg.define(s, n, self.in_dt, self.out_dt, D, fa.FEDAVG)
             for k in range(D):
-                t = torch.empty(n, dtype=tdt, device="cuda")
-                # element index offset by the rank's range so ranks hold disjoint slices of one bucket
-                fa.fill_uniform(t, n, self.in_dt, seed + s, k, idx0=rank * n)
-                clients.append(t)
-            self.sets.append(clients)
-        self.out = torch.empty(n, dtype=torch.float32 if out_dt == "f32" else torch.int16, device="cuda")
+                ptr, cnt, _ = self.agg.slot(s, 0, k)
+                # element index offset by the rank's range: ranks hold disjoint slices of one bucket
+                fa.fill_uniform(ptr, cnt, self.in_dt, seed + s, k, idx0=rank * n)
         self.w = self._weights(D)
 
     @staticmethod
@@ -151,8 +153,13 @@ class Setup:
         return np.array([float(x) / tot for x in nk], np.float32)
 
     def launch(self, step, stream):
-        self.fa.reduce_device(self.sets[step % self.nsets], self.w, self.n, self.in_dt, self.out, self.out_dt,
-                              self.fa.FEDAVG, stream=stream)
+        self.agg.reduce(step % self.nsets, self.w, stream=stream)
+
+    def clients(self, s=0):
+        return [self.agg.slot(s, 0, k)[0] for k in range(self.D)]
+
+    def close(self):
+        self.agg.close()
 
     def algo_bytes(self):
         return self.D * self.n * self.s_in + self.n * self.s_out
@@ -181,9 +188,9 @@ def timed_loop(torch, setup, steps, warmup, stream, dist, barrier):
     return wall, kern_ms
 
 
-def run_rs_step(fa, torch, setup, partial, shard, stream, dist):
+def run_rs_step(fa, torch, setup, cl, partial, shard, stream, dist):
     """client-rs: local chain over this rank's clients into fp32 partials, then RCCL reduce-scatter."""
-    fa.reduce_device(setup.sets[0], setup.w, setup.n, setup.in_dt, partial, fa.F32, fa.FEDAVG, stream=stream)
+    fa.reduce_device(cl, setup.w, setup.n, setup.in_dt, partial, fa.F32, fa.FEDAVG, stream=stream)
     with torch.cuda.stream(stream):
         dist.reduce_scatter_tensor(shard, partial, op=dist.ReduceOp.SUM)
 
@@ -229,7 +236,7 @@ def main():
             pass
 
     stream = torch.cuda.Stream()
-    setup = Setup(fa, torch, D, n, in_dt, out_dt, rank)
+    setup = Setup(fa, torch, D, n, in_dt, out_dt, rank, local_rank)
     torch.cuda.synchronize()
 
     if args.layout == "range":
@@ -240,8 +247,9 @@ def main():
     else:
         partial = torch.empty(n, dtype=torch.float32, device="cuda")
         shard = torch.empty(n // world, dtype=torch.float32, device="cuda")
+        cl = setup.clients()
         for _ in range(args.warmup):
-            run_rs_step(fa, torch, setup, partial, shard, stream, dist)
+            run_rs_step(fa, torch, setup, cl, partial, shard, stream, dist)
         torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
@@ -249,7 +257,7 @@ def main():
         t0 = time.perf_counter()
         for i in range(args.steps):
             evs[i][0].record(stream)
-            fa.reduce_device(setup.sets[0], setup.w, n, setup.in_dt, partial, fa.F32, fa.FEDAVG, stream=stream)
+            fa.reduce_device(cl, setup.w, n, setup.in_dt, partial, fa.F32, fa.FEDAVG, stream=stream)
             evs[i][1].record(stream)
             with torch.cuda.stream(stream):
                 if world > 1:
@@ -300,13 +308,12 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_secondary:
         sec = {}
-        del setup
-        torch.cuda.empty_cache()
+        setup.close()
         for name in sorted(WORKLOADS):
             if name == args.workload:
                 continue
             sD, sn, si, so, sdesc = WORKLOADS[name]
-            s = Setup(fa, torch, sD, sn, si, so, 0)
+            s = Setup(fa, torch, sD, sn, si, so, 0, local_rank)
             torch.cuda.synchronize()
             w2, km = timed_loop(torch, s, max(10, args.steps), 3, stream, dist, barrier)
             ka = statistics.mean(km)
@@ -315,8 +322,8 @@ def main():
                          "achieved_GBs": round(s.algo_bytes() / (ka * 1e-3) / 1e9, 1),
                          "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          "input_sets_rotated": s.nsets}
+            s.close()
             del s
-            torch.cuda.empty_cache()
         line["secondary"] = sec
 
     if rank == 0:

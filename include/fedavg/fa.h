@@ -63,6 +63,8 @@ int fa_device_count(int* out);   /* visible HIP devices */
  * + refactor() -> init_model_sate (aggregator.cpp:47,53; systemAPI.cpp:17-38).
  * Uses devices 0..n_gpus-1. */
 int fa_create(fa_ctx** out, int n_gpus, int flags);
+/* Same on an explicit device list (e.g. {LOCAL_RANK} for one process per GPU). */
+int fa_create_ex(fa_ctx** out, const int* device_ids, int n_gpus, int flags);
 void fa_destroy(fa_ctx* ctx);
 
 /* One reduced bucket = the flattened named_parameters() of one model part
@@ -88,6 +90,25 @@ int fa_submit_pinned(fa_ctx* ctx, int part_id, int client_slot, const void* host
  * GPU, copies the result (out dtype) to host_dst and resets the round. */
 int fa_finalize(fa_ctx* ctx, int part_id, void* host_dst);
 
+/* Device-resident round (the data path with buckets already in HBM, e.g. a
+ * zero-copy ingest that lands receipts straight in the slots): reduce the
+ * part's slots into its device output on every GPU, no host copies.
+ * h_weights: D floats, NULL = the weights given to fa_submit.  hip_stream:
+ * NULL = ctx compute streams; non-NULL only for a single-GPU ctx.  Async. */
+int fa_reduce_part(fa_ctx* ctx, int part_id, const float* h_weights, void* hip_stream);
+/* Device pointer of client slot `client_slot` on GPU `gpu` (n_elems elements of
+ * the input dtype, covering bucket elements [elem_offset, elem_offset+n_elems)),
+ * and of the part's device output.  Slots of one bucket share one allocation
+ * with a small per-slot byte skew (fa_tuning.slot_skew) so that the wave's
+ * simultaneous loads spread over HBM channels. */
+int fa_bucket_slot(fa_ctx* ctx, int part_id, int gpu, int client_slot, void** d_ptr, size_t* n_elems,
+                   size_t* elem_offset);
+int fa_bucket_output(fa_ctx* ctx, int part_id, int gpu, void** d_ptr);
+/* D2H of the part's current device output (after fa_reduce_part), waiting for it. */
+int fa_copy_output(fa_ctx* ctx, int part_id, void* host_dst);
+/* Wait for all copy and compute work of the ctx. */
+int fa_sync(fa_ctx* ctx);
+
 /* Raw device entry for benches and device-resident callers: reduce D client
  * buckets already resident on device `gpu` into d_out.  d_clients[k] are device
  * pointers, h_weights a host array of D floats (copied into kernel arguments,
@@ -108,12 +129,14 @@ int fa_reduce_device(fa_ctx* ctx, int gpu, const void* const* d_clients, const f
 int fa_fill_uniform(void* d_dst, size_t n, fa_dtype dt, uint64_t seed, uint32_t client, uint64_t idx0,
                     void* hip_stream);
 
-/* Kernel tuning knobs for benches (0 = library default). */
+/* Kernel and layout tuning knobs for benches (0 = keep the current value). */
 typedef struct {
     int block;       /* threads per workgroup (multiple of 64) */
     int max_blocks;  /* grid cap; grid-stride beyond it */
     int unroll;      /* clients loaded per FMA group: 4, 8 or 16 */
     int nontemporal; /* 0 default policy, 1 nt loads+stores, 2 nt loads only, 3 nt stores only; -1 keep */
+    int slot_skew;   /* bytes between consecutive client slots beyond 4 KiB alignment (multiple of 16);
+                        -1 = none; applies to buckets defined afterwards */
 } fa_tuning;
 int fa_set_tuning(const fa_tuning* t);
 int fa_get_tuning(fa_tuning* t);

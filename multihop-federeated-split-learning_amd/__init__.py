@@ -34,7 +34,7 @@ class FaError(RuntimeError):
 
 class _Tuning(ctypes.Structure):
     _fields_ = [("block", ctypes.c_int), ("max_blocks", ctypes.c_int), ("unroll", ctypes.c_int),
-                ("nontemporal", ctypes.c_int)]
+                ("nontemporal", ctypes.c_int), ("slot_skew", ctypes.c_int)]
 
 
 def build():
@@ -58,6 +58,12 @@ def lib():
         "fa_last_error": (ctypes.c_char_p, []),
         "fa_device_count": (I, [ctypes.POINTER(I)]),
         "fa_create": (I, [ctypes.POINTER(P), I, I]),
+        "fa_create_ex": (I, [ctypes.POINTER(P), ctypes.POINTER(I), I, I]),
+        "fa_reduce_part": (I, [P, I, P, P]),
+        "fa_bucket_slot": (I, [P, I, I, I, ctypes.POINTER(P), ctypes.POINTER(S), ctypes.POINTER(S)]),
+        "fa_bucket_output": (I, [P, I, I, ctypes.POINTER(P)]),
+        "fa_sync": (I, [P]),
+        "fa_copy_output": (I, [P, I, P]),
         "fa_destroy": (None, [P]),
         "fa_bucket_define": (I, [P, I, S, I, I, I, I]),
         "fa_set_literal_divisor": (I, [P, I, F]),
@@ -133,11 +139,12 @@ def fill_uniform(dst, n, dtype, seed, client, idx0=0, stream=None):
 def get_tuning():
     t = _Tuning()
     check(lib().fa_get_tuning(ctypes.byref(t)))
-    return {"block": t.block, "max_blocks": t.max_blocks, "unroll": t.unroll, "nontemporal": t.nontemporal}
+    return {"block": t.block, "max_blocks": t.max_blocks, "unroll": t.unroll, "nontemporal": t.nontemporal,
+            "slot_skew": t.slot_skew}
 
 
-def set_tuning(block=0, max_blocks=0, unroll=0, nontemporal=-1):
-    t = _Tuning(block, max_blocks, unroll, nontemporal)
+def set_tuning(block=0, max_blocks=0, unroll=0, nontemporal=-1, slot_skew=0):
+    t = _Tuning(block, max_blocks, unroll, nontemporal, slot_skew)
     check(lib().fa_set_tuning(ctypes.byref(t)))
 
 
@@ -148,11 +155,16 @@ class Aggregator:
     once (refactor), submit every receipt, finalize to obtain the reduced part.
     """
 
-    def __init__(self, n_gpus=1, flags=None):
+    def __init__(self, n_gpus=1, flags=None, devices=None):
+        if devices is None:
+            devices = list(range(n_gpus))
+        n_gpus = len(devices)
         if flags is None:
             flags = SHARD_RANGE if n_gpus > 1 else 0
         h = ctypes.c_void_p()
-        check(lib().fa_create(ctypes.byref(h), n_gpus, flags))
+        ids = (ctypes.c_int * n_gpus)(*devices)
+        check(lib().fa_create_ex(ctypes.byref(h), ids, n_gpus, flags))
+        self.devices = list(devices)
         self.handle = h
         self.parts = {}
 
@@ -181,6 +193,37 @@ class Aggregator:
             out = np.empty(n, np.float32 if out_dtype == F32 else np.uint16)
         check(lib().fa_finalize(self.handle, part_id, out.ctypes.data))
         return out
+
+    def slot(self, part_id, gpu, client_slot):
+        """(device address, n_elems, elem_offset) of a client slot."""
+        ptr, n, off = ctypes.c_void_p(), ctypes.c_size_t(), ctypes.c_size_t()
+        check(lib().fa_bucket_slot(self.handle, part_id, gpu, client_slot, ctypes.byref(ptr), ctypes.byref(n),
+                                   ctypes.byref(off)))
+        return ptr.value, n.value, off.value
+
+    def output(self, part_id, gpu=0):
+        ptr = ctypes.c_void_p()
+        check(lib().fa_bucket_output(self.handle, part_id, gpu, ctypes.byref(ptr)))
+        return ptr.value
+
+    def reduce(self, part_id, weights=None, stream=None):
+        """fa_reduce_part: device-resident reduction of the part's slots (async)."""
+        wp = None
+        if weights is not None:
+            w = np.ascontiguousarray(np.asarray(weights, np.float32))
+            self._w_keep = w
+            wp = w.ctypes.data
+        check(lib().fa_reduce_part(self.handle, part_id, wp, _stream(stream)))
+
+    def copy_output(self, part_id, out=None):
+        n, _, out_dtype = self.parts[part_id][:3]
+        if out is None:
+            out = np.empty(n, np.float32 if out_dtype == F32 else np.uint16)
+        check(lib().fa_copy_output(self.handle, part_id, out.ctypes.data))
+        return out
+
+    def sync(self):
+        check(lib().fa_sync(self.handle))
 
     def close(self):
         if self.handle:

@@ -28,7 +28,9 @@
 namespace {
 
 thread_local std::string g_err;
-fa::Tuning g_tuning{256, 0, 8, 1};
+fa::Tuning g_tuning{128, 0, 8, 1};
+// Byte skew between consecutive client slots of one bucket (see slot_stride).
+size_t g_slot_skew = 512;
 
 int fail(int code, const char* fmt, ...) {
     char buf[512];
@@ -81,8 +83,10 @@ struct Part {
     fa_mode mode = FA_FEDAVG;
     float divisor = FA_DEFAULT_DIVISOR;
     std::vector<size_t> off, cnt;  // per-GPU element range
-    std::vector<char*> slots;      // per GPU: D * cnt * dsize(in)
-    std::vector<void*> dout;       // per GPU: cnt * dsize(out)
+    std::vector<char*> pool;       // per GPU: D client slots + the output, one allocation
+    std::vector<size_t> stride;    // per GPU: bytes between consecutive slots
+    std::vector<char*> slots;      // per GPU: == pool (slot k at pool + k * stride)
+    std::vector<void*> dout;       // per GPU: pool + D * stride
     std::vector<float> w;
     std::vector<char> submitted;
     int n_submitted = 0;
@@ -184,13 +188,44 @@ int check_part(fa_ctx* ctx, int part_id, Part** out) {
 }
 
 void free_part(fa_ctx* ctx, Part& p) {
-    for (size_t g = 0; g < p.slots.size(); ++g) {
+    for (size_t g = 0; g < p.pool.size(); ++g) {
         DeviceGuard dg(ctx->gpu[g].dev);
-        if (p.slots[g]) (void)hipFree(p.slots[g]);
-        if (p.dout[g]) (void)hipFree(p.dout[g]);
+        if (p.pool[g]) (void)hipFree(p.pool[g]);
     }
+    p.pool.clear();
     p.slots.clear();
     p.dout.clear();
+}
+
+// HBM placement of a bucket's slots.  Client buckets that start at the same
+// address modulo a large power of two put the U simultaneous loads of a wave
+// (and its store) on the same HBM channels; a small per-slot skew spreads them.
+// Measured on MI355X (profiles/r01_summary.json, tools/exp_layout.py): 256-512 B
+// skew -> 1.30-1.32 ms for 32 x 256 MiB vs 1.47-1.51 ms unskewed; 64 B and
+// >= 1 KiB skews do not help reliably.  Slots stay 16-byte aligned.
+size_t slot_stride(size_t bytes) { return (bytes + 4095) / 4096 * 4096 + g_slot_skew; }
+
+inline char* slot_ptr(const Part& p, int g, int k) { return p.slots[g] + (size_t)k * p.stride[g]; }
+
+// Enqueue the reduction of part p on every GPU's compute stream (or `s` for a single GPU).
+int reduce_part(fa_ctx* ctx, Part& p, const float* w, hipStream_t s) {
+    std::vector<const void*> ptrs(p.D);
+    for (int g = 0; g < ctx->G; ++g) {
+        GpuRes& r = ctx->gpu[g];
+        DeviceGuard dg(r.dev);
+        hipStream_t st = s ? s : r.compute;
+        for (int k = 0; k < p.D; ++k) ptrs[k] = slot_ptr(p, g, k);
+        int rc;
+        if (p.mode == FA_LITERAL) {
+            const void* last = ptrs[p.last_slot >= 0 ? p.last_slot : p.D - 1];
+            rc = reduce_on(ctx, g, &last, w, 1, p.cnt[g], p.in, p.dout[g], p.out, p.mode, p.divisor, nullptr, st);
+        } else {
+            rc = reduce_on(ctx, g, ptrs.data(), w, p.D, p.cnt[g], p.in, p.dout[g], p.out, p.mode, p.divisor, nullptr,
+                           st);
+        }
+        if (rc) return rc;
+    }
+    return FA_OK;
 }
 
 int submit_impl(fa_ctx* ctx, int part_id, int slot, const void* src, float weight, bool pinned) {
@@ -204,7 +239,7 @@ int submit_impl(fa_ctx* ctx, int part_id, int slot, const void* src, float weigh
         GpuRes& r = ctx->gpu[g];
         DeviceGuard dg(r.dev);
         const char* hs = static_cast<const char*>(src) + p->off[g] * si;
-        char* ds = p->slots[g] + (size_t)slot * p->cnt[g] * si;
+        char* ds = slot_ptr(*p, g, slot);
         size_t bytes = p->cnt[g] * si;
         if (pinned) {
             if (bytes) FA_HIP(hipMemcpyAsync(ds, hs, bytes, hipMemcpyHostToDevice, r.copy));
@@ -227,6 +262,28 @@ int submit_impl(fa_ctx* ctx, int part_id, int slot, const void* src, float weigh
     }
     p->w[slot] = weight;
     p->last_slot = slot;
+    return FA_OK;
+}
+
+// D2H of the part's device output through the pinned chunks (the result leaves for new_message()).
+// Waits for all work on the device first (the reduction may have run on a caller's stream).
+int copy_output(fa_ctx* ctx, Part& p, void* host_dst) {
+    const size_t so = dsize(p.out);
+    for (int g = 0; g < ctx->G; ++g) {
+        GpuRes& r = ctx->gpu[g];
+        DeviceGuard dg(r.dev);
+        FA_HIP(hipDeviceSynchronize());
+        const char* src = static_cast<const char*>(p.dout[g]);
+        char* dst = static_cast<char*>(host_dst) + p.off[g] * so;
+        const size_t bytes = p.cnt[g] * so;
+        for (size_t o = 0; o < bytes; o += kStageBytes) {
+            const size_t b = std::min(kStageBytes, bytes - o);
+            FA_HIP(hipMemcpyAsync(r.stage[0], src + o, b, hipMemcpyDeviceToHost, r.compute));
+            FA_HIP(hipStreamSynchronize(r.compute));
+            std::memcpy(dst + o, r.stage[0], b);
+        }
+        FA_HIP(hipStreamSynchronize(r.compute));
+    }
     return FA_OK;
 }
 
@@ -260,6 +317,10 @@ int fa_set_tuning(const fa_tuning* t) {
         if (t->unroll != 4 && t->unroll != 8 && t->unroll != 16) return fail(FA_ERR_ARG, "unroll must be 4/8/16");
         nt.unroll = t->unroll;
     }
+    if (t->slot_skew) {
+        if (t->slot_skew > 0 && t->slot_skew % 16) return fail(FA_ERR_ARG, "slot_skew must be a multiple of 16");
+        g_slot_skew = t->slot_skew < 0 ? 0 : (size_t)t->slot_skew;
+    }
     if (t->nontemporal >= 0) {
         if (t->nontemporal > 3) return fail(FA_ERR_ARG, "nontemporal must be 0..3");
         nt.nontemporal = t->nontemporal;
@@ -275,22 +336,34 @@ int fa_get_tuning(fa_tuning* t) {
     t->max_blocks = g_tuning.max_blocks;
     t->unroll = g_tuning.unroll;
     t->nontemporal = g_tuning.nontemporal;
+    t->slot_skew = (int)g_slot_skew;
     return FA_OK;
 }
 
 int fa_create(fa_ctx** out, int n_gpus, int flags) {
+    std::vector<int> ids;
+    for (int g = 0; g < n_gpus; ++g) ids.push_back(g);
+    return fa_create_ex(out, ids.data(), n_gpus, flags);
+}
+
+int fa_create_ex(fa_ctx** out, const int* device_ids, int n_gpus, int flags) {
     g_err.clear();
     if (!out) return fail(FA_ERR_ARG, "out is null");
     *out = nullptr;
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return fail(FA_ERR_NODEV, "no HIP device visible");
-    if (n_gpus < 1 || n_gpus > count) return fail(FA_ERR_ARG, "n_gpus=%d but %d device(s) visible", n_gpus, count);
+    if (n_gpus < 1 || n_gpus > count || (!device_ids && n_gpus > 0))
+        return fail(FA_ERR_ARG, "n_gpus=%d but %d device(s) visible", n_gpus, count);
     if (n_gpus > 1 && !(flags & FA_SHARD_RANGE)) return fail(FA_ERR_ARG, "n_gpus > 1 needs FA_SHARD_RANGE");
     for (int g = 0; g < n_gpus; ++g) {
+        const int d = device_ids[g];
+        if (d < 0 || d >= count) return fail(FA_ERR_ARG, "device id %d out of range [0,%d)", d, count);
+        for (int h = 0; h < g; ++h)
+            if (device_ids[h] == d) return fail(FA_ERR_ARG, "device id %d listed twice", d);
         hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, g) != hipSuccess) return fail(FA_ERR_NODEV, "device %d unreadable", g);
+        if (hipGetDeviceProperties(&prop, d) != hipSuccess) return fail(FA_ERR_NODEV, "device %d unreadable", d);
         if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
-            return fail(FA_ERR_NODEV, "device %d is %s; libfa.so is built for gfx950 only", g, prop.gcnArchName);
+            return fail(FA_ERR_NODEV, "device %d is %s; libfa.so is built for gfx950 only", d, prop.gcnArchName);
     }
     fa_ctx* ctx = new fa_ctx();
     ctx->G = n_gpus;
@@ -298,8 +371,8 @@ int fa_create(fa_ctx** out, int n_gpus, int flags) {
     ctx->gpu.resize(n_gpus);
     for (int g = 0; g < n_gpus; ++g) {
         GpuRes& r = ctx->gpu[g];
-        r.dev = g;
-        DeviceGuard dg(g);
+        r.dev = device_ids[g];
+        DeviceGuard dg(r.dev);
         bool ok = hipStreamCreateWithFlags(&r.compute, hipStreamNonBlocking) == hipSuccess &&
                   hipStreamCreateWithFlags(&r.copy, hipStreamNonBlocking) == hipSuccess;
         for (int i = 0; ok && i < 2; ++i)
@@ -307,7 +380,7 @@ int fa_create(fa_ctx** out, int n_gpus, int flags) {
                  hipEventCreateWithFlags(&r.stage_ev[i], hipEventDisableTiming) == hipSuccess;
         if (!ok) {
             fa_destroy(ctx);
-            return fail(FA_ERR_NOMEM, "stream/staging setup failed on device %d", g);
+            return fail(FA_ERR_NOMEM, "stream/staging setup failed on device %d", device_ids[g]);
         }
     }
     *out = ctx;
@@ -361,16 +434,20 @@ int fa_bucket_define(fa_ctx* ctx, int part_id, size_t n_elems, fa_dtype in, fa_d
         p.off.push_back(lo);
         p.cnt.push_back(hi - lo);
     }
+    p.pool.assign(G, nullptr);
     p.slots.assign(G, nullptr);
     p.dout.assign(G, nullptr);
+    p.stride.assign(G, 0);
     for (size_t g = 0; g < G; ++g) {
         DeviceGuard dg(ctx->gpu[g].dev);
-        size_t sb = std::max<size_t>(1, (size_t)n_clients * p.cnt[g] * dsize(in));
-        size_t ob = std::max<size_t>(1, p.cnt[g] * dsize(out));
-        if (hipMalloc((void**)&p.slots[g], sb) != hipSuccess || hipMalloc(&p.dout[g], ob) != hipSuccess) {
+        p.stride[g] = slot_stride(p.cnt[g] * dsize(in));
+        const size_t bytes = (size_t)n_clients * p.stride[g] + std::max<size_t>(1, p.cnt[g] * dsize(out));
+        if (hipMalloc((void**)&p.pool[g], bytes) != hipSuccess) {
             free_part(ctx, p);
-            return fail(FA_ERR_NOMEM, "device alloc for part %d (%zu B slots) failed on GPU %zu", part_id, sb, g);
+            return fail(FA_ERR_NOMEM, "device alloc of %zu B for part %d failed on GPU %zu", bytes, part_id, g);
         }
+        p.slots[g] = p.pool[g];
+        p.dout[g] = p.pool[g] + (size_t)n_clients * p.stride[g];
     }
     ctx->parts.emplace(part_id, std::move(p));
     return FA_OK;
@@ -410,9 +487,7 @@ int fa_finalize(fa_ctx* ctx, int part_id, void* host_dst) {
         return fail(FA_ERR_STATE, "part %d: %d of %d clients submitted", part_id, p->n_submitted, p->D);
     if (p->n_submitted == 0) return fail(FA_ERR_STATE, "part %d: nothing submitted", part_id);
     if (!host_dst && p->n) return fail(FA_ERR_ARG, "host_dst is null");
-    const size_t si = dsize(p->in), so = dsize(p->out);
-    std::vector<const void*> ptrs(p->D);
-    for (int g = 0; g < ctx->G; ++g) {
+    for (int g = 0; g < ctx->G; ++g) {  // the reduction waits for this round's H2D copies
         GpuRes& r = ctx->gpu[g];
         DeviceGuard dg(r.dev);
         hipEvent_t ev;
@@ -420,35 +495,67 @@ int fa_finalize(fa_ctx* ctx, int part_id, void* host_dst) {
         FA_HIP(hipEventRecord(ev, r.copy));
         FA_HIP(hipStreamWaitEvent(r.compute, ev, 0));
         FA_HIP(hipEventDestroy(ev));
-        for (int k = 0; k < p->D; ++k) ptrs[k] = p->slots[g] + (size_t)k * p->cnt[g] * si;
-        if (p->mode == FA_LITERAL) {
-            const void* last = ptrs[p->last_slot];
-            rc = reduce_on(ctx, g, &last, p->w.data(), 1, p->cnt[g], p->in, p->dout[g], p->out, p->mode, p->divisor,
-                           nullptr, r.compute);
-        } else {
-            rc = reduce_on(ctx, g, ptrs.data(), p->w.data(), p->D, p->cnt[g], p->in, p->dout[g], p->out, p->mode,
-                           p->divisor, nullptr, r.compute);
-        }
-        if (rc) return rc;
     }
-    // D2H through the pinned chunks (the result leaves for new_message()).
-    for (int g = 0; g < ctx->G; ++g) {
-        GpuRes& r = ctx->gpu[g];
-        DeviceGuard dg(r.dev);
-        const char* src = static_cast<const char*>(p->dout[g]);
-        char* dst = static_cast<char*>(host_dst) + p->off[g] * so;
-        const size_t bytes = p->cnt[g] * so;
-        for (size_t o = 0; o < bytes; o += kStageBytes) {
-            const size_t b = std::min(kStageBytes, bytes - o);
-            FA_HIP(hipMemcpyAsync(r.stage[0], src + o, b, hipMemcpyDeviceToHost, r.compute));
-            FA_HIP(hipStreamSynchronize(r.compute));
-            std::memcpy(dst + o, r.stage[0], b);
-        }
-        FA_HIP(hipStreamSynchronize(r.compute));
-    }
+    rc = reduce_part(ctx, *p, p->w.data(), nullptr);
+    if (rc) return rc;
+    rc = copy_output(ctx, *p, host_dst);
+    if (rc) return rc;
     std::fill(p->submitted.begin(), p->submitted.end(), 0);
     p->n_submitted = 0;
     p->last_slot = -1;
+    return FA_OK;
+}
+
+int fa_bucket_slot(fa_ctx* ctx, int part_id, int gpu, int client_slot, void** d_ptr, size_t* n_elems,
+                   size_t* elem_offset) {
+    g_err.clear();
+    Part* p;
+    int rc = check_part(ctx, part_id, &p);
+    if (rc) return rc;
+    if (gpu < 0 || gpu >= ctx->G) return fail(FA_ERR_ARG, "gpu %d out of range", gpu);
+    if (client_slot < 0 || client_slot >= p->D) return fail(FA_ERR_ARG, "client slot %d out of range", client_slot);
+    if (d_ptr) *d_ptr = slot_ptr(*p, gpu, client_slot);
+    if (n_elems) *n_elems = p->cnt[gpu];
+    if (elem_offset) *elem_offset = p->off[gpu];
+    return FA_OK;
+}
+
+int fa_bucket_output(fa_ctx* ctx, int part_id, int gpu, void** d_ptr) {
+    g_err.clear();
+    Part* p;
+    int rc = check_part(ctx, part_id, &p);
+    if (rc) return rc;
+    if (gpu < 0 || gpu >= ctx->G) return fail(FA_ERR_ARG, "gpu %d out of range", gpu);
+    if (d_ptr) *d_ptr = p->dout[gpu];
+    return FA_OK;
+}
+
+int fa_reduce_part(fa_ctx* ctx, int part_id, const float* h_weights, void* hip_stream) {
+    g_err.clear();
+    Part* p;
+    int rc = check_part(ctx, part_id, &p);
+    if (rc) return rc;
+    if (hip_stream && ctx->G != 1) return fail(FA_ERR_ARG, "an explicit stream needs a single-GPU ctx");
+    return reduce_part(ctx, *p, h_weights ? h_weights : p->w.data(), static_cast<hipStream_t>(hip_stream));
+}
+
+int fa_copy_output(fa_ctx* ctx, int part_id, void* host_dst) {
+    g_err.clear();
+    Part* p;
+    int rc = check_part(ctx, part_id, &p);
+    if (rc) return rc;
+    if (!host_dst && p->n) return fail(FA_ERR_ARG, "host_dst is null");
+    return copy_output(ctx, *p, host_dst);
+}
+
+int fa_sync(fa_ctx* ctx) {
+    g_err.clear();
+    if (!ctx) return fail(FA_ERR_ARG, "ctx is null");
+    for (auto& r : ctx->gpu) {
+        DeviceGuard dg(r.dev);
+        FA_HIP(hipStreamSynchronize(r.copy));
+        FA_HIP(hipStreamSynchronize(r.compute));
+    }
     return FA_OK;
 }
 

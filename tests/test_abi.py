@@ -66,7 +66,12 @@ def test_version_and_errors_without_gpu(fa):
 def test_tuning_roundtrip(fa):
     before = fa.get_tuning()
     fa.set_tuning(block=128, unroll=16, nontemporal=0)
-    assert fa.get_tuning() == {"block": 128, "max_blocks": before["max_blocks"], "unroll": 16, "nontemporal": 0}
+    assert fa.get_tuning() == {"block": 128, "max_blocks": before["max_blocks"], "unroll": 16, "nontemporal": 0,
+                               "slot_skew": before["slot_skew"]}
+    fa.set_tuning(slot_skew=-1)
+    assert fa.get_tuning()["slot_skew"] == 0
+    with pytest.raises(fa.FaError):
+        fa.set_tuning(slot_skew=100)
     fa.set_tuning(**{k: v for k, v in before.items()})
     assert fa.get_tuning() == before
 

@@ -307,3 +307,45 @@ def test_context_multi_gpu_range_shards(fa, O, torch_gpu):
         for k in range(D):
             agg.submit(1, k, xs[k], w[k])
         assert_bits(agg.finalize(1), O.fedavg(xs, w))
+
+
+def test_device_resident_part_round(fa, O, torch_gpu):
+    """fa_bucket_slot + fa_reduce_part + fa_copy_output: receipts written straight into the pooled slots."""
+    n, D = 777_777, 6
+    w = O.weights(D)
+    xs = host_clients(O, 50, D, n, False)
+    with fa.Aggregator(1) as agg:
+        agg.define(3, n, fa.F32, fa.F32, D, fa.FEDAVG)
+        ptrs = []
+        for k in range(D):
+            ptr, cnt, off = agg.slot(3, 0, k)
+            assert (cnt, off) == (n, 0) and ptr % 16 == 0
+            ptrs.append(ptr)
+            fa.fill_uniform(ptr, cnt, fa.F32, 50, k)
+        gaps = {b - a for a, b in zip(ptrs, ptrs[1:])}
+        assert len(gaps) == 1 and gaps.pop() % 4096 == fa.get_tuning()["slot_skew"] % 4096
+        agg.reduce(3, w)
+        assert_bits(agg.copy_output(3), O.fedavg(xs, w))
+        # literal mode on the same layout: the last slot when nothing was submitted
+        agg.define(4, n, fa.F32, fa.F32, D, fa.LITERAL)
+        for k in range(D):
+            fa.fill_uniform(agg.slot(4, 0, k)[0], n, fa.F32, 50, k)
+        agg.reduce(4)
+        assert_bits(agg.copy_output(4), O.literal(xs[-1]))
+
+
+@pytest.mark.parametrize("skew", [-1, 256, 512, 4096 + 512])
+def test_slot_skew_does_not_change_bits(fa, O, torch_gpu, skew):
+    before = fa.get_tuning()
+    try:
+        fa.set_tuning(slot_skew=skew)
+        n, D = 300_007, 9
+        w = O.weights(D)
+        xs = host_clients(O, 51, D, n, False)
+        with fa.Aggregator(1) as agg:
+            agg.define(1, n, fa.F32, fa.F32, D, fa.FEDAVG)
+            for k in range(D):
+                agg.submit(1, k, xs[k], w[k])
+            assert_bits(agg.finalize(1), O.fedavg(xs, w))
+    finally:
+        fa.set_tuning(slot_skew=before["slot_skew"] or -1)

@@ -21,9 +21,9 @@ def main():
     fa.lib()
     workload = sys.argv[1] if len(sys.argv) > 1 else "northstar"
     D, n, i, o, _ = bench.WORKLOADS[workload]
-    setup = bench.Setup(fa, torch, D, n, i, o, 0)
+    setup = bench.Setup(fa, torch, D, n, i, o, 0, 0)
     stream = torch.cuda.Stream()
-    grid = list(itertools.product([128, 256], [0, 1024, 2048, 4096, 8192], [4, 8, 16], [0, 1]))
+    grid = list(itertools.product([64, 128, 256], [0, 2048, 8192], [4, 8, 16], [1, 2]))
     times = {g: [] for g in grid}
     for rnd in range(5):
         for g in grid:
