@@ -1,13 +1,14 @@
 #!/usr/bin/env python3
-"""Experiment (GPU box): does the placement of the D client buckets in HBM matter?
+"""Experiment (GPU box): is the FedAvg kernel's speed a property of the per-client
+skew or of where an allocation happens to land physically?
 
-All buckets allocated separately sit at the same offset modulo their (2 MiB
-aligned) size, so lane l of a wave reads the same low address bits from all U
-clients it loads at once.  This places the D buckets (and optionally the
-output) in one pool with a skew of `pad` elements between consecutive buckets
-and times the north-star reduce, interleaved in rounds in one process.
+For each skew (`pad` fp32 elements between consecutive client buckets inside
+one pool) this allocates REPS independent pools, interleaving allocation order,
+and times the reduce on every pool in interleaved rounds in one process.  A skew
+effect shows as a shift of all REPS pools; a placement effect as spread within
+one skew.
 
-  python tools/exp_layout.py [pads...]     (pads in fp32 elements; default set below)
+  python tools/exp_layout.py [n_log2] [reps] [pads...]
 """
 import json
 import os
@@ -22,43 +23,39 @@ def main():
     import torch
     fa = bench.load_pkg()
     fa.lib()
-    D, n = 32, 64 << 20
+    n = 1 << int(sys.argv[1]) if len(sys.argv) > 1 else 32 << 20
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+    pads = [int(x) for x in sys.argv[3:]] or [0, 64, 128, 1024]
+    D = 32
     w = bench.Setup._weights(D)
-    pads = [int(x) for x in sys.argv[1:]] or [0, 16, 32, 64, 128, 256, 512, 1024]
+    fa.set_tuning(block=128, max_blocks=-1, unroll=8, nontemporal=1)
     stream = torch.cuda.Stream()
-    sep_out = torch.empty(n, dtype=torch.float32, device="cuda")
     pools = {}
-    for pad in pads:
-        # D client slots then the output slot, all `n + pad` apart
-        pool = torch.empty((D + 1) * (n + pad), dtype=torch.float32, device="cuda")
-        clients = [pool[k * (n + pad): k * (n + pad) + n] for k in range(D)]
-        for k, c in enumerate(clients):
-            fa.fill_uniform(c, n, fa.F32, 0x5EED, k)
-        pools[pad] = (pool, clients, pool[D * (n + pad): D * (n + pad) + n])
+    for r in range(reps):
+        for pad in pads:
+            pool = torch.empty((D + 1) * (n + pad), dtype=torch.float32, device="cuda")
+            clients = [pool[k * (n + pad): k * (n + pad) + n] for k in range(D)]
+            for k, c in enumerate(clients):
+                fa.fill_uniform(c, n, fa.F32, 0x5EED, k)
+            pools[(pad, r)] = (pool, clients, pool[D * (n + pad): D * (n + pad) + n])
     torch.cuda.synchronize()
-    variants = [(pad, where, blk) for pad in pads for where in ("pool", "separate") for blk in (128, 256)]
-    results = {v: [] for v in variants}
+    results = {key: [] for key in pools}
     for rnd in range(4):
-        for v in variants:
-            pad, where, blk = v
-            fa.set_tuning(block=blk, max_blocks=-1, unroll=8, nontemporal=1)
-            out = pools[pad][2] if where == "pool" else sep_out
-            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
+        for key, (pool, clients, out) in pools.items():
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(4)]
             for a, b in ev:
                 a.record(stream)
-                fa.reduce_device(pools[pad][1], w, n, fa.F32, out, fa.F32, stream=stream)
+                fa.reduce_device(clients, w, n, fa.F32, out, fa.F32, stream=stream)
                 b.record(stream)
             torch.cuda.synchronize()
-            results[v] += [a.elapsed_time(b) for a, b in ev[1:]]
+            results[key] += [a.elapsed_time(b) for a, b in ev[1:]]
     algo = (D + 1) * n * 4
-    rows = []
-    for v, t in results.items():
-        med = statistics.median(t)
-        rows.append({"pad_elems": v[0], "out": v[1], "block": v[2], "ms_median": round(med, 4),
-                     "ms_min": round(min(t), 4), "GBs": round(algo / med / 1e6, 1)})
-    rows.sort(key=lambda r: r["ms_median"])
-    for r in rows:
-        print(json.dumps(r))
+    for pad in pads:
+        meds = [statistics.median(results[(pad, r)]) for r in range(reps)]
+        print(json.dumps({"pad_elems": pad, "pool_ms_medians": [round(m, 4) for m in meds],
+                          "GBs": [round(algo / m / 1e6) for m in meds],
+                          "base_mod_2MiB": [pools[(pad, r)][0].data_ptr() % (2 << 20) for r in range(reps)],
+                          "base_GiB": [round(pools[(pad, r)][0].data_ptr() / 2**30, 2) for r in range(reps)]}))
 
 
 if __name__ == "__main__":
