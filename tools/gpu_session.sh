@@ -51,6 +51,12 @@ for s in $STEPS; do
     layout)
         timeout -k 10 600 python tools/exp_layout.py > "$OUT/exp_layout.jsonl" 2> "$OUT/exp_layout.err"
         rc=$?; head -8 "$OUT/exp_layout.jsonl"; tail -3 "$OUT/exp_layout.err"; ok_or_fail $rc layout ;;
+    alloc)
+        timeout -k 10 600 python tools/exp_alloc.py > "$OUT/exp_alloc.jsonl" 2> "$OUT/exp_alloc.err"
+        rc=$?; cat "$OUT/exp_alloc.jsonl"; tail -3 "$OUT/exp_alloc.err"; ok_or_fail $rc alloc ;;
+    counters)
+        timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1
+        rc=$?; grep -i -E "utcl|tlb|translat" "$OUT/counters.txt" | head -30; ok_or_fail $rc counters ;;
     *)
         echo "unknown step $s" ;;
     esac
