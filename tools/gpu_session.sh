@@ -54,6 +54,13 @@ for s in $STEPS; do
     alloc)
         timeout -k 10 600 python tools/exp_alloc.py > "$OUT/exp_alloc.jsonl" 2> "$OUT/exp_alloc.err"
         rc=$?; cat "$OUT/exp_alloc.jsonl"; tail -3 "$OUT/exp_alloc.err"; ok_or_fail $rc alloc ;;
+    allocpmc)
+        timeout -k 10 600 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum --kernel-trace \
+            --output-format csv -d "$OUT/allocpmc1" -o run -- python3 tools/exp_alloc.py 25 3 > "$OUT/allocpmc1.jsonl" 2> "$OUT/allocpmc1.err"
+        rc=$?; cat "$OUT/allocpmc1.jsonl"; ok_or_fail $rc allocpmc1
+        timeout -k 10 600 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum --kernel-trace \
+            --output-format csv -d "$OUT/allocpmc2" -o run -- python3 tools/exp_alloc.py 25 3 > "$OUT/allocpmc2.jsonl" 2> "$OUT/allocpmc2.err"
+        rc=$?; cat "$OUT/allocpmc2.jsonl"; ok_or_fail $rc allocpmc2 ;;
     counters)
         timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1
         rc=$?; grep -i -E "utcl|tlb|translat" "$OUT/counters.txt" | head -30; ok_or_fail $rc counters ;;
