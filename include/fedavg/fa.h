@@ -137,6 +137,7 @@ typedef struct {
     int nontemporal; /* 0 default policy, 1 nt loads+stores, 2 nt loads only, 3 nt stores only; -1 keep */
     int slot_skew;   /* bytes between consecutive client slots beyond 4 KiB alignment (multiple of 16);
                         -1 = none; applies to buckets defined afterwards */
+    int lane_vectors; /* 16-byte vectors per lane per client in one tile: 1, 2 or 4 */
 } fa_tuning;
 int fa_set_tuning(const fa_tuning* t);
 int fa_get_tuning(fa_tuning* t);

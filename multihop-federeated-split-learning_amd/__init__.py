@@ -34,7 +34,7 @@ class FaError(RuntimeError):
 
 class _Tuning(ctypes.Structure):
     _fields_ = [("block", ctypes.c_int), ("max_blocks", ctypes.c_int), ("unroll", ctypes.c_int),
-                ("nontemporal", ctypes.c_int), ("slot_skew", ctypes.c_int)]
+                ("nontemporal", ctypes.c_int), ("slot_skew", ctypes.c_int), ("lane_vectors", ctypes.c_int)]
 
 
 def build():
@@ -140,11 +140,11 @@ def get_tuning():
     t = _Tuning()
     check(lib().fa_get_tuning(ctypes.byref(t)))
     return {"block": t.block, "max_blocks": t.max_blocks, "unroll": t.unroll, "nontemporal": t.nontemporal,
-            "slot_skew": t.slot_skew}
+            "slot_skew": t.slot_skew, "lane_vectors": t.lane_vectors}
 
 
-def set_tuning(block=0, max_blocks=0, unroll=0, nontemporal=-1, slot_skew=0):
-    t = _Tuning(block, max_blocks, unroll, nontemporal, slot_skew)
+def set_tuning(block=0, max_blocks=0, unroll=0, nontemporal=-1, slot_skew=0, lane_vectors=0):
+    t = _Tuning(block, max_blocks, unroll, nontemporal, slot_skew, lane_vectors)
     check(lib().fa_set_tuning(ctypes.byref(t)))
 
 

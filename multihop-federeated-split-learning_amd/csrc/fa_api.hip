@@ -28,7 +28,7 @@
 namespace {
 
 thread_local std::string g_err;
-fa::Tuning g_tuning{128, 0, 8, 1};
+fa::Tuning g_tuning{128, 0, 8, 1, 1};
 // Byte skew between consecutive client slots of one bucket (see slot_stride).
 size_t g_slot_skew = 512;
 
@@ -317,6 +317,11 @@ int fa_set_tuning(const fa_tuning* t) {
         if (t->unroll != 4 && t->unroll != 8 && t->unroll != 16) return fail(FA_ERR_ARG, "unroll must be 4/8/16");
         nt.unroll = t->unroll;
     }
+    if (t->lane_vectors) {
+        if (t->lane_vectors != 1 && t->lane_vectors != 2 && t->lane_vectors != 4)
+            return fail(FA_ERR_ARG, "lane_vectors must be 1/2/4");
+        nt.lane_vectors = t->lane_vectors;
+    }
     if (t->slot_skew) {
         if (t->slot_skew > 0 && t->slot_skew % 16) return fail(FA_ERR_ARG, "slot_skew must be a multiple of 16");
         g_slot_skew = t->slot_skew < 0 ? 0 : (size_t)t->slot_skew;
@@ -337,6 +342,7 @@ int fa_get_tuning(fa_tuning* t) {
     t->unroll = g_tuning.unroll;
     t->nontemporal = g_tuning.nontemporal;
     t->slot_skew = (int)g_slot_skew;
+    t->lane_vectors = g_tuning.lane_vectors;
     return FA_OK;
 }
 

@@ -127,51 +127,81 @@ __device__ __forceinline__ void chain_scalar_edges(const ClientTable& t, int nc,
     }
 }
 
-// Vector body over nvec lane-vectors starting at element `head`.
-// POL: bit 0 = non-temporal loads, bit 1 = non-temporal stores.
-template <typename IN, typename OUT, int U, int POL, bool INIT>
+// Chain over L lane-vectors of one thread: vector j is v0 + j * vstep (elements head + v * V ...).
+template <typename IN, typename OUT, int U, int POL, bool INIT, int L>
+__device__ __forceinline__ void chain_vectors(const ClientTable& t, int nc, const float* init, void* out,
+                                              int64_t head, int64_t v0, int64_t vstep) {
+    constexpr int V = In<IN>::kVec;
+    constexpr bool NTL = (POL & 1) != 0;
+    float acc[L][V];
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+        const int64_t e = head + (v0 + l * vstep) * V;
+        if constexpr (INIT) {
+#pragma unroll
+            for (int j = 0; j < V; j += 4) {
+                u32x4 r = ld16<NTL>(init + e + j);
+                acc[l][j] = __uint_as_float(r.x); acc[l][j + 1] = __uint_as_float(r.y);
+                acc[l][j + 2] = __uint_as_float(r.z); acc[l][j + 3] = __uint_as_float(r.w);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < V; ++j) acc[l][j] = 0.0f;
+        }
+    }
+    int k = 0;
+    for (; k + U <= nc; k += U) {
+        u32x4 raw[U][L];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int l = 0; l < L; ++l)
+                raw[u][l] = ld16<NTL>(reinterpret_cast<const IN*>(t.src[k + u]) + head + (v0 + l * vstep) * V);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float w = t.w[k + u];
+#pragma unroll
+            for (int l = 0; l < L; ++l) {
+                float x[V];
+                In<IN>::widen(raw[u][l], x);
+#pragma unroll
+                for (int j = 0; j < V; ++j) acc[l][j] = __builtin_fmaf(x[j], w, acc[l][j]);
+            }
+        }
+    }
+    for (; k < nc; ++k) {
+        const float w = t.w[k];
+#pragma unroll
+        for (int l = 0; l < L; ++l) {
+            float x[V];
+            In<IN>::widen(ld16<NTL>(reinterpret_cast<const IN*>(t.src[k]) + head + (v0 + l * vstep) * V), x);
+#pragma unroll
+            for (int j = 0; j < V; ++j) acc[l][j] = __builtin_fmaf(x[j], w, acc[l][j]);
+        }
+    }
+#pragma unroll
+    for (int l = 0; l < L; ++l)
+        Out<OUT>::template store<V, (POL & 2) != 0>(out, head + (v0 + l * vstep) * V, acc[l]);
+}
+
+// Vector body over nvec lane-vectors starting at element `head`.  A workgroup
+// tile is blockDim * L consecutive lane-vectors: every client bucket is read
+// in L * 1 KiB contiguous pieces per wave (L > 1 raises DRAM row locality and
+// the loads in flight per lane).  POL: bit 0 = non-temporal loads, bit 1 =
+// non-temporal stores.
+template <typename IN, typename OUT, int U, int POL, bool INIT, int L>
 __global__ __launch_bounds__(256) void fedavg_chain_kernel(const ClientTable t, int nc, const float* init, void* out,
                                                            int64_t head, int64_t nvec, int64_t n) {
     constexpr int V = In<IN>::kVec;
     chain_scalar_edges<IN, OUT, INIT>(t, nc, init, out, head, head + nvec * V, n);
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
-        const int64_t e = head + v * V;  // first element owned by this lane
-        float acc[V];
-        if constexpr (INIT) {
-#pragma unroll
-            for (int j = 0; j < V; j += 4) {
-                u32x4 r = ld16<(POL & 1) != 0>(init + e + j);
-                acc[j] = __uint_as_float(r.x); acc[j + 1] = __uint_as_float(r.y);
-                acc[j + 2] = __uint_as_float(r.z); acc[j + 3] = __uint_as_float(r.w);
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < V; ++j) acc[j] = 0.0f;
-        }
-        int k = 0;
-        for (; k + U <= nc; k += U) {
-            u32x4 raw[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) raw[u] = ld16<(POL & 1) != 0>(reinterpret_cast<const IN*>(t.src[k + u]) + e);
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                float x[V];
-                In<IN>::widen(raw[u], x);
-                const float w = t.w[k + u];
-#pragma unroll
-                for (int j = 0; j < V; ++j) acc[j] = __builtin_fmaf(x[j], w, acc[j]);
-            }
-        }
-        for (; k < nc; ++k) {
-            float x[V];
-            In<IN>::widen(ld16<(POL & 1) != 0>(reinterpret_cast<const IN*>(t.src[k]) + e), x);
-            const float w = t.w[k];
-#pragma unroll
-            for (int j = 0; j < V; ++j) acc[j] = __builtin_fmaf(x[j], w, acc[j]);
-        }
-        Out<OUT>::template store<V, (POL & 2) != 0>(out, e, acc);
-    }
+    const int64_t tile = (int64_t)blockDim.x * L;
+    const int64_t full_tiles = nvec / tile;
+    for (int64_t b = blockIdx.x; b < full_tiles; b += gridDim.x)
+        chain_vectors<IN, OUT, U, POL, INIT, L>(t, nc, init, out, head, b * tile + threadIdx.x, blockDim.x);
+    // remainder (< one tile): one vector per thread, spread over the grid
+    for (int64_t v = full_tiles * tile + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec;
+         v += (int64_t)gridDim.x * blockDim.x)
+        chain_vectors<IN, OUT, U, POL, INIT, 1>(t, nc, init, out, head, v, 0);
 }
 
 // Fully general path (pointers whose 16-byte phases differ): one element per lane.
@@ -253,17 +283,27 @@ inline int64_t grid_for(int64_t work, const Tuning& tu) {
     return g;
 }
 
+template <typename IN, typename OUT, int U, int POL, int L>
+hipError_t launch_chain_l(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
+                          int64_t n, const Tuning& tu, hipStream_t s) {
+    int64_t g = grid_for(nvec > 0 ? (nvec + L - 1) / L : 1, tu);
+    if (init)
+        hipLaunchKernelGGL((fedavg_chain_kernel<IN, OUT, U, POL, true, L>), dim3((unsigned)g), dim3(tu.block), 0, s,
+                           t, nc, init, out, head, nvec, n);
+    else
+        hipLaunchKernelGGL((fedavg_chain_kernel<IN, OUT, U, POL, false, L>), dim3((unsigned)g), dim3(tu.block), 0, s,
+                           t, nc, init, out, head, nvec, n);
+    return hipGetLastError();
+}
+
 template <typename IN, typename OUT, int U, int POL>
 hipError_t launch_chain_u(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
                           int64_t n, const Tuning& tu, hipStream_t s) {
-    const int64_t g = grid_for(nvec > 0 ? nvec : 1, tu);
-    if (init)
-        hipLaunchKernelGGL((fedavg_chain_kernel<IN, OUT, U, POL, true>), dim3((unsigned)g), dim3(tu.block), 0, s, t,
-                           nc, init, out, head, nvec, n);
-    else
-        hipLaunchKernelGGL((fedavg_chain_kernel<IN, OUT, U, POL, false>), dim3((unsigned)g), dim3(tu.block), 0, s, t,
-                           nc, init, out, head, nvec, n);
-    return hipGetLastError();
+    switch (tu.lane_vectors) {
+        case 2: return launch_chain_l<IN, OUT, U, POL, 2>(t, nc, init, out, head, nvec, n, tu, s);
+        case 4: return launch_chain_l<IN, OUT, (U > 8 ? 8 : U), POL, 4>(t, nc, init, out, head, nvec, n, tu, s);
+        default: return launch_chain_l<IN, OUT, U, POL, 1>(t, nc, init, out, head, nvec, n, tu, s);
+    }
 }
 
 template <typename IN, typename OUT, int POL>
@@ -342,7 +382,7 @@ hipError_t launch_literal(const void* x, fa_dtype in, void* out, fa_dtype outdt,
 
 hipError_t launch_fill(void* dst, int64_t n, fa_dtype dt, uint64_t seed, uint32_t client, uint64_t idx0,
                        hipStream_t s) {
-    Tuning tu{256, 8192, 8, 0};
+    Tuning tu{256, 8192, 8, 0, 1};
     const int64_t g = grid_for(n, tu);
     if (dt == FA_F32)
         hipLaunchKernelGGL((fill_kernel<float>), dim3((unsigned)g), dim3(256), 0, s, dst, n, seed, client, idx0);

@@ -67,7 +67,7 @@ def test_tuning_roundtrip(fa):
     before = fa.get_tuning()
     fa.set_tuning(block=128, unroll=16, nontemporal=0)
     assert fa.get_tuning() == {"block": 128, "max_blocks": before["max_blocks"], "unroll": 16, "nontemporal": 0,
-                               "slot_skew": before["slot_skew"]}
+                               "slot_skew": before["slot_skew"], "lane_vectors": before["lane_vectors"]}
     fa.set_tuning(slot_skew=-1)
     assert fa.get_tuning()["slot_skew"] == 0
     with pytest.raises(fa.FaError):

@@ -153,17 +153,20 @@ def test_literal_mode(fa, O, torch_gpu, bf16):
 
 @pytest.mark.parametrize("tuning", [dict(block=64, unroll=4, nontemporal=0), dict(block=128, unroll=16, nontemporal=1),
                                     dict(block=256, unroll=8, nontemporal=0, max_blocks=7),
-                                    dict(block=256, unroll=16, nontemporal=1, max_blocks=1)])
+                                    dict(block=256, unroll=16, nontemporal=1, max_blocks=1),
+                                    dict(block=128, unroll=8, nontemporal=2, lane_vectors=2),
+                                    dict(block=64, unroll=16, nontemporal=3, lane_vectors=4, max_blocks=5),
+                                    dict(block=256, unroll=4, nontemporal=1, lane_vectors=4)])
 def test_tuning_variants_same_bits(fa, O, torch_gpu, tuning):
     torch = torch_gpu
     before = fa.get_tuning()
     try:
         fa.set_tuning(**tuning)
-        n, D = 200_003, 19
-        w = O.weights(D)
-        xs = host_clients(O, 8, D, n, False)
-        clients = [filled(fa, torch, n, False, 8, k) for k in range(D)]
-        assert_bits(run_fedavg(fa, torch, clients, w, n, False, False), O.fedavg(xs, w))
+        for n, D, bf16 in [(200_003, 19, False), (1_048_573, 33, False), (3001, 3, False), (250_001, 21, True)]:
+            w = O.weights(D)
+            xs = host_clients(O, 8, D, n, bf16)
+            clients = [filled(fa, torch, n, bf16, 8, k) for k in range(D)]
+            assert_bits(run_fedavg(fa, torch, clients, w, n, bf16, bf16), O.fedavg(xs, w, out_dtype="bf16" if bf16 else "f32"))
     finally:
         fa.set_tuning(**before)
 

@@ -21,26 +21,32 @@ def main():
     fa.lib()
     workload = sys.argv[1] if len(sys.argv) > 1 else "northstar"
     D, n, i, o, _ = bench.WORKLOADS[workload]
-    setup = bench.Setup(fa, torch, D, n, i, o, 0, 0)
+    pools = int(os.environ.get("SWEEP_POOLS", "3"))
+    setups = [bench.Setup(fa, torch, D, n, i, o, 0, 0) for _ in range(pools)]  # placement varies per pool
+    setup = setups[0]
     stream = torch.cuda.Stream()
-    grid = list(itertools.product([64, 128, 256], [0, 2048, 8192], [4, 8, 16], [1, 2]))
-    times = {g: [] for g in grid}
-    for rnd in range(5):
+    grid = list(itertools.product([128, 256], [0], [4, 8, 16], [1, 2], [1, 2, 4]))
+    times = {(g, p): [] for g in grid for p in range(pools)}
+    for rnd in range(3):
         for g in grid:
-            fa.set_tuning(block=g[0], max_blocks=g[1] if g[1] else -1, unroll=g[2], nontemporal=g[3])
-            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(6)]
-            for a, b in ev:
-                a.record(stream)
-                setup.launch(0, stream)
-                b.record(stream)
-            torch.cuda.synchronize()
-            times[g] += [a.elapsed_time(b) for a, b in ev[1:]]
+            fa.set_tuning(block=g[0], max_blocks=g[1] if g[1] else -1, unroll=g[2], nontemporal=g[3],
+                          lane_vectors=g[4])
+            for p, st in enumerate(setups):
+                ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(4)]
+                for a, b in ev:
+                    a.record(stream)
+                    st.launch(0, stream)
+                    b.record(stream)
+                torch.cuda.synchronize()
+                times[(g, p)] += [a.elapsed_time(b) for a, b in ev[1:]]
     rows = []
-    for g, t in times.items():
-        med = statistics.median(t)
-        rows.append({"block": g[0], "max_blocks": g[1], "unroll": g[2], "nt": g[3], "ms_median": round(med, 4),
-                     "ms_min": round(min(t), 4), "GBs": round(setup.algo_bytes() / med / 1e6, 1)})
-    rows.sort(key=lambda r: r["ms_median"])
+    for g in grid:
+        meds = [statistics.median(times[(g, p)]) for p in range(pools)]
+        med = statistics.mean(meds)
+        rows.append({"block": g[0], "max_blocks": g[1], "unroll": g[2], "nt": g[3], "lane_vectors": g[4],
+                     "ms_mean_of_pool_medians": round(med, 4), "pool_ms": [round(m, 4) for m in meds],
+                     "GBs": round(setup.algo_bytes() / med / 1e6, 1)})
+    rows.sort(key=lambda r: r["ms_mean_of_pool_medians"])
     for r in rows:
         print(json.dumps(r))
 
