@@ -71,6 +71,33 @@ __global__ __launch_bounds__(256) void mstream_read_kernel(Table t, int64_t nvec
     }
 }
 
+// The same 32-stream pattern WITH the per-lane result store (STORE: 0 none, 1 nt store, 2 plain store,
+// 3 store into a 1 MiB L2-resident window): isolates what the output stream costs.
+template <int STORE, int U>
+__global__ __launch_bounds__(128) void mstream_store_kernel(Table t, int64_t nvec, f32x4* out) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+        f32x4 acc = {0, 0, 0, 0};
+        for (int k = 0; k < 32; k += U) {
+            f32x4 x[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) x[u] = __builtin_nontemporal_load(t.p[k + u] + v);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc = acc * 0.5f + x[u];
+        }
+        if constexpr (STORE == 0) {
+            float s = acc.x + acc.y + acc.z + acc.w;
+            if (s == 12345.678f) out[threadIdx.x] = acc;
+        } else if constexpr (STORE == 1) {
+            __builtin_nontemporal_store(acc, out + v);
+        } else if constexpr (STORE == 2) {
+            out[v] = acc;
+        } else {
+            out[v & 65535] = acc;
+        }
+    }
+}
+
 template <typename F>
 double time_ms(F f, int reps) {
     hipEvent_t a, b;
@@ -122,6 +149,25 @@ int main() {
     for (int k = 0; k < 32; ++k) t.p[k] = a + k * per;
     double m = time_ms([&] { mstream_read_kernel<<<(unsigned)(per / 256), 256>>>(t, per, sink); }, 10);
     printf(",\"mstream32_read_GBs\":%.1f", bytes / m / 1e6);
+    // output stream ablation: 32 x 128 MiB clients + 128 MiB output (in b)
+    {
+        Table t2;
+        const int64_t per2 = nvec / 64;  // 128 MiB per client
+        for (int k = 0; k < 32; ++k) t2.p[k] = a + k * per2;
+        const unsigned g = (unsigned)(per2 / 128);
+        const double rd = 32.0 * per2 * 16, wr = per2 * 16.0;
+        double s0 = 0, s1 = 0, s2 = 0, s3 = 0, s16 = 0;
+        for (int rep = 0; rep < 3; ++rep) {  // interleaved
+            s0 += time_ms([&] { mstream_store_kernel<0, 8><<<g, 128>>>(t2, per2, b); }, 5);
+            s1 += time_ms([&] { mstream_store_kernel<1, 8><<<g, 128>>>(t2, per2, b); }, 5);
+            s2 += time_ms([&] { mstream_store_kernel<2, 8><<<g, 128>>>(t2, per2, b); }, 5);
+            s3 += time_ms([&] { mstream_store_kernel<3, 8><<<g, 128>>>(t2, per2, b); }, 5);
+            s16 += time_ms([&] { mstream_store_kernel<1, 16><<<g, 128>>>(t2, per2, b); }, 5);
+        }
+        printf(",\"store_ablation_ms\":{\"no_store\":%.4f,\"nt_store\":%.4f,\"plain_store\":%.4f,"
+               "\"l2_window_store\":%.4f,\"nt_store_u16\":%.4f,\"algo_GBs_nt_store\":%.1f,\"read_GBs_no_store\":%.1f}",
+               s0 / 3, s1 / 3, s2 / 3, s3 / 3, s16 / 3, (rd + wr) / (s1 / 3) / 1e6, rd / (s0 / 3) / 1e6);
+    }
     printf(",\"copy_GBs\":%.1f,\"write_GBs\":%.1f,\"unit\":\"GB/s (1e9 B/s), median of 10, 8 GiB read / 4 GiB copy+write\"}\n",
            2.0 * (bytes / 2) / c / 1e6, (bytes / 2) / w / 1e6);
     return 0;
