@@ -61,6 +61,11 @@ for s in $STEPS; do
         timeout -k 10 600 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum --kernel-trace \
             --output-format csv -d "$OUT/allocpmc2" -o run -- python3 tools/exp_alloc.py 25 3 > "$OUT/allocpmc2.jsonl" 2> "$OUT/allocpmc2.err"
         rc=$?; cat "$OUT/allocpmc2.jsonl"; ok_or_fail $rc allocpmc2 ;;
+    stride)
+        timeout -k 10 600 python tools/exp_stride.py 25 > "$OUT/exp_stride.jsonl" 2> "$OUT/exp_stride.err"
+        rc=$?; cat "$OUT/exp_stride.jsonl"; tail -2 "$OUT/exp_stride.err"; ok_or_fail $rc stride
+        timeout -k 10 600 python tools/exp_stride.py 26 >> "$OUT/exp_stride.jsonl" 2>> "$OUT/exp_stride.err"
+        rc=$?; tail -2 "$OUT/exp_stride.jsonl"; ok_or_fail $rc stride26 ;;
     counters)
         timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1
         rc=$?; grep -i -E "utcl|tlb|translat" "$OUT/counters.txt" | head -30; ok_or_fail $rc counters ;;
