@@ -66,6 +66,9 @@ for s in $STEPS; do
         rc=$?; cat "$OUT/exp_stride.jsonl"; tail -2 "$OUT/exp_stride.err"; ok_or_fail $rc stride
         timeout -k 10 600 python tools/exp_stride.py 26 >> "$OUT/exp_stride.jsonl" 2>> "$OUT/exp_stride.err"
         rc=$?; tail -2 "$OUT/exp_stride.jsonl"; ok_or_fail $rc stride26 ;;
+    map)
+        timeout -k 10 600 python tools/exp_map.py 200 > "$OUT/exp_map.jsonl" 2> "$OUT/exp_map.err"
+        rc=$?; cat "$OUT/exp_map.jsonl"; tail -2 "$OUT/exp_map.err"; ok_or_fail $rc map ;;
     counters)
         timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1
         rc=$?; grep -i -E "utcl|tlb|translat" "$OUT/counters.txt" | head -30; ok_or_fail $rc counters ;;
