@@ -7,13 +7,14 @@ already resident in HBM: the ordered weighted-sum reduction of D client buckets
 libfa.so's C ABI (fa_reduce_device).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload northstar|c2|c3]
-                  [--layout range|client-rs] [--no-cpu-baseline] [--no-secondary]
+                  [--layout range|rs|chain] [--no-cpu-baseline] [--no-secondary]
 
 N > 1 runs one process per GPU (torch.distributed.run sets RANK/LOCAL_RANK/
 WORLD_SIZE).  Layout "range" (default) shards every bucket by element range:
 each rank reduces its own 256 MiB slice of all D clients, no collective
-(weak scaling).  Layout "client-rs" gives each rank 32 whole clients and
-combines the fp32 partials with an RCCL reduce-scatter over xGMI.
+(weak scaling).  Layouts "rs" and "chain" give each rank 32 whole clients:
+"rs" combines the fp32 partials with an RCCL reduce-scatter over xGMI, "chain"
+hands the ordered fp32 chain rank to rank (bit-exact) over RCCL p2p.
 
 value = bytes of client input reduced by all ranks / max-over-ranks wall time,
 in GiB/s (D * N * sizeof(in) / t / 2^30).  roofline.achieved = algorithmic HBM
@@ -118,7 +119,8 @@ class Setup:
     fa_reduce_part -- the device-resident round of the aggregator.
     """
 
-    def __init__(self, fa, torch, D, n, in_dt, out_dt, rank, device, seed=0x5EED, min_rotate_bytes=ROTATE_MIN_BYTES):
+    def __init__(self, fa, torch, D, n, in_dt, out_dt, elem0, device, client0=0, seed=0x5EED,
+                 min_rotate_bytes=ROTATE_MIN_BYTES):
         self.fa, self.torch = fa, torch
         self.D, self.n = D, n
         self.in_dt = fa.F32 if in_dt == "f32" else fa.BF16
@@ -132,8 +134,8 @@ class Setup:
             self.agg.define(s, n, self.in_dt, self.out_dt, D, fa.FEDAVG)
             for k in range(D):
                 ptr, cnt, _ = self.agg.slot(s, 0, k)
-                # element index offset by the rank's range: ranks hold disjoint slices of one bucket
-                fa.fill_uniform(ptr, cnt, self.in_dt, seed + s, k, idx0=rank * n)
+                # global client id and element offset: ranks hold disjoint clients or slices of one bucket
+                fa.fill_uniform(ptr, cnt, self.in_dt, seed + s, client0 + k, idx0=elem0)
         self.w = self._weights(D)
 
     @staticmethod
@@ -188,11 +190,10 @@ def timed_loop(torch, setup, steps, warmup, stream, dist, barrier):
     return wall, kern_ms
 
 
-def run_rs_step(fa, torch, setup, cl, partial, shard, stream, dist):
-    """client-rs: local chain over this rank's clients into fp32 partials, then RCCL reduce-scatter."""
-    fa.reduce_device(cl, setup.w, setup.n, setup.in_dt, partial, fa.F32, fa.FEDAVG, stream=stream)
-    with torch.cuda.stream(stream):
-        dist.reduce_scatter_tensor(shard, partial, op=dist.ReduceOp.SUM)
+def load_shard():
+    load_pkg()
+    import importlib
+    return importlib.import_module("mhfsl_amd.shard")
 
 
 def main():
@@ -201,7 +202,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="northstar", choices=sorted(WORKLOADS))
-    ap.add_argument("--layout", default="range", choices=["range", "client-rs"])
+    ap.add_argument("--layout", default="range", choices=["range", "rs", "chain"])
+    ap.add_argument("--chunks", type=int, default=16, help="chain layout: pipeline chunks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--tune", default="", help="block,max_blocks,unroll,nontemporal")
@@ -221,6 +223,7 @@ def main():
     import torch
     import torch.distributed as dist
     fa = load_pkg()
+    shard = load_shard()
     torch.cuda.set_device(local_rank)
     fa.lib()
     if args.tune:
@@ -236,39 +239,52 @@ def main():
             pass
 
     stream = torch.cuda.Stream()
-    setup = Setup(fa, torch, D, n, in_dt, out_dt, rank, local_rank)
+    # weak scaling: per-rank work is fixed -- range: a 256 MiB slice of every one of D buckets;
+    # rs / chain: D whole 256 MiB buckets (global clients rank*D .. rank*D+D-1 of D*world).
+    if args.layout == "range":
+        setup = Setup(fa, torch, D, n, in_dt, out_dt, rank * n, local_rank)
+    else:
+        setup = Setup(fa, torch, D, n, in_dt, out_dt, 0, local_rank, client0=rank * D)
+        setup.w = Setup._weights(D * world)[rank * D:(rank + 1) * D]
     torch.cuda.synchronize()
 
+    # the dominant kernel alone (roofline), HIP events on its stream
+    wall_k, kern_ms = timed_loop(torch, setup, args.steps, args.warmup, stream, dist, barrier)
     if args.layout == "range":
-        wall, kern_ms = timed_loop(torch, setup, args.steps, args.warmup, stream, dist, barrier)
-        units_bytes = setup.input_bytes() * world
+        wall = wall_k
         layout_desc = "range-sharded: each rank owns %d of %d elements of every bucket, no collective" % (
             n, n * world)
     else:
-        partial = torch.empty(n, dtype=torch.float32, device="cuda")
-        shard = torch.empty(n // world, dtype=torch.float32, device="cuda")
+        reducer = shard.fa_reducer(fa, setup.in_dt, stream)
         cl = setup.clients()
+        dev = torch.device("cuda", local_rank)
+        npad = -(-n // (world * shard.UNIT)) * world * shard.UNIT
+        assert npad == n, "workload size must be a multiple of world * 64"
+
+        def step():
+            with torch.cuda.stream(stream):
+                if args.layout == "rs":
+                    return shard.reduce_rs(reducer, dist, cl, setup.w, n, dev) if world > 1 else reducer(
+                        cl, setup.w, n)
+                return shard.reduce_chain(reducer, dist, cl, setup.w, n, dev, chunks=args.chunks,
+                                          itemsize=setup.s_in) if world > 1 else reducer(cl, setup.w, n)
         for _ in range(args.warmup):
-            run_rs_step(fa, torch, setup, cl, partial, shard, stream, dist)
+            step()
         torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
         t0 = time.perf_counter()
-        for i in range(args.steps):
-            evs[i][0].record(stream)
-            fa.reduce_device(cl, setup.w, n, setup.in_dt, partial, fa.F32, fa.FEDAVG, stream=stream)
-            evs[i][1].record(stream)
-            with torch.cuda.stream(stream):
-                if world > 1:
-                    dist.reduce_scatter_tensor(shard, partial, op=dist.ReduceOp.SUM)
+        for _ in range(args.steps):
+            step()
         torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
-        kern_ms = [a.elapsed_time(b) for a, b in evs]
-        units_bytes = setup.input_bytes() * world
-        layout_desc = "client-sharded: each rank reduces %d whole clients into fp32 partials, RCCL reduce-scatter" % D
+        layout_desc = ("client-sharded: each rank reduces its %d whole clients into fp32 partials, RCCL "
+                       "reduce-scatter over xGMI" % D if args.layout == "rs" else
+                       "client-sharded, bit-exact: the fp32 chain is handed rank to rank over RCCL p2p in %d "
+                       "chunks, last rank scatters the ranges" % args.chunks)
+    units_bytes = setup.input_bytes() * world
 
     if world > 1:
         t = torch.tensor([wall], dtype=torch.float64, device="cuda")
@@ -291,11 +307,10 @@ def main():
         "vs_baseline": None,
         "dtype": in_dt,
         "data": "synthetic (counter-based splitmix64 uniform[-1,1), generated in HBM)",
-        "config": {"workload": args.workload, "description": desc, "clients": D * (world if args.layout ==
-                                                                                     "client-rs" else 1),
+        "config": {"workload": args.workload, "description": desc,
+                   "clients": D * (world if args.layout != "range" else 1),
                    "elems_per_client": n * (world if args.layout == "range" else 1), "in_dtype": in_dt,
-                   "out_dtype": out_dt, "layout": layout_desc, "parallelism": "%s%d" % (
-                       "range" if args.layout == "range" else "rs", world),
+                   "out_dtype": out_dt, "layout": layout_desc, "parallelism": "%s%d" % (args.layout, world),
                    "tuning": fa.get_tuning(), "input_sets_rotated": setup.nsets},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -323,7 +338,6 @@ def main():
                          "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          "input_sets_rotated": s.nsets}
             s.close()
-            del s
         line["secondary"] = sec
 
     if rank == 0:

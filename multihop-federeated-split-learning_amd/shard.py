@@ -1,0 +1,131 @@
+"""Multi-GPU layouts of the aggregation round, one process per GPU.
+
+The reference has one aggregator process reducing every receipt itself
+(pipeline_simulation/aggregator.cpp:59-150); on a node of G GPUs the buckets
+are partitioned instead:
+
+* ``range``  -- rank r owns elements [lo_r, hi_r) of EVERY client bucket and
+  reduces them locally.  No collective; bit-exact with the oracle.
+* ``rs``     -- rank r owns clients [c_r, c_{r+1}) (whole buckets), reduces them
+  into an fp32 partial of the full bucket, and an RCCL reduce-scatter
+  (``torch.distributed.reduce_scatter_tensor``, backend "nccl" = RCCL over
+  xGMI) sums the partials so rank r ends with elements [lo_r, hi_r).  The
+  summation order changes: parity is by tolerance (1e-6 relative to
+  sum_k |w_k x_k|).
+* ``chain``  -- client-sharded like ``rs`` but bit-exact: the ordered FMA chain
+  is passed rank to rank (rank r continues from rank r-1's fp32 accumulator via
+  fa_reduce_device's d_init), pipelined over element chunks with point-to-point
+  send/recv, and the last rank scatters each rank's range to it.
+
+The local reduction is a callable so the exchange logic runs unchanged on CPU
+tensors under gloo in tests; on the GPU it is ``fa_reducer`` (libfa.so).
+"""
+import numpy as np
+
+UNIT = 64  # shard boundaries in elements (keeps every shard's 16-byte phase)
+
+
+def range_bounds(n, world, rank, unit=UNIT):
+    """[lo, hi) of bucket elements owned by `rank` (shards are multiples of `unit` except the last)."""
+    per_rank = (n + world - 1) // world
+    per = (per_rank + unit - 1) // unit * unit
+    lo = min(n, rank * per)
+    return lo, min(n, lo + per)
+
+
+def client_bounds(n_clients, world, rank):
+    """[c0, c1) of client slots held by `rank` (contiguous, balanced, client order preserved)."""
+    base, extra = divmod(n_clients, world)
+    c0 = rank * base + min(rank, extra)
+    return c0, c0 + base + (1 if rank < extra else 0)
+
+
+def fa_reducer(fa, in_dtype, stream=None):
+    """Local reduction on the GPU through libfa.so: (clients, weights, n, init) -> fp32 tensor."""
+    import torch
+
+    def reduce(clients, weights, n, init=None, out=None):
+        if out is None:
+            out = torch.empty(n, dtype=torch.float32, device="cuda")
+        fa.reduce_device(clients, weights, n, in_dtype, out, fa.F32, fa.FEDAVG, init=init, stream=stream)
+        return out
+    return reduce
+
+
+def reduce_range(reduce, clients, weights, lo, hi):
+    """`clients` are this rank's slices [lo, hi) of every bucket."""
+    return reduce(clients, weights, hi - lo)
+
+
+def reduce_rs(reduce, dist, clients, weights, n, device):
+    """Client-sharded partial + reduce-scatter; returns this rank's [lo, hi) of the sum.
+
+    `n` must be a multiple of world * UNIT (pad the bucket) so that reduce-scatter
+    shards are equal and line up with range_bounds.
+    """
+    import torch
+    world, rank = dist.get_world_size(), dist.get_rank()
+    assert n % (world * UNIT) == 0, "pad the bucket to a multiple of world * %d" % UNIT
+    if clients:
+        partial = reduce(clients, weights, n)
+    else:  # a rank without clients contributes zeros
+        partial = torch.zeros(n, dtype=torch.float32, device=device)
+    lo, hi = range_bounds(n, world, rank)
+    shard = torch.empty(hi - lo, dtype=torch.float32, device=device)
+    dist.reduce_scatter_tensor(shard, partial, op=dist.ReduceOp.SUM)
+    return shard
+
+
+def _piece(x, a, b, itemsize):
+    """Elements [a, b) of a client bucket given as a tensor or a raw device address."""
+    return x + a * itemsize if isinstance(x, int) else x[a:b]
+
+
+def reduce_chain(reduce, dist, clients, weights, n, device, chunks=8, itemsize=4):
+    """Bit-exact client-sharded reduction: the fp32 chain is handed rank r -> r+1 chunk by chunk.
+
+    Rank r holds clients in global order after rank r-1's.  Returns this rank's
+    [lo, hi) of the ordered chain over ALL clients (== the single-GPU result).
+    """
+    import torch
+    world, rank = dist.get_world_size(), dist.get_rank()
+    edges = sorted({min(n, (n * c // chunks) // UNIT * UNIT) for c in range(chunks)} | {n})
+    acc = torch.empty(n, dtype=torch.float32, device=device)
+    sends = []
+    for a, b in zip(edges, edges[1:]):
+        init = None
+        if rank > 0:
+            dist.recv(acc[a:b], src=rank - 1)
+            init = acc[a:b]
+        if clients:
+            acc[a:b] = reduce([_piece(x, a, b, itemsize) for x in clients], weights, b - a, init=init)
+        elif rank == 0:
+            acc[a:b].zero_()  # the chain starts at +0
+        if rank < world - 1:
+            sends.append(dist.isend(acc[a:b], dst=rank + 1))
+    for r in sends:
+        r.wait()
+    # the last rank holds the full chain: it sends every rank its range
+    lo, hi = range_bounds(n, world, rank)
+    mine = torch.empty(hi - lo, dtype=torch.float32, device=device)
+    last = world - 1
+    if rank == last:
+        outs = []
+        for r in range(world - 1):
+            rlo, rhi = range_bounds(n, world, r)
+            if rhi > rlo:
+                outs.append(dist.isend(acc[rlo:rhi].contiguous(), dst=r))
+        mine.copy_(acc[lo:hi])
+        for o in outs:
+            o.wait()
+    elif hi > lo:
+        dist.recv(mine, src=last)
+    return mine
+
+
+def tolerance_ok(got, ref, xs_abs_weighted, rel=1e-6):
+    """|got - ref| <= rel * sum_k |w_k x_k| elementwise (the rs layout's parity bound)."""
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    bound = rel * np.asarray(xs_abs_weighted, np.float64) + 1e-30
+    return bool(np.all(np.abs(got - ref) <= bound)), float(np.max(np.abs(got - ref) / bound))
