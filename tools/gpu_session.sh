@@ -39,6 +39,11 @@ for s in $STEPS; do
                 python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-secondary > "$OUT/pmc_$c.json" 2> "$OUT/pmc_$c.err"
             rc=$?; tail -2 "$OUT/pmc_$c.err"; ok_or_fail $rc pmc_$c
         done ;;
+    layouts)
+        for L in rs chain; do
+            timeout -k 10 300 python bench.py --layout $L --steps 10 --no-cpu-baseline --no-secondary > "$OUT/bench_$L.json" 2> "$OUT/bench_$L.err"
+            rc=$?; cat "$OUT/bench_$L.json"; tail -2 "$OUT/bench_$L.err"; ok_or_fail $rc layout_$L
+        done ;;
     probe)
         hipcc --offload-arch=gfx950 -O3 tools/hbm_probe.hip -o "$OUT/hbm_probe" > "$OUT/probe_build.log" 2>&1 &&
         timeout -k 10 300 "$OUT/hbm_probe" > "$OUT/hbm_probe.json" 2> "$OUT/probe.err"
