@@ -44,6 +44,9 @@ for s in $STEPS; do
             timeout -k 10 300 python bench.py --layout $L --steps 10 --no-cpu-baseline --no-secondary > "$OUT/bench_$L.json" 2> "$OUT/bench_$L.err"
             rc=$?; cat "$OUT/bench_$L.json"; tail -2 "$OUT/bench_$L.err"; ok_or_fail $rc layout_$L
         done ;;
+    h2d)
+        timeout -k 10 600 python tools/h2d_rate.py 8 26 3 > "$OUT/h2d.jsonl" 2> "$OUT/h2d.err"
+        rc=$?; cat "$OUT/h2d.jsonl"; tail -2 "$OUT/h2d.err"; ok_or_fail $rc h2d ;;
     probe)
         hipcc --offload-arch=gfx950 -O3 tools/hbm_probe.hip -o "$OUT/hbm_probe" > "$OUT/probe_build.log" 2>&1 &&
         timeout -k 10 300 "$OUT/hbm_probe" > "$OUT/hbm_probe.json" 2> "$OUT/probe.err"

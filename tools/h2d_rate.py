@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Host-inclusive aggregation rate (GPU box tool): client buckets start in host
+memory (as they arrive from network_layer.cpp's receiver) and the reduced
+bucket ends in host memory (as it leaves through new_message()).
+
+One round = D x fa_submit (or fa_submit_pinned) + fa_finalize (reduce + D2H).
+Reports GiB/s of client input per round, for pageable and pinned host buffers,
+and the device-resident rate of the same round for comparison.
+
+  python tools/h2d_rate.py [D] [n_log2] [rounds]
+"""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+
+def main():
+    import numpy as np
+    import torch
+    fa = bench.load_pkg()
+    fa.lib()
+    D = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    n = 1 << int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 26
+    rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+    w = bench.Setup._weights(D)
+    rng = np.random.default_rng(0)
+    pageable = [rng.uniform(-1, 1, n).astype(np.float32) for _ in range(D)]
+    pinned = []
+    for x in pageable:
+        t = torch.empty(n, dtype=torch.float32, pin_memory=True)
+        t.numpy()[:] = x
+        pinned.append(t)
+    out = np.empty(n, np.float32)
+    res = {"D": D, "n": n, "bytes_per_client": n * 4}
+    with fa.Aggregator(1) as agg:
+        agg.define(1, n, fa.F32, fa.F32, D, fa.FEDAVG)
+        for mode in ("pageable", "pinned"):
+            times = []
+            for r in range(rounds + 1):
+                t0 = time.perf_counter()
+                for k in range(D):
+                    if mode == "pinned":
+                        agg.submit(1, k, pinned[k].numpy(), w[k], pinned=True)
+                    else:
+                        agg.submit(1, k, pageable[k], w[k])
+                agg.finalize(1, out)
+                times.append(time.perf_counter() - t0)
+            t = min(times[1:])
+            res[mode] = {"round_s": round(t, 4), "GiB_s_input": round(D * n * 4 / t / 2**30, 2),
+                         "GB_s_pcie_bytes": round((D + 1) * n * 4 / t / 1e9, 2)}
+        # device-resident round on the same slots
+        stream = torch.cuda.Stream()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
+        for a, b in ev:
+            a.record(stream)
+            agg.reduce(1, w, stream=stream)
+            b.record(stream)
+        torch.cuda.synchronize()
+        ms = min(a.elapsed_time(b) for a, b in ev[1:])
+        res["device_resident"] = {"round_ms": round(ms, 4), "GiB_s_input": round(D * n * 4 / ms / 1e-3 / 2**30, 1)}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
