@@ -47,6 +47,9 @@ for s in $STEPS; do
     h2d)
         timeout -k 10 600 python tools/h2d_rate.py 8 26 3 > "$OUT/h2d.jsonl" 2> "$OUT/h2d.err"
         rc=$?; cat "$OUT/h2d.jsonl"; tail -2 "$OUT/h2d.err"; ok_or_fail $rc h2d ;;
+    outexp)
+        timeout -k 10 600 python tools/exp_out.py 25 10 > "$OUT/exp_out.jsonl" 2> "$OUT/exp_out.err"
+        rc=$?; cat "$OUT/exp_out.jsonl"; tail -2 "$OUT/exp_out.err"; ok_or_fail $rc outexp ;;
     probe)
         hipcc --offload-arch=gfx950 -O3 tools/hbm_probe.hip -o "$OUT/hbm_probe" > "$OUT/probe_build.log" 2>&1 &&
         timeout -k 10 300 "$OUT/hbm_probe" > "$OUT/hbm_probe.json" 2> "$OUT/probe.err"
