@@ -98,6 +98,50 @@ __global__ __launch_bounds__(128) void mstream_store_kernel(Table t, int64_t nve
     }
 }
 
+// Store policy variants through buffer stores (aux: 1 = sc0, 2 = nt, 16 = sc1).
+template <int AUX>
+__global__ __launch_bounds__(128) void mstream_bstore_kernel(Table t, int64_t nvec, f32x4* out) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out, 0, 0x7fffffff, 0x00020000);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+        f32x4 acc = {0, 0, 0, 0};
+        for (int k = 0; k < 32; k += 8) {
+            f32x4 x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) x[u] = __builtin_nontemporal_load(t.p[k + u] + v);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc = acc * 0.5f + x[u];
+        }
+        // 32-bit byte offset within a 2 GiB window of the output
+        __builtin_amdgcn_raw_buffer_store_b128(acc, r, (int)((v & ((1 << 27) - 1)) * 16), 0, AUX);
+    }
+}
+
+// Write-combining: a workgroup computes TILES consecutive 256-vector tiles, keeps the results in LDS and
+// writes them out as one contiguous TILES * 4 KiB burst.
+template <int TILES>
+__global__ __launch_bounds__(256) void mstream_lds_burst_kernel(Table t, int64_t nvec, f32x4* out) {
+    __shared__ f32x4 buf[TILES * 256];
+    const int64_t base = (int64_t)blockIdx.x * TILES * 256;
+    for (int tile = 0; tile < TILES; ++tile) {
+        const int64_t v = base + tile * 256 + threadIdx.x;
+        f32x4 acc = {0, 0, 0, 0};
+        if (v < nvec) {
+            for (int k = 0; k < 32; k += 8) {
+                f32x4 x[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) x[u] = __builtin_nontemporal_load(t.p[k + u] + v);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc = acc * 0.5f + x[u];
+            }
+        }
+        buf[tile * 256 + threadIdx.x] = acc;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < TILES * 256; i += 256)
+        if (base + i < nvec) __builtin_nontemporal_store(buf[i], out + base + i);
+}
+
 template <typename F>
 double time_ms(F f, int reps) {
     hipEvent_t a, b;
@@ -164,6 +208,24 @@ int main() {
             s3 += time_ms([&] { mstream_store_kernel<3, 8><<<g, 128>>>(t2, per2, b); }, 5);
             s16 += time_ms([&] { mstream_store_kernel<1, 16><<<g, 128>>>(t2, per2, b); }, 5);
         }
+        double pol[8] = {0};
+        const int auxs[8] = {0, 1, 2, 3, 16, 17, 18, 19};
+        double lb8 = 0, lb16 = 0;
+        for (int rep = 0; rep < 3; ++rep) {
+            pol[0] += time_ms([&] { mstream_bstore_kernel<0><<<g, 128>>>(t2, per2, b); }, 5);
+            pol[1] += time_ms([&] { mstream_bstore_kernel<1><<<g, 128>>>(t2, per2, b); }, 5);
+            pol[2] += time_ms([&] { mstream_bstore_kernel<2><<<g, 128>>>(t2, per2, b); }, 5);
+            pol[3] += time_ms([&] { mstream_bstore_kernel<3><<<g, 128>>>(t2, per2, b); }, 5);
+            pol[4] += time_ms([&] { mstream_bstore_kernel<16><<<g, 128>>>(t2, per2, b); }, 5);
+            pol[5] += time_ms([&] { mstream_bstore_kernel<17><<<g, 128>>>(t2, per2, b); }, 5);
+            pol[6] += time_ms([&] { mstream_bstore_kernel<18><<<g, 128>>>(t2, per2, b); }, 5);
+            pol[7] += time_ms([&] { mstream_bstore_kernel<19><<<g, 128>>>(t2, per2, b); }, 5);
+            lb8 += time_ms([&] { mstream_lds_burst_kernel<8><<<(unsigned)((per2 + 2047) / 2048), 256>>>(t2, per2, b); }, 5);
+            lb16 += time_ms([&] { mstream_lds_burst_kernel<16><<<(unsigned)((per2 + 4095) / 4096), 256>>>(t2, per2, b); }, 5);
+        }
+        printf(",\"store_policy_ms\":{");
+        for (int i = 0; i < 8; ++i) printf("%s\"aux%d\":%.4f", i ? "," : "", auxs[i], pol[i] / 3);
+        printf(",\"lds_burst8\":%.4f,\"lds_burst16\":%.4f}", lb8 / 3, lb16 / 3);
         printf(",\"store_ablation_ms\":{\"no_store\":%.4f,\"nt_store\":%.4f,\"plain_store\":%.4f,"
                "\"l2_window_store\":%.4f,\"nt_store_u16\":%.4f,\"algo_GBs_nt_store\":%.1f,\"read_GBs_no_store\":%.1f}",
                s0 / 3, s1 / 3, s2 / 3, s3 / 3, s16 / 3, (rd + wr) / (s1 / 3) / 1e6, rd / (s0 / 3) / 1e6);
