@@ -206,7 +206,7 @@ def main():
     ap.add_argument("--chunks", type=int, default=16, help="chain layout: pipeline chunks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
-    ap.add_argument("--tune", default="", help="block,max_blocks,unroll,nontemporal")
+    ap.add_argument("--tune", default="", help="block,max_blocks,unroll,load_policy,store_policy (fa_tuning)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -227,8 +227,8 @@ def main():
     torch.cuda.set_device(local_rank)
     fa.lib()
     if args.tune:
-        b, mb, u, nt = [int(x) for x in args.tune.split(",")]
-        fa.set_tuning(block=b, max_blocks=mb, unroll=u, nontemporal=nt)
+        b, mb, u, lp, sp = [int(x) for x in args.tune.split(",")]
+        fa.set_tuning(block=b, max_blocks=mb, unroll=u, load_policy=lp, store_policy=sp)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 

@@ -129,15 +129,15 @@ int fa_reduce_device(fa_ctx* ctx, int gpu, const void* const* d_clients, const f
 int fa_fill_uniform(void* d_dst, size_t n, fa_dtype dt, uint64_t seed, uint32_t client, uint64_t idx0,
                     void* hip_stream);
 
-/* Kernel and layout tuning knobs for benches (0 = keep the current value). */
+/* Kernel and layout tuning knobs for benches (every field: 0 = keep the current value). */
 typedef struct {
-    int block;       /* threads per workgroup (multiple of 64) */
-    int max_blocks;  /* grid cap; grid-stride beyond it */
-    int unroll;      /* clients loaded per FMA group: 4, 8 or 16 */
-    int nontemporal; /* 0 default policy, 1 nt loads+stores, 2 nt loads only, 3 nt stores only; -1 keep */
-    int slot_skew;   /* bytes between consecutive client slots beyond 4 KiB alignment (multiple of 16);
-                        -1 = none; applies to buckets defined afterwards */
-    int lane_vectors; /* 16-byte vectors per lane per client in one tile: 1, 2 or 4 */
+    int block;        /* threads per workgroup: 64, 128 or 256 */
+    int max_blocks;   /* grid cap, grid-stride beyond it; -1 = uncapped (one-shot grid) */
+    int unroll;       /* clients loaded per FMA group: 4, 8 or 16 */
+    int load_policy;  /* client loads: 1 default cache policy, 2 non-temporal */
+    int store_policy; /* output stores: 1 plain, 2 nt, 3 sc1 (write-through), 4 sc0 sc1 */
+    int slot_skew;    /* bytes between consecutive client slots beyond 4 KiB alignment (multiple of 16);
+                         -1 = none; applies to buckets defined afterwards */
 } fa_tuning;
 int fa_set_tuning(const fa_tuning* t);
 int fa_get_tuning(fa_tuning* t);

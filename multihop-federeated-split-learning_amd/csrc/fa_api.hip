@@ -28,7 +28,9 @@
 namespace {
 
 thread_local std::string g_err;
-fa::Tuning g_tuning{128, 0, 8, 1, 1};
+// block 128, one-shot grid, 8 clients per load group, nt loads, write-through (sc1) stores:
+// tools/sweep.py + tools/hbm_probe.hip store_policy_ms (profiles/r01_summary.json).
+fa::Tuning g_tuning{128, 0, 8, 1, 2};
 // Byte skew between consecutive client slots of one bucket (see slot_stride).
 size_t g_slot_skew = 512;
 
@@ -308,6 +310,7 @@ int fa_set_tuning(const fa_tuning* t) {
     g_err.clear();
     if (!t) return fail(FA_ERR_ARG, "tuning is null");
     fa::Tuning nt = g_tuning;
+    size_t skew = g_slot_skew;
     if (t->block) {
         if (t->block != 64 && t->block != 128 && t->block != 256) return fail(FA_ERR_ARG, "block must be 64/128/256");
         nt.block = t->block;
@@ -317,20 +320,20 @@ int fa_set_tuning(const fa_tuning* t) {
         if (t->unroll != 4 && t->unroll != 8 && t->unroll != 16) return fail(FA_ERR_ARG, "unroll must be 4/8/16");
         nt.unroll = t->unroll;
     }
-    if (t->lane_vectors) {
-        if (t->lane_vectors != 1 && t->lane_vectors != 2 && t->lane_vectors != 4)
-            return fail(FA_ERR_ARG, "lane_vectors must be 1/2/4");
-        nt.lane_vectors = t->lane_vectors;
+    if (t->load_policy) {
+        if (t->load_policy < 1 || t->load_policy > 2) return fail(FA_ERR_ARG, "load_policy must be 1 or 2");
+        nt.load_nt = t->load_policy == 2;
+    }
+    if (t->store_policy) {
+        if (t->store_policy < 1 || t->store_policy > 4) return fail(FA_ERR_ARG, "store_policy must be 1..4");
+        nt.store_policy = t->store_policy - 1;
     }
     if (t->slot_skew) {
         if (t->slot_skew > 0 && t->slot_skew % 16) return fail(FA_ERR_ARG, "slot_skew must be a multiple of 16");
-        g_slot_skew = t->slot_skew < 0 ? 0 : (size_t)t->slot_skew;
-    }
-    if (t->nontemporal >= 0) {
-        if (t->nontemporal > 3) return fail(FA_ERR_ARG, "nontemporal must be 0..3");
-        nt.nontemporal = t->nontemporal;
+        skew = t->slot_skew < 0 ? 0 : (size_t)t->slot_skew;
     }
     g_tuning = nt;
+    g_slot_skew = skew;
     return FA_OK;
 }
 
@@ -340,9 +343,9 @@ int fa_get_tuning(fa_tuning* t) {
     t->block = g_tuning.block;
     t->max_blocks = g_tuning.max_blocks;
     t->unroll = g_tuning.unroll;
-    t->nontemporal = g_tuning.nontemporal;
+    t->load_policy = g_tuning.load_nt ? 2 : 1;
+    t->store_policy = g_tuning.store_policy + 1;
     t->slot_skew = (int)g_slot_skew;
-    t->lane_vectors = g_tuning.lane_vectors;
     return FA_OK;
 }
 

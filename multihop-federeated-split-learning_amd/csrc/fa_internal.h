@@ -20,8 +20,8 @@ struct Tuning {
     int block;       // threads per workgroup: 64, 128 or 256
     int max_blocks;  // grid cap (grid-stride beyond it), <= 0: uncapped
     int unroll;      // clients per load group: 4, 8, 16
-    int nontemporal; // 0 none, 1 nt loads+stores, 2 nt loads, 3 nt stores
-    int lane_vectors; // 16-byte vectors per lane per client per tile: 1, 2, 4
+    int load_nt;      // non-temporal client loads
+    int store_policy; // 0 plain, 1 nt, 2 sc1 (write-through), 3 sc0 sc1
 };
 
 hipError_t launch_chain(const ClientTable& t, int nc, fa_dtype in, fa_dtype out, const float* init, void* dst,

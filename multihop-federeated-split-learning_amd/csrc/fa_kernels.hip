@@ -36,14 +36,24 @@ __device__ __forceinline__ u32x4 ld16(const void* p) {
     if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
     else return *reinterpret_cast<const u32x4*>(p);
 }
-template <bool NT>
+// Store cache policies (fa_tuning.store_policy - 1): plain, nt, sc1 (write-through, the
+// line is dropped from the XCD L2), sc0 sc1.  The asm stores need no waitcnt: nothing in
+// the kernel reads the output back.
+enum { kStPlain = 0, kStNt = 1, kStSc1 = 2, kStSc01 = 3 };
+template <int SP>
 __device__ __forceinline__ void st16(void* p, u32x4 v) {
-    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+    if constexpr (SP == kStNt) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+    else if constexpr (SP == kStSc1) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (SP == kStSc01)
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
     else *reinterpret_cast<u32x4*>(p) = v;
 }
-template <bool NT>
+template <int SP>
 __device__ __forceinline__ void st8(void* p, u32x2 v) {
-    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x2*>(p));
+    if constexpr (SP == kStNt) __builtin_nontemporal_store(v, reinterpret_cast<u32x2*>(p));
+    else if constexpr (SP == kStSc1) asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (SP == kStSc01)
+        asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
     else *reinterpret_cast<u32x2*>(p) = v;
 }
 
@@ -83,12 +93,12 @@ template <> struct In<uint16_t> {
 
 template <typename T> struct Out;
 template <> struct Out<float> {
-    template <int V, bool NT>
+    template <int V, int SP>
     __device__ static __forceinline__ void store(void* base, int64_t e, const float* a) {
         float* p = reinterpret_cast<float*>(base) + e;
 #pragma unroll
         for (int j = 0; j < V; j += 4)
-            st16<NT>(p + j, u32x4{__float_as_uint(a[j]), __float_as_uint(a[j + 1]), __float_as_uint(a[j + 2]),
+            st16<SP>(p + j, u32x4{__float_as_uint(a[j]), __float_as_uint(a[j + 1]), __float_as_uint(a[j + 2]),
                                   __float_as_uint(a[j + 3])});
     }
     __device__ static __forceinline__ void scalar(void* base, int64_t i, float a) {
@@ -96,14 +106,14 @@ template <> struct Out<float> {
     }
 };
 template <> struct Out<uint16_t> {
-    template <int V, bool NT>
+    template <int V, int SP>
     __device__ static __forceinline__ void store(void* base, int64_t e, const float* a) {
         uint16_t* p = reinterpret_cast<uint16_t*>(base) + e;
         if constexpr (V == 8) {
-            st16<NT>(p, u32x4{f32_to_bf16(a[0]) | (f32_to_bf16(a[1]) << 16), f32_to_bf16(a[2]) | (f32_to_bf16(a[3]) << 16),
+            st16<SP>(p, u32x4{f32_to_bf16(a[0]) | (f32_to_bf16(a[1]) << 16), f32_to_bf16(a[2]) | (f32_to_bf16(a[3]) << 16),
                               f32_to_bf16(a[4]) | (f32_to_bf16(a[5]) << 16), f32_to_bf16(a[6]) | (f32_to_bf16(a[7]) << 16)});
         } else {
-            st8<NT>(p, u32x2{f32_to_bf16(a[0]) | (f32_to_bf16(a[1]) << 16), f32_to_bf16(a[2]) | (f32_to_bf16(a[3]) << 16)});
+            st8<SP>(p, u32x2{f32_to_bf16(a[0]) | (f32_to_bf16(a[1]) << 16), f32_to_bf16(a[2]) | (f32_to_bf16(a[3]) << 16)});
         }
     }
     __device__ static __forceinline__ void scalar(void* base, int64_t i, float a) {
@@ -127,81 +137,52 @@ __device__ __forceinline__ void chain_scalar_edges(const ClientTable& t, int nc,
     }
 }
 
-// Chain over L lane-vectors of one thread: vector j is v0 + j * vstep (elements head + v * V ...).
-template <typename IN, typename OUT, int U, int POL, bool INIT, int L>
-__device__ __forceinline__ void chain_vectors(const ClientTable& t, int nc, const float* init, void* out,
-                                              int64_t head, int64_t v0, int64_t vstep) {
-    constexpr int V = In<IN>::kVec;
-    constexpr bool NTL = (POL & 1) != 0;
-    float acc[L][V];
-#pragma unroll
-    for (int l = 0; l < L; ++l) {
-        const int64_t e = head + (v0 + l * vstep) * V;
-        if constexpr (INIT) {
-#pragma unroll
-            for (int j = 0; j < V; j += 4) {
-                u32x4 r = ld16<NTL>(init + e + j);
-                acc[l][j] = __uint_as_float(r.x); acc[l][j + 1] = __uint_as_float(r.y);
-                acc[l][j + 2] = __uint_as_float(r.z); acc[l][j + 3] = __uint_as_float(r.w);
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < V; ++j) acc[l][j] = 0.0f;
-        }
-    }
-    int k = 0;
-    for (; k + U <= nc; k += U) {
-        u32x4 raw[U][L];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int l = 0; l < L; ++l)
-                raw[u][l] = ld16<NTL>(reinterpret_cast<const IN*>(t.src[k + u]) + head + (v0 + l * vstep) * V);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const float w = t.w[k + u];
-#pragma unroll
-            for (int l = 0; l < L; ++l) {
-                float x[V];
-                In<IN>::widen(raw[u][l], x);
-#pragma unroll
-                for (int j = 0; j < V; ++j) acc[l][j] = __builtin_fmaf(x[j], w, acc[l][j]);
-            }
-        }
-    }
-    for (; k < nc; ++k) {
-        const float w = t.w[k];
-#pragma unroll
-        for (int l = 0; l < L; ++l) {
-            float x[V];
-            In<IN>::widen(ld16<NTL>(reinterpret_cast<const IN*>(t.src[k]) + head + (v0 + l * vstep) * V), x);
-#pragma unroll
-            for (int j = 0; j < V; ++j) acc[l][j] = __builtin_fmaf(x[j], w, acc[l][j]);
-        }
-    }
-#pragma unroll
-    for (int l = 0; l < L; ++l)
-        Out<OUT>::template store<V, (POL & 2) != 0>(out, head + (v0 + l * vstep) * V, acc[l]);
-}
-
-// Vector body over nvec lane-vectors starting at element `head`.  A workgroup
-// tile is blockDim * L consecutive lane-vectors: every client bucket is read
-// in L * 1 KiB contiguous pieces per wave (L > 1 raises DRAM row locality and
-// the loads in flight per lane).  POL: bit 0 = non-temporal loads, bit 1 =
-// non-temporal stores.
-template <typename IN, typename OUT, int U, int POL, bool INIT, int L>
+// Vector body over nvec lane-vectors starting at element `head`; lane-vector v
+// covers elements head + v*V .. head + v*V + V-1 of every bucket.  LNT: nt
+// loads; SP: store policy (st16).
+template <typename IN, typename OUT, int U, bool LNT, int SP, bool INIT>
 __global__ __launch_bounds__(256) void fedavg_chain_kernel(const ClientTable t, int nc, const float* init, void* out,
                                                            int64_t head, int64_t nvec, int64_t n) {
     constexpr int V = In<IN>::kVec;
     chain_scalar_edges<IN, OUT, INIT>(t, nc, init, out, head, head + nvec * V, n);
-    const int64_t tile = (int64_t)blockDim.x * L;
-    const int64_t full_tiles = nvec / tile;
-    for (int64_t b = blockIdx.x; b < full_tiles; b += gridDim.x)
-        chain_vectors<IN, OUT, U, POL, INIT, L>(t, nc, init, out, head, b * tile + threadIdx.x, blockDim.x);
-    // remainder (< one tile): one vector per thread, spread over the grid
-    for (int64_t v = full_tiles * tile + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec;
-         v += (int64_t)gridDim.x * blockDim.x)
-        chain_vectors<IN, OUT, U, POL, INIT, 1>(t, nc, init, out, head, v, 0);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+        const int64_t e = head + v * V;  // first element owned by this lane
+        float acc[V];
+        if constexpr (INIT) {
+#pragma unroll
+            for (int j = 0; j < V; j += 4) {
+                u32x4 r = ld16<LNT>(init + e + j);
+                acc[j] = __uint_as_float(r.x); acc[j + 1] = __uint_as_float(r.y);
+                acc[j + 2] = __uint_as_float(r.z); acc[j + 3] = __uint_as_float(r.w);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < V; ++j) acc[j] = 0.0f;
+        }
+        int k = 0;
+        for (; k + U <= nc; k += U) {
+            u32x4 raw[U];  // U loads in flight before the first FMA of the group
+#pragma unroll
+            for (int u = 0; u < U; ++u) raw[u] = ld16<LNT>(reinterpret_cast<const IN*>(t.src[k + u]) + e);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                float x[V];
+                In<IN>::widen(raw[u], x);
+                const float w = t.w[k + u];
+#pragma unroll
+                for (int j = 0; j < V; ++j) acc[j] = __builtin_fmaf(x[j], w, acc[j]);
+            }
+        }
+        for (; k < nc; ++k) {
+            float x[V];
+            In<IN>::widen(ld16<LNT>(reinterpret_cast<const IN*>(t.src[k]) + e), x);
+            const float w = t.w[k];
+#pragma unroll
+            for (int j = 0; j < V; ++j) acc[j] = __builtin_fmaf(x[j], w, acc[j]);
+        }
+        Out<OUT>::template store<V, SP>(out, e, acc);
+    }
 }
 
 // Fully general path (pointers whose 16-byte phases differ): one element per lane.
@@ -218,7 +199,7 @@ __global__ __launch_bounds__(256) void fedavg_chain_scalar_kernel(const ClientTa
 
 // ---------------------------------------------------------------- literal mode
 
-template <typename IN, typename OUT, bool NT>
+template <typename IN, typename OUT, bool LNT, int SP>
 __global__ __launch_bounds__(256) void literal_kernel(const void* x, void* out, float divisor, int64_t head,
                                                       int64_t nvec, int64_t n) {
     constexpr int V = In<IN>::kVec;
@@ -234,10 +215,10 @@ __global__ __launch_bounds__(256) void literal_kernel(const void* x, void* out, 
     for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
         const int64_t e = head + v * V;
         float xv[V], r[V];
-        In<IN>::widen(ld16<NT>(reinterpret_cast<const IN*>(x) + e), xv);
+        In<IN>::widen(ld16<LNT>(reinterpret_cast<const IN*>(x) + e), xv);
 #pragma unroll
         for (int j = 0; j < V; ++j) r[j] = (xv[j] + xv[j]) / divisor;
-        Out<OUT>::template store<V, NT>(out, e, r);
+        Out<OUT>::template store<V, SP>(out, e, r);
     }
 }
 
@@ -283,36 +264,37 @@ inline int64_t grid_for(int64_t work, const Tuning& tu) {
     return g;
 }
 
-template <typename IN, typename OUT, int U, int POL, int L>
-hipError_t launch_chain_l(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
+template <typename IN, typename OUT, int U, bool LNT, int SP>
+hipError_t launch_chain_u(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
                           int64_t n, const Tuning& tu, hipStream_t s) {
-    int64_t g = grid_for(nvec > 0 ? (nvec + L - 1) / L : 1, tu);
+    const int64_t g = grid_for(nvec > 0 ? nvec : 1, tu);
     if (init)
-        hipLaunchKernelGGL((fedavg_chain_kernel<IN, OUT, U, POL, true, L>), dim3((unsigned)g), dim3(tu.block), 0, s,
+        hipLaunchKernelGGL((fedavg_chain_kernel<IN, OUT, U, LNT, SP, true>), dim3((unsigned)g), dim3(tu.block), 0, s,
                            t, nc, init, out, head, nvec, n);
     else
-        hipLaunchKernelGGL((fedavg_chain_kernel<IN, OUT, U, POL, false, L>), dim3((unsigned)g), dim3(tu.block), 0, s,
-                           t, nc, init, out, head, nvec, n);
+        hipLaunchKernelGGL((fedavg_chain_kernel<IN, OUT, U, LNT, SP, false>), dim3((unsigned)g), dim3(tu.block), 0,
+                           s, t, nc, init, out, head, nvec, n);
     return hipGetLastError();
 }
 
-template <typename IN, typename OUT, int U, int POL>
-hipError_t launch_chain_u(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
-                          int64_t n, const Tuning& tu, hipStream_t s) {
-    switch (tu.lane_vectors) {
-        case 2: return launch_chain_l<IN, OUT, U, POL, 2>(t, nc, init, out, head, nvec, n, tu, s);
-        case 4: return launch_chain_l<IN, OUT, (U > 8 ? 8 : U), POL, 4>(t, nc, init, out, head, nvec, n, tu, s);
-        default: return launch_chain_l<IN, OUT, U, POL, 1>(t, nc, init, out, head, nvec, n, tu, s);
+template <typename IN, typename OUT, bool LNT, int SP>
+hipError_t launch_chain_sp(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
+                           int64_t n, const Tuning& tu, hipStream_t s) {
+    switch (tu.unroll) {
+        case 4: return launch_chain_u<IN, OUT, 4, LNT, SP>(t, nc, init, out, head, nvec, n, tu, s);
+        case 16: return launch_chain_u<IN, OUT, 16, LNT, SP>(t, nc, init, out, head, nvec, n, tu, s);
+        default: return launch_chain_u<IN, OUT, 8, LNT, SP>(t, nc, init, out, head, nvec, n, tu, s);
     }
 }
 
-template <typename IN, typename OUT, int POL>
-hipError_t launch_chain_pol(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
-                           int64_t n, const Tuning& tu, hipStream_t s) {
-    switch (tu.unroll) {
-        case 4: return launch_chain_u<IN, OUT, 4, POL>(t, nc, init, out, head, nvec, n, tu, s);
-        case 16: return launch_chain_u<IN, OUT, 16, POL>(t, nc, init, out, head, nvec, n, tu, s);
-        default: return launch_chain_u<IN, OUT, 8, POL>(t, nc, init, out, head, nvec, n, tu, s);
+template <typename IN, typename OUT, bool LNT>
+hipError_t launch_chain_lnt(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
+                            int64_t n, const Tuning& tu, hipStream_t s) {
+    switch (tu.store_policy) {
+        case kStNt: return launch_chain_sp<IN, OUT, LNT, kStNt>(t, nc, init, out, head, nvec, n, tu, s);
+        case kStSc1: return launch_chain_sp<IN, OUT, LNT, kStSc1>(t, nc, init, out, head, nvec, n, tu, s);
+        case kStSc01: return launch_chain_sp<IN, OUT, LNT, kStSc01>(t, nc, init, out, head, nvec, n, tu, s);
+        default: return launch_chain_sp<IN, OUT, LNT, kStPlain>(t, nc, init, out, head, nvec, n, tu, s);
     }
 }
 
@@ -329,13 +311,8 @@ hipError_t launch_chain_t(const ClientTable& t, int nc, const float* init, void*
                                s, t, nc, init, out, n);
         return hipGetLastError();
     }
-    // nontemporal knob: 0 none, 1 loads + stores, 2 loads only, 3 stores only
-    switch (tu.nontemporal) {
-        case 1: return launch_chain_pol<IN, OUT, 3>(t, nc, init, out, head, nvec, n, tu, s);
-        case 2: return launch_chain_pol<IN, OUT, 1>(t, nc, init, out, head, nvec, n, tu, s);
-        case 3: return launch_chain_pol<IN, OUT, 2>(t, nc, init, out, head, nvec, n, tu, s);
-        default: return launch_chain_pol<IN, OUT, 0>(t, nc, init, out, head, nvec, n, tu, s);
-    }
+    if (tu.load_nt) return launch_chain_lnt<IN, OUT, true>(t, nc, init, out, head, nvec, n, tu, s);
+    return launch_chain_lnt<IN, OUT, false>(t, nc, init, out, head, nvec, n, tu, s);
 }
 
 }  // namespace
@@ -358,11 +335,8 @@ hipError_t launch_literal_t(const void* x, void* out, float divisor, int64_t hea
     if (!vector_ok) {
         hipLaunchKernelGGL((literal_scalar_kernel<IN, OUT>), dim3((unsigned)grid_for(n, tu)), dim3(tu.block), 0, s,
                            x, out, divisor, n);
-    } else if (tu.nontemporal) {
-        hipLaunchKernelGGL((literal_kernel<IN, OUT, true>), dim3((unsigned)grid_for(nvec > 0 ? nvec : 1, tu)),
-                           dim3(tu.block), 0, s, x, out, divisor, head, nvec, n);
-    } else {
-        hipLaunchKernelGGL((literal_kernel<IN, OUT, false>), dim3((unsigned)grid_for(nvec > 0 ? nvec : 1, tu)),
+    } else {  // two streams only: nt loads, write-through stores
+        hipLaunchKernelGGL((literal_kernel<IN, OUT, true, kStSc1>), dim3((unsigned)grid_for(nvec > 0 ? nvec : 1, tu)),
                            dim3(tu.block), 0, s, x, out, divisor, head, nvec, n);
     }
     return hipGetLastError();
@@ -382,7 +356,7 @@ hipError_t launch_literal(const void* x, fa_dtype in, void* out, fa_dtype outdt,
 
 hipError_t launch_fill(void* dst, int64_t n, fa_dtype dt, uint64_t seed, uint32_t client, uint64_t idx0,
                        hipStream_t s) {
-    Tuning tu{256, 8192, 8, 0, 1};
+    Tuning tu{256, 8192, 8, 0, 0};
     const int64_t g = grid_for(n, tu);
     if (dt == FA_F32)
         hipLaunchKernelGGL((fill_kernel<float>), dim3((unsigned)g), dim3(256), 0, s, dst, n, seed, client, idx0);

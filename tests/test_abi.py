@@ -57,7 +57,7 @@ def test_version_and_errors_without_gpu(fa):
     rc = L.fa_reduce_device(None, 0, None, None, 0, 16, 0, None, 0, 0, None, None)
     assert rc == fa.ERR_ARG and "null" in fa.last_error()
     assert L.fa_fill_uniform(None, 4, 7, 0, 0, 0, None) == fa.ERR_ARG
-    t = fa._Tuning(96, 0, 0, -1)
+    t = fa._Tuning(96, 0, 0, 0, 0, 0)
     assert L.fa_set_tuning(ctypes.byref(t)) == fa.ERR_ARG
     assert L.fa_bucket_define(None, 1, 10, 0, 0, 1, 0) == fa.ERR_ARG
     assert fa.last_error() == "ctx is null"
@@ -65,14 +65,17 @@ def test_version_and_errors_without_gpu(fa):
 
 def test_tuning_roundtrip(fa):
     before = fa.get_tuning()
-    fa.set_tuning(block=128, unroll=16, nontemporal=0)
-    assert fa.get_tuning() == {"block": 128, "max_blocks": before["max_blocks"], "unroll": 16, "nontemporal": 0,
-                               "slot_skew": before["slot_skew"], "lane_vectors": before["lane_vectors"]}
+    fa.set_tuning(block=128, unroll=16, load_policy=1, store_policy=4)
+    assert fa.get_tuning() == {"block": 128, "max_blocks": before["max_blocks"], "unroll": 16, "load_policy": 1,
+                               "store_policy": 4, "slot_skew": before["slot_skew"]}
+    with pytest.raises(fa.FaError):
+        fa.set_tuning(store_policy=5)
+    assert fa.get_tuning()["store_policy"] == 4  # a rejected call changes nothing
     fa.set_tuning(slot_skew=-1)
     assert fa.get_tuning()["slot_skew"] == 0
     with pytest.raises(fa.FaError):
         fa.set_tuning(slot_skew=100)
-    fa.set_tuning(**{k: v for k, v in before.items()})
+    fa.set_tuning(**{k: (v or -1) if k in ("max_blocks", "slot_skew") else v for k, v in before.items()})
     assert fa.get_tuning() == before
 
 

@@ -151,12 +151,12 @@ def test_literal_mode(fa, O, torch_gpu, bf16):
         assert_bits(to_np(out, out_bf16), O.literal(xs[-1], out_dtype="bf16" if out_bf16 else "f32"))
 
 
-@pytest.mark.parametrize("tuning", [dict(block=64, unroll=4, nontemporal=0), dict(block=128, unroll=16, nontemporal=1),
-                                    dict(block=256, unroll=8, nontemporal=0, max_blocks=7),
-                                    dict(block=256, unroll=16, nontemporal=1, max_blocks=1),
-                                    dict(block=128, unroll=8, nontemporal=2, lane_vectors=2),
-                                    dict(block=64, unroll=16, nontemporal=3, lane_vectors=4, max_blocks=5),
-                                    dict(block=256, unroll=4, nontemporal=1, lane_vectors=4)])
+@pytest.mark.parametrize("tuning", [dict(block=64, unroll=4, load_policy=1, store_policy=1),
+                                    dict(block=128, unroll=16, load_policy=2, store_policy=2),
+                                    dict(block=256, unroll=8, load_policy=1, store_policy=3, max_blocks=7),
+                                    dict(block=256, unroll=16, load_policy=2, store_policy=4, max_blocks=1),
+                                    dict(block=128, unroll=8, load_policy=2, store_policy=3, max_blocks=-1),
+                                    dict(block=64, unroll=16, load_policy=1, store_policy=4, max_blocks=5)])
 def test_tuning_variants_same_bits(fa, O, torch_gpu, tuning):
     torch = torch_gpu
     before = fa.get_tuning()
@@ -168,7 +168,10 @@ def test_tuning_variants_same_bits(fa, O, torch_gpu, tuning):
             clients = [filled(fa, torch, n, bf16, 8, k) for k in range(D)]
             assert_bits(run_fedavg(fa, torch, clients, w, n, bf16, bf16), O.fedavg(xs, w, out_dtype="bf16" if bf16 else "f32"))
     finally:
-        fa.set_tuning(**before)
+        restore = dict(before)
+        restore["max_blocks"] = restore["max_blocks"] or -1
+        restore["slot_skew"] = restore["slot_skew"] or -1
+        fa.set_tuning(**restore)
 
 
 # ----------------------------------------------------------------- reference golden configs, full size

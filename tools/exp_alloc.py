@@ -29,7 +29,7 @@ def main():
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 4
     D = 32
     w = bench.Setup._weights(D)
-    fa.set_tuning(block=128, max_blocks=-1, unroll=8, nontemporal=1)
+    fa.set_tuning(block=128, max_blocks=-1, unroll=8, load_policy=2, store_policy=2)
     stream = torch.cuda.Stream()
     nbytes = (D + 1) * n * 4
     pools = {}

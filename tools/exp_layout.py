@@ -28,7 +28,7 @@ def main():
     pads = [int(x) for x in sys.argv[3:]] or [0, 64, 128, 1024]
     D = 32
     w = bench.Setup._weights(D)
-    fa.set_tuning(block=128, max_blocks=-1, unroll=8, nontemporal=1)
+    fa.set_tuning(block=128, max_blocks=-1, unroll=8, load_policy=2, store_policy=2)
     stream = torch.cuda.Stream()
     pools = {}
     for r in range(reps):

@@ -34,7 +34,7 @@ def main():
     nwin = (gib << 30) // wbytes
     fa.fill_uniform(base, (gib << 30) // 4, fa.F32, 3, 0)
     w = bench.Setup._weights(D)
-    fa.set_tuning(block=128, max_blocks=-1, unroll=16, nontemporal=1)
+    fa.set_tuning(block=128, max_blocks=-1, unroll=16, load_policy=2, store_policy=2)
     stream = torch.cuda.Stream()
     torch.cuda.synchronize()
     res = {i: [] for i in range(nwin)}

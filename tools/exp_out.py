@@ -25,7 +25,7 @@ def main():
     K = int(sys.argv[2]) if len(sys.argv) > 2 else 10
     D = 32
     w = bench.Setup._weights(D)
-    fa.set_tuning(block=128, max_blocks=-1, unroll=8, nontemporal=1)
+    fa.set_tuning(block=128, max_blocks=-1, unroll=8, load_policy=2, store_policy=2)
     agg = fa.Aggregator(1)
     agg.define(0, n, fa.F32, fa.F32, D, fa.FEDAVG)
     clients = []

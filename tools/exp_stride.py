@@ -33,7 +33,7 @@ def main():
     D = 32
     cb = n * 4
     w = bench.Setup._weights(D)
-    fa.set_tuning(block=128, max_blocks=-1, unroll=16, nontemporal=1)
+    fa.set_tuning(block=128, max_blocks=-1, unroll=16, load_policy=2, store_policy=2)
     rng = random.Random(7)
     layouts = {
         "pow2": [k * cb for k in range(D + 1)],

@@ -25,12 +25,12 @@ def main():
     setups = [bench.Setup(fa, torch, D, n, i, o, 0, 0) for _ in range(pools)]  # placement varies per pool
     setup = setups[0]
     stream = torch.cuda.Stream()
-    grid = list(itertools.product([128, 256], [0], [4, 8, 16], [1, 2], [1, 2, 4]))
+    grid = list(itertools.product([128, 256], [0], [8, 16], [2], [1, 2, 3, 4]))
     times = {(g, p): [] for g in grid for p in range(pools)}
     for rnd in range(3):
         for g in grid:
-            fa.set_tuning(block=g[0], max_blocks=g[1] if g[1] else -1, unroll=g[2], nontemporal=g[3],
-                          lane_vectors=g[4])
+            fa.set_tuning(block=g[0], max_blocks=g[1] if g[1] else -1, unroll=g[2], load_policy=g[3],
+                          store_policy=g[4])
             for p, st in enumerate(setups):
                 ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(4)]
                 for a, b in ev:
@@ -43,7 +43,7 @@ def main():
     for g in grid:
         meds = [statistics.median(times[(g, p)]) for p in range(pools)]
         med = statistics.mean(meds)
-        rows.append({"block": g[0], "max_blocks": g[1], "unroll": g[2], "nt": g[3], "lane_vectors": g[4],
+        rows.append({"block": g[0], "max_blocks": g[1], "unroll": g[2], "load_policy": g[3], "store_policy": g[4],
                      "ms_mean_of_pool_medians": round(med, 4), "pool_ms": [round(m, 4) for m in meds],
                      "GBs": round(setup.algo_bytes() / med / 1e6, 1)})
     rows.sort(key=lambda r: r["ms_mean_of_pool_medians"])
