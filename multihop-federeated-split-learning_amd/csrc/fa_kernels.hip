@@ -37,23 +37,25 @@ __device__ __forceinline__ u32x4 ld16(const void* p) {
     else return *reinterpret_cast<const u32x4*>(p);
 }
 // Store cache policies (fa_tuning.store_policy - 1): plain, nt, sc1 (write-through, the
-// line is dropped from the XCD L2), sc0 sc1.  The asm stores need no waitcnt: nothing in
-// the kernel reads the output back.
+// line is dropped from the XCD L2), sc0 sc1.  The asm stores need no waitcnt (nothing in
+// the kernel reads the output back) but end with s_nop 1: hipcc does not pad hazards
+// inside an asm statement and would otherwise overwrite the data VGPRs before the store
+// has read them (cdna_hip_programming.md 5.7 item 1).
 enum { kStPlain = 0, kStNt = 1, kStSc1 = 2, kStSc01 = 3 };
 template <int SP>
 __device__ __forceinline__ void st16(void* p, u32x4 v) {
     if constexpr (SP == kStNt) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
-    else if constexpr (SP == kStSc1) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (SP == kStSc1) asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
     else if constexpr (SP == kStSc01)
-        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
     else *reinterpret_cast<u32x4*>(p) = v;
 }
 template <int SP>
 __device__ __forceinline__ void st8(void* p, u32x2 v) {
     if constexpr (SP == kStNt) __builtin_nontemporal_store(v, reinterpret_cast<u32x2*>(p));
-    else if constexpr (SP == kStSc1) asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (SP == kStSc1) asm volatile("global_store_dwordx2 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
     else if constexpr (SP == kStSc01)
-        asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+        asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
     else *reinterpret_cast<u32x2*>(p) = v;
 }
 
