@@ -162,11 +162,15 @@ def test_tuning_variants_same_bits(fa, O, torch_gpu, tuning):
     before = fa.get_tuning()
     try:
         fa.set_tuning(**tuning)
-        for n, D, bf16 in [(200_003, 19, False), (1_048_573, 33, False), (3001, 3, False), (250_001, 21, True)]:
+        for n, D, bf16, bf16_out in [(200_003, 19, False, False), (1_048_573, 33, False, False), (3001, 3, False, False),
+                                     (250_001, 21, True, True), (250_001, 21, True, False), (99_999, 5, False, True)]:
             w = O.weights(D)
             xs = host_clients(O, 8, D, n, bf16)
             clients = [filled(fa, torch, n, bf16, 8, k) for k in range(D)]
-            assert_bits(run_fedavg(fa, torch, clients, w, n, bf16, bf16), O.fedavg(xs, w, out_dtype="bf16" if bf16 else "f32"))
+            ref = O.fedavg(xs, w, out_dtype="bf16" if bf16_out else "f32")
+            if bf16_out and not bf16:
+                ref = O.f32_to_bf16(O.fedavg(xs, w))
+            assert_bits(run_fedavg(fa, torch, clients, w, n, bf16, bf16_out), ref)
     finally:
         restore = dict(before)
         restore["max_blocks"] = restore["max_blocks"] or -1
