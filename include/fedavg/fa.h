@@ -85,6 +85,13 @@ int fa_submit(fa_ctx* ctx, int part_id, int client_slot, const void* host_src, f
  * caller keeps unchanged until fa_finalize returns: no staging copy. */
 int fa_submit_pinned(fa_ctx* ctx, int part_id, int client_slot, const void* host_src, float weight);
 
+/* Same as fa_submit for a receipt scattered over n_segments host pieces whose
+ * concatenation is the bucket (e.g. the parameter records of a torch::save
+ * archive mapped in place, in named_parameters() order): gathered straight into
+ * the pinned staging chunks, no intermediate flat copy. */
+int fa_submit_gather(fa_ctx* ctx, int part_id, int client_slot, int n_segments, const void* const* srcs,
+                     const size_t* bytes, float weight);
+
 /* Replaces the end of a phase: the reduced module handed to new_message()
  * (aggregator.cpp:96-106 / :153-166).  Waits for the submits, reduces on every
  * GPU, copies the result (out dtype) to host_dst and resets the round. */

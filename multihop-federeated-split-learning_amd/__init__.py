@@ -69,6 +69,7 @@ def lib():
         "fa_set_literal_divisor": (I, [P, I, F]),
         "fa_submit": (I, [P, I, I, P, F]),
         "fa_submit_pinned": (I, [P, I, I, P, F]),
+        "fa_submit_gather": (I, [P, I, I, I, P, P, F]),
         "fa_finalize": (I, [P, I, P]),
         "fa_reduce_device": (I, [P, I, P, P, I, S, I, P, I, I, P, P]),
         "fa_fill_uniform": (I, [P, S, I, U64, U32, U64, P]),
@@ -189,6 +190,13 @@ class Aggregator:
             raise ValueError("bucket %d expects %d bytes, got %d" % (part_id, n * DTYPE_SIZE[in_dtype], host.nbytes))
         fn = lib().fa_submit_pinned if pinned else lib().fa_submit
         check(fn(self.handle, part_id, slot, host.ctypes.data, float(weight)))
+
+    def submit_gather(self, part_id, slot, pieces, weight=1.0):
+        """fa_submit_gather: `pieces` (host arrays) concatenate to the bucket."""
+        pieces = [np.ascontiguousarray(x) for x in pieces]
+        ptrs = (ctypes.c_void_p * len(pieces))(*[x.ctypes.data for x in pieces])
+        sizes = (ctypes.c_size_t * len(pieces))(*[x.nbytes for x in pieces])
+        check(lib().fa_submit_gather(self.handle, part_id, slot, len(pieces), ptrs, sizes, float(weight)))
 
     def finalize(self, part_id, out=None):
         if part_id not in self.parts:  # let the library report it (FA_ERR_ARG)

@@ -231,21 +231,51 @@ int reduce_part(fa_ctx* ctx, Part& p, const float* w, hipStream_t s) {
     return FA_OK;
 }
 
-int submit_impl(fa_ctx* ctx, int part_id, int slot, const void* src, float weight, bool pinned) {
+// A host source for one receipt: the concatenation of `n` segments (one segment for a flat buffer,
+// one per parameter record for an archive mapped in place).
+struct Gather {
+    int n;
+    const void* const* src;
+    const size_t* bytes;
+    // Copies bytes [a, a + len) of the concatenation to dst.
+    void copy(size_t a, size_t len, char* dst) const {
+        size_t seg_lo = 0;
+        for (int k = 0; k < n && len > 0; ++k) {
+            const size_t seg_hi = seg_lo + bytes[k];
+            if (a < seg_hi) {
+                const size_t off = a - seg_lo, take = std::min(len, seg_hi - a);
+                std::memcpy(dst, static_cast<const char*>(src[k]) + off, take);
+                dst += take;
+                a += take;
+                len -= take;
+            }
+            seg_lo = seg_hi;
+        }
+    }
+};
+
+int submit_impl(fa_ctx* ctx, int part_id, int slot, const Gather& src, float weight, bool pinned) {
     Part* p;
     int rc = check_part(ctx, part_id, &p);
     if (rc) return rc;
     if (slot < 0 || slot >= p->D) return fail(FA_ERR_ARG, "client slot %d out of range [0,%d)", slot, p->D);
-    if (!src && p->n) return fail(FA_ERR_ARG, "host_src is null");
     const size_t si = dsize(p->in);
+    size_t total = 0;
+    for (int k = 0; k < src.n; ++k) {
+        if (!src.src[k] && src.bytes[k]) return fail(FA_ERR_ARG, "host source segment %d is null", k);
+        total += src.bytes[k];
+    }
+    if (total != p->n * si)
+        return fail(FA_ERR_ARG, "part %d expects %zu bytes per receipt, got %zu", part_id, p->n * si, total);
     for (int g = 0; g < ctx->G; ++g) {
         GpuRes& r = ctx->gpu[g];
         DeviceGuard dg(r.dev);
-        const char* hs = static_cast<const char*>(src) + p->off[g] * si;
+        const size_t base = p->off[g] * si;
         char* ds = slot_ptr(*p, g, slot);
-        size_t bytes = p->cnt[g] * si;
-        if (pinned) {
-            if (bytes) FA_HIP(hipMemcpyAsync(ds, hs, bytes, hipMemcpyHostToDevice, r.copy));
+        const size_t bytes = p->cnt[g] * si;
+        if (pinned) {  // one flat pinned buffer: DMA straight from it
+            if (bytes) FA_HIP(hipMemcpyAsync(ds, static_cast<const char*>(src.src[0]) + base, bytes,
+                                             hipMemcpyHostToDevice, r.copy));
             continue;
         }
         // Double-buffered staging: fill one pinned chunk while the other is in flight.
@@ -254,7 +284,7 @@ int submit_impl(fa_ctx* ctx, int part_id, int slot, const void* src, float weigh
             const int i = r.stage_i;
             r.stage_i ^= 1;
             FA_HIP(hipEventSynchronize(r.stage_ev[i]));
-            std::memcpy(r.stage[i], hs + o, b);
+            src.copy(base + o, b, r.stage[i]);
             FA_HIP(hipMemcpyAsync(ds + o, r.stage[i], b, hipMemcpyHostToDevice, r.copy));
             FA_HIP(hipEventRecord(r.stage_ev[i], r.copy));
         }
@@ -478,14 +508,31 @@ int fa_set_literal_divisor(fa_ctx* ctx, int part_id, float divisor) {
     return FA_OK;
 }
 
+static int submit_flat(fa_ctx* ctx, int part_id, int client_slot, const void* host_src, float weight, bool pinned) {
+    Part* p;
+    int rc = check_part(ctx, part_id, &p);
+    if (rc) return rc;
+    if (!host_src && p->n) return fail(FA_ERR_ARG, "host_src is null");
+    const size_t bytes = p->n * dsize(p->in);
+    const void* srcs[1] = {host_src};
+    return submit_impl(ctx, part_id, client_slot, Gather{1, srcs, &bytes}, weight, pinned);
+}
+
 int fa_submit(fa_ctx* ctx, int part_id, int client_slot, const void* host_src, float weight) {
     g_err.clear();
-    return submit_impl(ctx, part_id, client_slot, host_src, weight, false);
+    return submit_flat(ctx, part_id, client_slot, host_src, weight, false);
 }
 
 int fa_submit_pinned(fa_ctx* ctx, int part_id, int client_slot, const void* host_src, float weight) {
     g_err.clear();
-    return submit_impl(ctx, part_id, client_slot, host_src, weight, true);
+    return submit_flat(ctx, part_id, client_slot, host_src, weight, true);
+}
+
+int fa_submit_gather(fa_ctx* ctx, int part_id, int client_slot, int n_segments, const void* const* srcs,
+                     const size_t* bytes, float weight) {
+    g_err.clear();
+    if (n_segments < 0 || (n_segments > 0 && (!srcs || !bytes))) return fail(FA_ERR_ARG, "bad segment list");
+    return submit_impl(ctx, part_id, client_slot, Gather{n_segments, srcs, bytes}, weight, false);
 }
 
 int fa_finalize(fa_ctx* ctx, int part_id, void* host_dst) {

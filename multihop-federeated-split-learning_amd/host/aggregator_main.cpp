@@ -1,0 +1,318 @@
+// aggregator_main.cpp -- drop-in replacement for pipeline_simulation/aggregator.cpp.
+//
+// Same process role (node id -1), same CLI (-i/-d/-c, aggregator.cpp:13-32),
+// same wire protocol and the same round structure (aggregator.cpp:55-167):
+//   refactor  <- the init node's REFACTOR_DATA_OWNER message (:52-53)
+//   phase 1   <- D receipts of model_part 1, reduced, reply to 0 and i+c+1 (:59-106)
+//   phase 2   <- D*L receipts of model_parts 2..L+1, reduced, reply per layer (:108-166)
+// What changes is only how a receipt is consumed: the archive is mapped in
+// place (host/archive.h) and its parameter records are gathered into pinned
+// staging and DMA'd to the client's device slot (fa_submit_gather); at the end
+// of a phase one ordered FMA chain per bucket runs on the MI355X (fa_finalize)
+// and the reply archive is the last receipt's with the reduced parameters
+// written in (buffers stay the last receipt's, as in the reference), built
+// once and sent to every data owner.
+//
+// --mode literal reproduces the reference's arithmetic bit-for-bit
+// (fl(fl(x_last + x_last) / 1000)); --mode fedavg (default) is
+// the north star's weighted mean (weights n_k/N from --samples, else 1/D).
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <map>
+#include <memory>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "archive.h"
+#include "fedavg/fa.h"
+#include "net.h"
+
+using namespace fahost;
+
+namespace {
+
+struct Options {
+    int id = -1, data_owners = 1, compute_nodes = 1;
+    int gpus = 1, rounds = -1, port_base = 8079, last_layers = -1;
+    fa_mode mode = FA_FEDAVG;
+    float divisor = 1000.0f;  // kTrainSize_10, aggregator.cpp:48
+    bool discover = false;
+    double link_mbps = 0;
+    std::map<int, double> samples;  // client id -> n_k
+};
+
+void usage() {
+    std::cerr << "usage: fa_aggregator -i ID -d DATA_OWNERS -c COMPUTE_NODES [--mode fedavg|literal] [--gpus G]\n"
+                 "       [--rounds R] [--port-base P] [--discover] [--link-mbps M] [--samples id:n,...]\n"
+                 "       [--divisor K] [--last-layers L]\n";
+}
+
+bool parse_args(int argc, char** argv, Options* o) {
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i];
+        auto val = [&](const char* what) -> const char* {
+            if (i + 1 >= argc) {
+                std::cerr << "missing value for " << what << "\n";
+                std::exit(2);
+            }
+            return argv[++i];
+        };
+        if (a == "-i" || a == "--id") o->id = std::atoi(val("-i"));
+        else if (a == "-d" || a == "--data_owners") o->data_owners = std::atoi(val("-d"));
+        else if (a == "-c" || a == "--compute_nodes") o->compute_nodes = std::atoi(val("-c"));
+        else if (a == "--gpus") o->gpus = std::atoi(val("--gpus"));
+        else if (a == "--rounds") o->rounds = std::atoi(val("--rounds"));
+        else if (a == "--port-base") o->port_base = std::atoi(val("--port-base"));
+        else if (a == "--last-layers") o->last_layers = std::atoi(val("--last-layers"));
+        else if (a == "--divisor") o->divisor = (float)std::atof(val("--divisor"));
+        else if (a == "--discover") o->discover = true;
+        else if (a == "--link-mbps") o->link_mbps = std::atof(val("--link-mbps"));
+        else if (a == "--mode") {
+            std::string m = val("--mode");
+            if (m == "literal") o->mode = FA_LITERAL;
+            else if (m == "fedavg") o->mode = FA_FEDAVG;
+            else return false;
+        } else if (a == "--samples") {
+            std::stringstream ss(val("--samples"));
+            std::string tok;
+            while (std::getline(ss, tok, ',')) {
+                const size_t c = tok.find(':');
+                if (c == std::string::npos) return false;
+                o->samples[std::atoi(tok.substr(0, c).c_str())] = std::atof(tok.substr(c + 1).c_str());
+            }
+        } else if (a == "-h" || a == "--help") {
+            return false;
+        } else {
+            std::cerr << "unknown argument " << a << "\n";
+            return false;
+        }
+    }
+    return o->data_owners >= 1;
+}
+
+// parts[1].layers.size() for the aggregator's ModelPart(start, -1) (systemAPI.cpp:19):
+// resnet_part / lenet_part always return two Sequentials for end == -1
+// (resnet_split.cpp:176-188, lenet_help.cpp:170-183); vgg_part returns two iff
+// start - 1 <= 20 (vgg_help.cpp:250-256, ModelPart passes start - 1, models.h:25).
+int last_part_layers(int model_name, int start) {
+    if (model_name == 0) return (start - 1) <= 20 ? 2 : 1;
+    return 2;
+}
+
+long now_ms() {
+    return std::chrono::duration_cast<std::chrono::milliseconds>(
+               std::chrono::system_clock::now().time_since_epoch())
+        .count();
+}
+
+double secs_since(std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+}
+
+#define FA_CHECK(call)                                                                       \
+    do {                                                                                     \
+        int rc_ = (call);                                                                    \
+        if (rc_ != FA_OK) {                                                                  \
+            std::cerr << "[aggregator] " #call " failed: " << fa_last_error() << "\n";       \
+            std::exit(1);                                                                    \
+        }                                                                                    \
+    } while (0)
+
+class Aggregator {
+public:
+    Aggregator(const Options& o, NetLayer* net) : o_(o), net_(net) {
+        FA_CHECK(fa_create(&ctx_, o.gpus, o.gpus > 1 ? FA_SHARD_RANGE : 0));
+        FA_CHECK(fa_set_literal_divisor(ctx_, -1, o.divisor));
+    }
+    ~Aggregator() { fa_destroy(ctx_); }
+
+    // Consumes one receipt of bucket `mp` into its client slot.
+    void absorb(const Receipt& r) {
+        TorchArchive ar;
+        std::string err;
+        if (!ar.parse(r.blob(), r.blob_len, &err)) {
+            std::cerr << "[aggregator] receipt from " << r.client_id << ": " << err << "\n";
+            std::exit(1);
+        }
+        Bucket& b = buckets_[r.model_part];
+        if (!b.defined) {
+            if (!ar.params_are_float()) {
+                std::cerr << "[aggregator] bucket " << r.model_part << " has non-fp32 parameters\n";
+                std::exit(1);
+            }
+            b.numel = (size_t)ar.param_numel();
+            FA_CHECK(fa_bucket_define(ctx_, r.model_part, b.numel, FA_F32, FA_F32, o_.data_owners, o_.mode));
+            b.defined = true;
+        } else if ((size_t)ar.param_numel() != b.numel) {
+            std::cerr << "[aggregator] bucket " << r.model_part << " changed size\n";
+            std::exit(1);
+        }
+        const int slot = slot_of(r.client_id);
+        std::vector<const void*> ptrs;
+        std::vector<size_t> bytes;
+        if (ar.param_segments(&ptrs, &bytes)) {
+            FA_CHECK(fa_submit_gather(ctx_, r.model_part, slot, (int)ptrs.size(), ptrs.data(), bytes.data(),
+                                      weight_of(r.client_id)));
+        } else {  // strided parameters: flatten first
+            std::vector<float> flat(b.numel);
+            if (!ar.gather_params(flat.data(), &err)) {
+                std::cerr << "[aggregator] " << err << "\n";
+                std::exit(1);
+            }
+            FA_CHECK(fa_submit(ctx_, r.model_part, slot, flat.data(), weight_of(r.client_id)));
+        }
+        b.bytes_in += r.blob_len;
+        b.last = r;  // template of the reply: the last receipt (its buffers travel back, as in the reference)
+    }
+
+    // Reduces bucket mp and returns the framed reply (shared by every destination).
+    std::shared_ptr<const std::string> reduce(int mp) {
+        Bucket& b = buckets_[mp];
+        std::vector<float> out(b.numel);
+        FA_CHECK(fa_finalize(ctx_, mp, out.data()));
+        TorchArchive ar;
+        std::string err, archive;
+        if (!ar.parse(b.last.blob(), b.last.blob_len, &err) || !ar.with_params(out.data(), &archive, &err)) {
+            std::cerr << "[aggregator] reply for part " << mp << ": " << err << "\n";
+            std::exit(1);
+        }
+        Message m;  // Task(myid, aggregation_, myid) with model_part, aggregator.cpp:96-101
+        m.type = OPERATION;
+        m.client_id = o_.id;
+        m.prev_node = o_.id;
+        m.type_op = AGGREGATION;
+        m.model_part = mp;
+        m.t_start = now_ms();
+        m.values = std::move(archive);
+        b.bytes_in = 0;
+        return std::make_shared<const std::string>(frame(m));
+    }
+
+    // Fan-out to node 0 and the data owners i + c + 1, i < D - 1 (aggregator.cpp:102-106, :158-164).
+    void fan_out(const std::shared_ptr<const std::string>& f) {
+        net_->send(0, f);
+        for (int i = 0; i < o_.data_owners - 1; ++i) net_->send(i + o_.compute_nodes + 1, f);
+    }
+
+    size_t bytes_in(int mp) { return buckets_[mp].bytes_in; }
+
+private:
+    struct Bucket {
+        bool defined = false;
+        size_t numel = 0, bytes_in = 0;
+        Receipt last;
+    };
+
+    int slot_of(int client) {
+        auto it = slots_.find(client);
+        if (it != slots_.end()) return it->second;
+        const int s = (int)slots_.size();
+        if (s >= o_.data_owners) {
+            std::cerr << "[aggregator] more distinct clients than -d " << o_.data_owners << "\n";
+            std::exit(1);
+        }
+        slots_[client] = s;
+        return s;
+    }
+
+    float weight_of(int client) const {
+        if (o_.samples.empty()) return 1.0f / (float)o_.data_owners;
+        double total = 0;
+        for (auto& kv : o_.samples) total += kv.second;
+        auto it = o_.samples.find(client);
+        return it == o_.samples.end() ? 0.0f : (float)(it->second / total);
+    }
+
+    Options o_;
+    NetLayer* net_;
+    fa_ctx* ctx_ = nullptr;
+    std::map<int, Bucket> buckets_;
+    std::map<int, int> slots_;
+};
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    Options o;
+    if (!parse_args(argc, argv, &o)) {
+        usage();
+        return 2;
+    }
+    NetLayer net(o.id, RoutingTable(o.port_base));
+    net.set_link_mbps(o.link_mbps);
+    std::string err;
+    if (o.discover && !net.find_init(600, &err)) {
+        std::cerr << "[aggregator] discovery failed: " << err << "\n";
+        return 1;
+    }
+    if (!net.start()) {
+        std::cerr << "[aggregator] cannot listen on port " << net.routes().port_for(o.id) << "\n";
+        return 1;
+    }
+    std::cerr << "[aggregator] node " << o.id << " listening on " << net.listen_port() << "\n";
+
+    Message refactor = net.next_refactor();  // aggregator.cpp:52-53
+    const int L = o.last_layers > 0 ? o.last_layers : last_part_layers(refactor.model_name, refactor.start);
+    std::cerr << "[aggregator] refactor: model " << refactor.model_name << "/" << refactor.model_type << " start "
+              << refactor.start << " end " << refactor.end << " -> " << L << " last-part layer(s)\n";
+    Aggregator agg(o, &net);
+
+    for (int round = 0; o.rounds < 0 || round < o.rounds; ++round) {
+        // phase 1: model part 1 from every data owner (aggregator.cpp:59-93)
+        auto t0 = std::chrono::steady_clock::now();
+        std::vector<Receipt> early;  // phase-2 receipts that overtook phase 1 (not in the reference's FIFO)
+        int received = 0;
+        while (received < o.data_owners) {
+            Receipt r = net.next_receipt();
+            if (r.model_part != 1) {
+                early.push_back(std::move(r));
+                continue;
+            }
+            agg.absorb(r);
+            ++received;
+        }
+        const double recv1 = secs_since(t0);
+        const size_t in1 = agg.bytes_in(1);
+        auto t1 = std::chrono::steady_clock::now();
+        auto reply1 = agg.reduce(1);
+        const double red1 = secs_since(t1);
+        agg.fan_out(reply1);
+
+        // phase 2: every last-part layer from every data owner (:108-150)
+        auto t2 = std::chrono::steady_clock::now();
+        int got = 0;
+        const int want = o.data_owners * L;
+        for (auto& r : early) {
+            agg.absorb(r);
+            ++got;
+        }
+        while (got < want) {
+            Receipt r = net.next_receipt();
+            if (r.model_part < 2 || r.model_part > L + 1) {
+                std::cerr << "[aggregator] unexpected model_part " << r.model_part << " in phase 2\n";
+                continue;
+            }
+            agg.absorb(r);
+            ++got;
+        }
+        const double recv2 = secs_since(t2);
+        size_t in2 = 0;
+        for (int mp = 2; mp <= L + 1; ++mp) in2 += agg.bytes_in(mp);
+        auto t3 = std::chrono::steady_clock::now();
+        std::vector<std::shared_ptr<const std::string>> replies;
+        for (int mp = 2; mp <= L + 1; ++mp) replies.push_back(agg.reduce(mp));
+        const double red2 = secs_since(t3);
+        for (auto& f : replies) agg.fan_out(f);  // :153-166, in layer order
+        net.flush();
+        printf("{\"round\":%d,\"phase1\":{\"receive_s\":%.6f,\"reduce_s\":%.6f,\"bytes_in\":%zu},"
+               "\"phase2\":{\"receive_s\":%.6f,\"reduce_s\":%.6f,\"bytes_in\":%zu,\"layers\":%d}}\n",
+               round, recv1, red1, in1, recv2, red2, in2, L);
+        fflush(stdout);
+    }
+    net.stop();
+    return 0;
+}

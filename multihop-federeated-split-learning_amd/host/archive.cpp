@@ -1,0 +1,626 @@
+// archive.cpp -- see archive.h.  Zip (stored, zip64-aware) + a minimal pickle
+// machine for the protocol-2 `data.pkl` that libtorch's OutputArchive writes.
+#include "archive.h"
+
+#include <algorithm>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <memory>
+#include <unordered_map>
+
+#include <zlib.h>
+
+namespace fahost {
+
+// ------------------------------------------------------------------ CRC-32 (IEEE, slicing-by-8)
+
+namespace {
+struct CrcTables {
+    uint32_t t[8][256];
+    CrcTables() {
+        for (uint32_t i = 0; i < 256; ++i) {
+            uint32_t c = i;
+            for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+            t[0][i] = c;
+        }
+        for (uint32_t i = 0; i < 256; ++i)
+            for (int s = 1; s < 8; ++s) t[s][i] = (t[s - 1][i] >> 8) ^ t[0][t[s - 1][i] & 0xFF];
+    }
+};
+const CrcTables& crc_tables() {
+    static const CrcTables tabs;
+    return tabs;
+}
+}  // namespace
+
+uint32_t crc32(const uint8_t* p, size_t n, uint32_t crc) {
+    const auto& T = crc_tables().t;
+    uint32_t c = ~crc;
+    while (n >= 8) {
+        uint32_t a, b;
+        std::memcpy(&a, p, 4);
+        std::memcpy(&b, p + 4, 4);
+        a ^= c;
+        c = T[7][a & 0xFF] ^ T[6][(a >> 8) & 0xFF] ^ T[5][(a >> 16) & 0xFF] ^ T[4][a >> 24] ^ T[3][b & 0xFF] ^
+            T[2][(b >> 8) & 0xFF] ^ T[1][(b >> 16) & 0xFF] ^ T[0][b >> 24];
+        p += 8;
+        n -= 8;
+    }
+    while (n--) c = T[0][(c ^ *p++) & 0xFF] ^ (c >> 8);
+    return ~c;
+}
+
+// ------------------------------------------------------------------ little-endian helpers
+
+namespace {
+
+uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+uint32_t rd32(const uint8_t* p) {
+    uint32_t v;
+    std::memcpy(&v, p, 4);
+    return v;
+}
+uint64_t rd64(const uint8_t* p) {
+    uint64_t v;
+    std::memcpy(&v, p, 8);
+    return v;
+}
+void wr32(uint8_t* p, uint32_t v) { std::memcpy(p, &v, 4); }
+
+bool fail(std::string* err, const std::string& m) {
+    if (err) *err = m;
+    return false;
+}
+
+// ------------------------------------------------------------------ pickle objects
+
+struct PObj;
+using P = std::shared_ptr<PObj>;
+
+struct PObj {
+    enum Kind { None, Bool, Int, Float, Str, Tuple, List, Dict, Global, Object, Storage, Tensor, Mark } kind = None;
+    int64_t i = 0;
+    double f = 0;
+    std::string s;                          // Str; Global "module name"; Storage: key
+    std::string s2;                         // Storage: storage type name
+    std::vector<P> items;                   // Tuple / List
+    std::vector<std::pair<P, P>> dict;      // Dict (insertion order)
+    P cls, state;                           // Object
+    // Tensor
+    P storage;
+    int64_t offset = 0;
+    std::vector<int64_t> sizes, strides;
+};
+
+P make(PObj::Kind k) {
+    auto p = std::make_shared<PObj>();
+    p->kind = k;
+    return p;
+}
+
+// Runs data.pkl; returns the root object.
+P unpickle(const uint8_t* p, size_t n, std::string* err) {
+    std::vector<P> stack;
+    std::vector<size_t> marks;
+    std::unordered_map<uint32_t, P> memo;
+    size_t i = 0;
+    auto need = [&](size_t k) { return i + k <= n; };
+    auto pop = [&]() -> P {
+        if (stack.empty()) return nullptr;
+        P v = stack.back();
+        stack.pop_back();
+        return v;
+    };
+    auto pop_mark = [&](std::vector<P>* out) -> bool {
+        if (marks.empty()) return false;
+        size_t m = marks.back();
+        marks.pop_back();
+        if (m > stack.size()) return false;
+        out->assign(stack.begin() + (long)m, stack.end());
+        stack.resize(m);
+        return true;
+    };
+    while (i < n) {
+        const uint8_t op = p[i++];
+        switch (op) {
+            case 0x80:  // PROTO
+                if (!need(1)) return fail(err, "pickle: truncated PROTO"), nullptr;
+                ++i;
+                break;
+            case 0x95:  // FRAME
+                if (!need(8)) return fail(err, "pickle: truncated FRAME"), nullptr;
+                i += 8;
+                break;
+            case 'c': {  // GLOBAL "module\nname\n"
+                const uint8_t* e1 = (const uint8_t*)memchr(p + i, '\n', n - i);
+                if (!e1) return fail(err, "pickle: bad GLOBAL"), nullptr;
+                const uint8_t* e2 = (const uint8_t*)memchr(e1 + 1, '\n', n - (size_t)(e1 + 1 - p));
+                if (!e2) return fail(err, "pickle: bad GLOBAL"), nullptr;
+                P g = make(PObj::Global);
+                g->s = std::string((const char*)p + i, e1 - (p + i)) + " " + std::string((const char*)e1 + 1, e2 - e1 - 1);
+                i = (size_t)(e2 + 1 - p);
+                stack.push_back(g);
+                break;
+            }
+            case 'q':  // BINPUT
+                if (!need(1) || stack.empty()) return fail(err, "pickle: bad BINPUT"), nullptr;
+                memo[p[i++]] = stack.back();
+                break;
+            case 'r':  // LONG_BINPUT
+                if (!need(4) || stack.empty()) return fail(err, "pickle: bad LONG_BINPUT"), nullptr;
+                memo[rd32(p + i)] = stack.back();
+                i += 4;
+                break;
+            case 0x94:  // MEMOIZE
+                if (stack.empty()) return fail(err, "pickle: bad MEMOIZE"), nullptr;
+                memo[(uint32_t)memo.size()] = stack.back();
+                break;
+            case 'h': {  // BINGET
+                if (!need(1)) return fail(err, "pickle: bad BINGET"), nullptr;
+                auto it = memo.find(p[i++]);
+                if (it == memo.end()) return fail(err, "pickle: BINGET of unknown memo"), nullptr;
+                stack.push_back(it->second);
+                break;
+            }
+            case 'j': {  // LONG_BINGET
+                if (!need(4)) return fail(err, "pickle: bad LONG_BINGET"), nullptr;
+                auto it = memo.find(rd32(p + i));
+                i += 4;
+                if (it == memo.end()) return fail(err, "pickle: LONG_BINGET of unknown memo"), nullptr;
+                stack.push_back(it->second);
+                break;
+            }
+            case '(':
+                marks.push_back(stack.size());
+                break;
+            case ')':
+                stack.push_back(make(PObj::Tuple));
+                break;
+            case ']':
+                stack.push_back(make(PObj::List));
+                break;
+            case '}':
+                stack.push_back(make(PObj::Dict));
+                break;
+            case 'N':
+                stack.push_back(make(PObj::None));
+                break;
+            case 0x88:
+            case 0x89: {
+                P b = make(PObj::Bool);
+                b->i = op == 0x88;
+                stack.push_back(b);
+                break;
+            }
+            case 'K':
+            case 'M':
+            case 'J': {
+                const size_t w = op == 'K' ? 1 : op == 'M' ? 2 : 4;
+                if (!need(w)) return fail(err, "pickle: truncated int"), nullptr;
+                P v = make(PObj::Int);
+                v->i = op == 'K' ? p[i] : op == 'M' ? rd16(p + i) : (int32_t)rd32(p + i);
+                i += w;
+                stack.push_back(v);
+                break;
+            }
+            case 0x8a: {  // LONG1
+                if (!need(1)) return fail(err, "pickle: truncated LONG1"), nullptr;
+                const size_t w = p[i++];
+                if (!need(w) || w > 8) return fail(err, "pickle: unsupported LONG1"), nullptr;
+                uint64_t u = 0;
+                for (size_t k = 0; k < w; ++k) u |= (uint64_t)p[i + k] << (8 * k);
+                if (w && w < 8 && (p[i + w - 1] & 0x80)) u |= ~0ull << (8 * w);  // sign-extend
+                i += w;
+                P v = make(PObj::Int);
+                v->i = (int64_t)u;
+                stack.push_back(v);
+                break;
+            }
+            case 'G': {  // BINFLOAT (big-endian double)
+                if (!need(8)) return fail(err, "pickle: truncated BINFLOAT"), nullptr;
+                uint64_t u = 0;
+                for (int k = 0; k < 8; ++k) u = (u << 8) | p[i + k];
+                i += 8;
+                P v = make(PObj::Float);
+                std::memcpy(&v->f, &u, 8);
+                stack.push_back(v);
+                break;
+            }
+            case 'X':
+            case 0x8c:
+            case 'U':
+            case 'T': {  // BINUNICODE / SHORT_BINUNICODE / SHORT_BINSTRING / BINSTRING
+                const bool shortlen = op == 0x8c || op == 'U';
+                if (!need(shortlen ? 1 : 4)) return fail(err, "pickle: truncated string"), nullptr;
+                const size_t len = shortlen ? p[i] : rd32(p + i);
+                i += shortlen ? 1 : 4;
+                if (!need(len)) return fail(err, "pickle: truncated string"), nullptr;
+                P v = make(PObj::Str);
+                v->s.assign((const char*)p + i, len);
+                i += len;
+                stack.push_back(v);
+                break;
+            }
+            case 't': {
+                P t = make(PObj::Tuple);
+                if (!pop_mark(&t->items)) return fail(err, "pickle: TUPLE without MARK"), nullptr;
+                stack.push_back(t);
+                break;
+            }
+            case 0x85:
+            case 0x86:
+            case 0x87: {
+                const size_t k = op - 0x84;
+                if (stack.size() < k) return fail(err, "pickle: short TUPLEn"), nullptr;
+                P t = make(PObj::Tuple);
+                t->items.assign(stack.end() - (long)k, stack.end());
+                stack.resize(stack.size() - k);
+                stack.push_back(t);
+                break;
+            }
+            case 'a': {  // APPEND
+                P v = pop();
+                if (!v || stack.empty() || stack.back()->kind != PObj::List) return fail(err, "pickle: bad APPEND"), nullptr;
+                stack.back()->items.push_back(v);
+                break;
+            }
+            case 'e': {  // APPENDS
+                std::vector<P> xs;
+                if (!pop_mark(&xs) || stack.empty()) return fail(err, "pickle: bad APPENDS"), nullptr;
+                for (auto& x : xs) stack.back()->items.push_back(x);
+                break;
+            }
+            case 's': {  // SETITEM
+                P v = pop(), k = pop();
+                if (!v || !k || stack.empty() || stack.back()->kind != PObj::Dict) return fail(err, "pickle: bad SETITEM"), nullptr;
+                stack.back()->dict.emplace_back(k, v);
+                break;
+            }
+            case 'u': {  // SETITEMS
+                std::vector<P> kv;
+                if (!pop_mark(&kv) || (kv.size() & 1) || stack.empty() || stack.back()->kind != PObj::Dict)
+                    return fail(err, "pickle: bad SETITEMS"), nullptr;
+                for (size_t k = 0; k < kv.size(); k += 2) stack.back()->dict.emplace_back(kv[k], kv[k + 1]);
+                break;
+            }
+            case 'Q': {  // BINPERSID: ('storage', <StorageType global>, key, location, numel)
+                P pid = pop();
+                if (!pid || pid->kind != PObj::Tuple || pid->items.size() < 3 || pid->items[2]->kind != PObj::Str)
+                    return fail(err, "pickle: unsupported persistent id"), nullptr;
+                P st = make(PObj::Storage);
+                st->s = pid->items[2]->s;
+                const std::string& g = pid->items[1]->s;  // "torch FloatStorage"
+                st->s2 = g.substr(g.find(' ') + 1);
+                stack.push_back(st);
+                break;
+            }
+            case 0x81: {  // NEWOBJ
+                P args = pop(), cls = pop();
+                if (!cls) return fail(err, "pickle: bad NEWOBJ"), nullptr;
+                P o = make(PObj::Object);
+                o->cls = cls;
+                stack.push_back(o);
+                break;
+            }
+            case 'R': {  // REDUCE
+                P args = pop(), fn = pop();
+                if (!fn || !args || args->kind != PObj::Tuple) return fail(err, "pickle: bad REDUCE"), nullptr;
+                if (fn->kind == PObj::Global && fn->s == "torch._utils _rebuild_tensor_v2") {
+                    if (args->items.size() < 4 || args->items[0]->kind != PObj::Storage)
+                        return fail(err, "pickle: bad _rebuild_tensor_v2"), nullptr;
+                    P t = make(PObj::Tensor);
+                    t->storage = args->items[0];
+                    t->offset = args->items[1]->i;
+                    for (auto& x : args->items[2]->items) t->sizes.push_back(x->i);
+                    for (auto& x : args->items[3]->items) t->strides.push_back(x->i);
+                    stack.push_back(t);
+                } else if (fn->kind == PObj::Global && fn->s == "collections OrderedDict") {
+                    stack.push_back(make(PObj::Dict));
+                } else {
+                    P o = make(PObj::Object);
+                    o->cls = fn;
+                    o->state = args;
+                    stack.push_back(o);
+                }
+                break;
+            }
+            case 'b': {  // BUILD
+                P st = pop();
+                if (!st || stack.empty()) return fail(err, "pickle: bad BUILD"), nullptr;
+                if (stack.back()->kind == PObj::Object) stack.back()->state = st;
+                break;
+            }
+            case '.':
+                if (stack.empty()) return fail(err, "pickle: empty at STOP"), nullptr;
+                return stack.back();
+            default: {
+                char b[64];
+                snprintf(b, sizeof b, "pickle: unsupported opcode 0x%02x at %zu", op, i - 1);
+                fail(err, b);
+                return nullptr;
+            }
+        }
+    }
+    fail(err, "pickle: no STOP");
+    return nullptr;
+}
+
+size_t storage_elem_size(const std::string& t) {
+    static const std::map<std::string, size_t> m = {
+        {"FloatStorage", 4}, {"DoubleStorage", 8}, {"HalfStorage", 2}, {"BFloat16Storage", 2},
+        {"LongStorage", 8},  {"IntStorage", 4},    {"ShortStorage", 2}, {"CharStorage", 1},
+        {"ByteStorage", 1},  {"BoolStorage", 1}};
+    auto it = m.find(t);
+    return it == m.end() ? 0 : it->second;
+}
+
+// "__parameters__ = ["weight", "bias", ]" inside `class <name>(...)` of a code file.
+std::vector<std::string> class_parameters(const std::string& code, const std::string& cls) {
+    std::vector<std::string> out;
+    size_t c = code.find("class " + cls + "(");
+    if (c == std::string::npos) return out;
+    size_t end = code.find("\nclass ", c + 1);
+    size_t a = code.find("__parameters__ = [", c);
+    if (a == std::string::npos || (end != std::string::npos && a > end)) return out;
+    size_t b = code.find(']', a);
+    std::string lst = code.substr(a, b - a);
+    for (size_t q = lst.find('"'); q != std::string::npos; q = lst.find('"', q + 1)) {
+        size_t r = lst.find('"', q + 1);
+        if (r == std::string::npos) break;
+        out.push_back(lst.substr(q + 1, r - q - 1));
+        q = r;
+    }
+    return out;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ TorchArchive
+
+bool TorchArchive::parse(const uint8_t* bytes, size_t size, std::string* err) {
+    base_ = bytes;
+    size_ = size;
+    entries_.clear();
+    params_.clear();
+    buffers_.clear();
+    if (size < 22) return fail(err, "archive too small");
+    // end of central directory (+ zip64 records when present)
+    size_t eocd = std::string::npos;
+    for (size_t i = size - 22 + 1; i-- > 0 && size - i <= 22 + 65535;)
+        if (rd32(bytes + i) == 0x06054b50) {
+            eocd = i;
+            break;
+        }
+    if (eocd == std::string::npos) return fail(err, "zip: no end-of-central-directory record");
+    uint64_t n_entries = rd16(bytes + eocd + 10), cd_off = rd32(bytes + eocd + 16);
+    if (eocd >= 20 && rd32(bytes + eocd - 20) == 0x07064b50) {  // zip64 locator
+        const uint64_t z64 = rd64(bytes + eocd - 20 + 8);
+        if (z64 + 56 > size || rd32(bytes + z64) != 0x06064b50) return fail(err, "zip: bad zip64 record");
+        n_entries = rd64(bytes + z64 + 32);
+        cd_off = rd64(bytes + z64 + 48);
+    }
+    uint64_t q = cd_off;
+    for (uint64_t e = 0; e < n_entries; ++e) {
+        if (q + 46 > size || rd32(bytes + q) != 0x02014b50) return fail(err, "zip: bad central directory");
+        const uint16_t method = rd16(bytes + q + 10), nlen = rd16(bytes + q + 28), xlen = rd16(bytes + q + 30),
+                       clen = rd16(bytes + q + 32);
+        ZipEntry z;
+        z.crc = rd32(bytes + q + 16);
+        uint64_t csize = rd32(bytes + q + 20), usize = rd32(bytes + q + 24), loff = rd32(bytes + q + 42);
+        z.name.assign((const char*)bytes + q + 46, nlen);
+        // zip64 extended information: only the fields that are 0xFFFFFFFF are present, in this order
+        for (uint64_t x = q + 46 + nlen; x + 4 <= q + 46 + nlen + xlen;) {
+            const uint16_t id = rd16(bytes + x), len = rd16(bytes + x + 2);
+            if (id == 0x0001) {
+                uint64_t f = x + 4;
+                if (usize == 0xFFFFFFFFu) usize = rd64(bytes + f), f += 8;
+                if (csize == 0xFFFFFFFFu) csize = rd64(bytes + f), f += 8;
+                if (loff == 0xFFFFFFFFu) loff = rd64(bytes + f), f += 8;
+            }
+            x += 4 + len;
+        }
+        if (method != 0 && method != 8) return fail(err, "zip: record " + z.name + " uses an unsupported method");
+        if (method == 0 && csize != usize) return fail(err, "zip: stored record " + z.name + " has mismatched sizes");
+        z.method = method;
+        z.comp_size = csize;
+        if (loff + 30 > size || rd32(bytes + loff) != 0x04034b50) return fail(err, "zip: bad local header");
+        const uint16_t lflags = rd16(bytes + loff + 6);
+        z.data_offset = loff + 30 + rd16(bytes + loff + 26) + rd16(bytes + loff + 28);
+        z.size = usize;
+        z.cd_offset = q;
+        z.local_offset = loff;
+        if (z.data_offset + z.comp_size > size) return fail(err, "zip: record " + z.name + " out of bounds");
+        if (lflags & 0x08) {  // data descriptor follows the data, optionally with its signature
+            uint64_t d = z.data_offset + z.comp_size;
+            if (d + 4 <= size && rd32(bytes + d) == 0x08074b50) d += 4;
+            z.desc_offset = d;
+        }
+        entries_.push_back(z);
+        q += 46 + nlen + xlen + clen;
+    }
+    if (entries_.empty()) return fail(err, "zip: empty archive");
+    prefix_ = entries_[0].name.substr(0, entries_[0].name.find('/'));
+    std::map<std::string, int> by_name;
+    for (size_t k = 0; k < entries_.size(); ++k) by_name[entries_[k].name] = (int)k;
+    auto rec = [&](const std::string& n) -> const ZipEntry* {
+        auto it = by_name.find(prefix_ + "/" + n);
+        return it == by_name.end() ? nullptr : &entries_[it->second];
+    };
+    const ZipEntry* pkl = rec("data.pkl");
+    if (!pkl) return fail(err, "archive: no data.pkl");
+    if (pkl->method != 0) return fail(err, "archive: data.pkl is compressed");
+    std::string perr;
+    P root = unpickle(bytes + pkl->data_offset, pkl->size, &perr);
+    if (!root) return fail(err, perr);
+
+    // Walk the module tree: own attributes in registration order (parameters, buffers), then children
+    // -- exactly named_parameters(recurse=true) / named_buffers(recurse=true).
+    std::string werr;
+    std::map<std::string, std::string> code_cache;
+    std::function<bool(const P&, const std::string&, std::vector<TensorView>*, bool)> walk;
+    auto code_for = [&](const std::string& global) -> std::pair<std::string, std::string> {
+        // "__torch__.___torch_mangle_0 Module" -> (code/__torch__/___torch_mangle_0.py, "Module")
+        const size_t sp = global.find(' ');
+        std::string mod = global.substr(0, sp), cls = global.substr(sp + 1), path = "code/";
+        for (char ch : mod) path += ch == '.' ? '/' : ch;
+        path += ".py";
+        auto it = code_cache.find(path);
+        if (it == code_cache.end()) {
+            const ZipEntry* z = rec(path);
+            std::string text;
+            if (z && z->method == 0) {
+                text.assign((const char*)bytes + z->data_offset, z->size);
+            } else if (z) {  // raw deflate (libtorch compresses some code records)
+                text.resize(z->size);
+                z_stream zs{};
+                if (inflateInit2(&zs, -MAX_WBITS) == Z_OK) {
+                    zs.next_in = const_cast<Bytef*>(bytes + z->data_offset);
+                    zs.avail_in = (uInt)z->comp_size;
+                    zs.next_out = (Bytef*)&text[0];
+                    zs.avail_out = (uInt)z->size;
+                    const int rc = inflate(&zs, Z_FINISH);
+                    inflateEnd(&zs);
+                    if (rc != Z_STREAM_END) text.clear();
+                } else {
+                    text.clear();
+                }
+            }
+            it = code_cache.emplace(path, text).first;
+        }
+        return {it->second, cls};
+    };
+    walk = [&](const P& obj, const std::string& prefix, std::vector<TensorView>* out, bool want_params) -> bool {
+        if (!obj || obj->kind != PObj::Object || !obj->state || obj->state->kind != PObj::Dict) return true;
+        auto code = code_for(obj->cls ? obj->cls->s : std::string());
+        const std::vector<std::string> pnames = class_parameters(code.first, code.second);
+        std::vector<std::pair<P, std::string>> children;
+        for (auto& kv : obj->state->dict) {
+            if (!kv.first || kv.first->kind != PObj::Str) continue;
+            const std::string& key = kv.first->s;
+            const P& v = kv.second;
+            if (v->kind == PObj::Tensor) {
+                const bool is_param = std::find(pnames.begin(), pnames.end(), key) != pnames.end();
+                if (is_param != want_params) continue;
+                TensorView tv;
+                tv.name = prefix + key;
+                tv.storage_type = v->storage->s2;
+                tv.elem_size = storage_elem_size(tv.storage_type);
+                if (!tv.elem_size) return fail(&werr, "archive: unknown storage " + tv.storage_type);
+                tv.sizes = v->sizes;
+                tv.strides = v->strides;
+                tv.storage_offset = v->offset;
+                tv.numel = 1;
+                for (auto s : tv.sizes) tv.numel *= s;
+                int64_t expect = 1;
+                tv.contiguous = true;
+                for (size_t d = tv.sizes.size(); d-- > 0;) {
+                    if (tv.sizes[d] != 1 && tv.strides[d] != expect) tv.contiguous = false;
+                    expect *= tv.sizes[d];
+                }
+                auto it = by_name.find(prefix_ + "/data/" + v->storage->s);
+                if (it == by_name.end()) return fail(&werr, "archive: missing storage record " + v->storage->s);
+                tv.record = it->second;
+                const ZipEntry& z = entries_[tv.record];
+                if (z.method != 0) return fail(&werr, "archive: tensor record " + z.name + " is compressed");
+                int64_t max_index = tv.storage_offset;
+                for (size_t d = 0; d < tv.sizes.size(); ++d)
+                    if (tv.sizes[d] > 0) max_index += (tv.sizes[d] - 1) * tv.strides[d];
+                if (tv.numel > 0 && (uint64_t)(max_index + 1) * tv.elem_size > z.size)
+                    return fail(&werr, "archive: tensor " + tv.name + " exceeds its storage");
+                tv.data = bytes + z.data_offset + (uint64_t)tv.storage_offset * tv.elem_size;
+                out->push_back(tv);
+            } else if (v->kind == PObj::Object) {
+                children.emplace_back(v, prefix + key + ".");
+            }
+        }
+        for (auto& c : children)
+            if (!walk(c.first, c.second, out, want_params)) return false;
+        return true;
+    };
+    if (!walk(root, "", &params_, true) || !walk(root, "", &buffers_, false)) return fail(err, werr);
+    return true;
+}
+
+int64_t TorchArchive::param_numel() const {
+    int64_t n = 0;
+    for (auto& t : params_) n += t.numel;
+    return n;
+}
+
+bool TorchArchive::params_are_float() const {
+    for (auto& t : params_)
+        if (t.storage_type != "FloatStorage") return false;
+    return true;
+}
+
+bool TorchArchive::param_segments(std::vector<const void*>* ptrs, std::vector<size_t>* bytes) const {
+    ptrs->clear();
+    bytes->clear();
+    for (auto& t : params_) {
+        if (!t.contiguous || t.storage_type != "FloatStorage") return false;
+        if (t.numel == 0) continue;
+        ptrs->push_back(t.data);
+        bytes->push_back((size_t)t.numel * 4);
+    }
+    return true;
+}
+
+bool TorchArchive::gather_params(float* dst, std::string* err) const {
+    for (auto& t : params_) {
+        if (t.storage_type != "FloatStorage") return fail(err, "parameter " + t.name + " is not fp32");
+        if (t.contiguous) {
+            std::memcpy(dst, t.data, (size_t)t.numel * 4);
+        } else {  // strided: walk the index space in row-major order
+            std::vector<int64_t> idx(t.sizes.size(), 0);
+            for (int64_t e = 0; e < t.numel; ++e) {
+                int64_t off = 0;
+                for (size_t d = 0; d < idx.size(); ++d) off += idx[d] * t.strides[d];
+                std::memcpy(dst + e, t.data + off * 4, 4);
+                for (size_t d = idx.size(); d-- > 0;) {
+                    if (++idx[d] < t.sizes[d]) break;
+                    idx[d] = 0;
+                }
+            }
+        }
+        dst += t.numel;
+    }
+    return true;
+}
+
+bool TorchArchive::with_params(const float* src, std::string* out, std::string* err) const {
+    out->assign((const char*)base_, size_);
+    uint8_t* o = (uint8_t*)&(*out)[0];
+    std::vector<char> touched(entries_.size(), 0);
+    for (auto& t : params_) {
+        if (t.storage_type != "FloatStorage") return fail(err, "parameter " + t.name + " is not fp32");
+        uint8_t* d = o + (t.data - base_);
+        if (t.contiguous) {
+            std::memcpy(d, src, (size_t)t.numel * 4);
+        } else {
+            std::vector<int64_t> idx(t.sizes.size(), 0);
+            for (int64_t e = 0; e < t.numel; ++e) {
+                int64_t off = 0;
+                for (size_t k = 0; k < idx.size(); ++k) off += idx[k] * t.strides[k];
+                std::memcpy(d + off * 4, src + e, 4);
+                for (size_t k = idx.size(); k-- > 0;) {
+                    if (++idx[k] < t.sizes[k]) break;
+                    idx[k] = 0;
+                }
+            }
+        }
+        src += t.numel;
+        touched[t.record] = 1;
+    }
+    for (size_t k = 0; k < entries_.size(); ++k) {
+        if (!touched[k]) continue;
+        const ZipEntry& z = entries_[k];
+        const uint32_t c = crc32(o + z.data_offset, z.size);
+        wr32(o + z.cd_offset + 16, c);
+        if (z.desc_offset) wr32(o + z.desc_offset, c);   // flag bit 3: CRC lives in the data descriptor
+        else wr32(o + z.local_offset + 14, c);           // otherwise in the local header
+    }
+    return true;
+}
+
+}  // namespace fahost

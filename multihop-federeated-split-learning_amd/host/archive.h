@@ -1,0 +1,77 @@
+// archive.h -- zero-copy view of a libtorch `torch::save(module)` archive.
+//
+// The reference ships every model part between data owners and the aggregator
+// as the bytes of `torch::save(task.model_part_, s)` (network_layer.cpp:305-313)
+// and decodes them with `torch::load` (aggregator.cpp:63-64, ~0.5 GiB/s).  The
+// archive is a zip of STORED (uncompressed, 64-byte aligned) records:
+//   <prefix>/data.pkl            pickled module tree (protocol 2)
+//   <prefix>/data/<key>          raw little-endian tensor storages
+//   <prefix>/code/__torch__/*.py class declarations: __parameters__ / __buffers__
+// This reader maps the tensors in place (no copy) in `named_parameters()`
+// order -- the order aggregator.cpp:72-88 iterates -- and can emit a copy of
+// the archive with new parameter values and rewritten CRC-32s, which
+// `torch::load` on the data owner accepts (data_owner.cpp:232-253).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace fahost {
+
+struct ZipEntry {
+    std::string name;
+    uint64_t data_offset = 0;   // first byte of the stored data
+    uint64_t size = 0;          // uncompressed size
+    uint64_t comp_size = 0;     // bytes on disk (== size for stored records)
+    uint16_t method = 0;        // 0 stored, 8 deflate (only non-tensor records may be deflated)
+    uint32_t crc = 0;
+    uint64_t cd_offset = 0;     // central-directory header of this entry
+    uint64_t local_offset = 0;  // local header of this entry
+    uint64_t desc_offset = 0;   // data descriptor after the data (0 if none)
+};
+
+struct TensorView {
+    std::string name;           // dotted path, e.g. "0.conv1.weight"
+    std::string storage_type;   // "FloatStorage", "BFloat16Storage", "LongStorage", ...
+    size_t elem_size = 0;
+    std::vector<int64_t> sizes, strides;
+    int64_t storage_offset = 0; // elements
+    int64_t numel = 0;
+    bool contiguous = false;
+    int record = -1;            // index into entries()
+    const uint8_t* data = nullptr;  // first element (storage + offset) inside the archive bytes
+};
+
+class TorchArchive {
+public:
+    // Parses `bytes[0, size)`; the memory must outlive the object (views point into it).
+    bool parse(const uint8_t* bytes, size_t size, std::string* err);
+
+    const std::vector<ZipEntry>& entries() const { return entries_; }
+    const std::vector<TensorView>& params() const { return params_; }   // named_parameters(true) order
+    const std::vector<TensorView>& buffers() const { return buffers_; } // named_buffers(true) order
+    int64_t param_numel() const;
+    bool params_are_float() const;
+
+    // Contiguous pieces of the parameter bucket, in order (one per contiguous fp32 param):
+    // a gather list for fa_submit_gather.  Returns false if some param is not contiguous fp32.
+    bool param_segments(std::vector<const void*>* ptrs, std::vector<size_t>* bytes) const;
+    // Strided-safe copy of all parameters (as fp32) into dst[param_numel()].
+    bool gather_params(float* dst, std::string* err) const;
+    // A copy of the archive bytes with every parameter replaced by src (fp32, named order) and
+    // the CRC-32 of every rewritten record updated in its data descriptor and central directory.
+    bool with_params(const float* src, std::string* out, std::string* err) const;
+
+private:
+    const uint8_t* base_ = nullptr;
+    size_t size_ = 0;
+    std::string prefix_;
+    std::vector<ZipEntry> entries_;
+    std::vector<TensorView> params_, buffers_;
+};
+
+uint32_t crc32(const uint8_t* p, size_t n, uint32_t crc = 0);
+
+}  // namespace fahost

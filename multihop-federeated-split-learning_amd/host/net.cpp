@@ -1,0 +1,366 @@
+// net.cpp -- see net.h.
+#include "net.h"
+
+#include <arpa/inet.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/select.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstring>
+#include <iostream>
+
+namespace fahost {
+
+namespace {
+long now_ms() {
+    return std::chrono::duration_cast<std::chrono::milliseconds>(
+               std::chrono::system_clock::now().time_since_epoch())
+        .count();
+}
+}  // namespace
+
+// ------------------------------------------------------------------ routing
+
+RoutingTable::RoutingTable(int base) {
+    const int d = base - 8079;
+    t_[-2] = {"localhost", 8079 + d};
+    t_[-1] = {"localhost", 8080 + d};
+    t_[0] = {"localhost", 8081 + d};
+    t_[1] = {"localhost", 8082 + d};
+    t_[2] = {"localhost", 8083 + d};
+    t_[3] = {"localhost", 8083 + d};
+    t_[18] = {"localhost", 8081 + d};
+}
+
+int RoutingTable::port_for(int id) const {
+    if (id > 3 && id < 18) return t_.at(0).second + id + 3;   // network_layer.cpp:510-514
+    if (id >= 18) return t_.at(18).second + (id - 18);         // :530-534
+    auto it = t_.find(id);
+    return it == t_.end() ? -1 : it->second.second;
+}
+
+std::string RoutingTable::host_for(int id) const {
+    auto it = t_.find(id);
+    return it == t_.end() ? std::string("localhost") : it->second.first;
+}
+
+void RoutingTable::set_host(int id, const std::string& host) {
+    auto it = t_.find(id);
+    if (it == t_.end()) t_[id] = {host, port_for(id)};
+    else it->second.first = host;
+}
+
+void RoutingTable::apply(const std::vector<std::pair<int, std::string>>& table) {
+    for (auto& e : table) {  // systemAPI.cpp:200-255
+        if (e.first > 3 && e.first < 18) t_[e.first] = {e.second, t_.at(0).second + e.first + 3};
+        else if (e.first >= 18) t_[e.first] = {e.second, t_.at(18).second + (e.first - 18)};
+        else t_[e.first].first = e.second;
+    }
+}
+
+// ------------------------------------------------------------------ socket helpers
+
+bool send_all(int fd, const void* p, size_t n) {
+    const char* c = static_cast<const char*>(p);
+    while (n > 0) {
+        ssize_t k = ::send(fd, c, n, MSG_NOSIGNAL);
+        if (k <= 0) return false;
+        c += k;
+        n -= (size_t)k;
+    }
+    return true;
+}
+
+static bool recv_all(int fd, void* p, size_t n) {
+    char* c = static_cast<char*>(p);
+    while (n > 0) {
+        ssize_t k = ::recv(fd, c, n, 0);
+        if (k <= 0) return false;
+        c += k;
+        n -= (size_t)k;
+    }
+    return true;
+}
+
+bool recv_frame(int fd, std::string* text) {
+    int32_t len = 0;
+    if (!recv_all(fd, &len, 4) || len < 0) return false;
+    text->resize((size_t)len);
+    return len == 0 || recv_all(fd, &(*text)[0], (size_t)len);
+}
+
+int connect_to(const std::string& host, int port, int tries, int wait_ms) {
+    for (int t = 0; t < tries; ++t) {
+        addrinfo hints{}, *res = nullptr;
+        hints.ai_family = AF_INET;
+        hints.ai_socktype = SOCK_STREAM;
+        if (getaddrinfo(host == "localhost" ? "127.0.0.1" : host.c_str(), std::to_string(port).c_str(), &hints,
+                        &res) == 0) {
+            int fd = socket(AF_INET, SOCK_STREAM, 0);
+            if (fd >= 0 && ::connect(fd, res->ai_addr, res->ai_addrlen) == 0) {
+                freeaddrinfo(res);
+                int one = 1;
+                setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+                return fd;
+            }
+            if (fd >= 0) close(fd);
+            freeaddrinfo(res);
+        }
+        std::this_thread::sleep_for(std::chrono::milliseconds(wait_ms));  // the reference retries every 4 s
+    }
+    return -1;
+}
+
+// ------------------------------------------------------------------ NetLayer
+
+NetLayer::~NetLayer() { stop(); }
+
+bool NetLayer::start(int port) {
+    port_ = port >= 0 ? port : routes_.port_for(my_id_);
+    listen_fd_ = socket(AF_INET, SOCK_STREAM, 0);
+    if (listen_fd_ < 0) return false;
+    int one = 1;
+    setsockopt(listen_fd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_addr.s_addr = INADDR_ANY;
+    a.sin_port = htons((uint16_t)port_);
+    if (bind(listen_fd_, (sockaddr*)&a, sizeof a) < 0 || listen(listen_fd_, 64) < 0) {
+        close(listen_fd_);
+        listen_fd_ = -1;
+        return false;
+    }
+    running_ = true;
+    rx_ = std::thread(&NetLayer::receiver_loop, this);
+    tx_ = std::thread(&NetLayer::sender_loop, this);
+    return true;
+}
+
+void NetLayer::stop() {
+    if (!running_.exchange(false)) return;
+    cv_tx_.notify_all();
+    if (listen_fd_ >= 0) {
+        shutdown(listen_fd_, SHUT_RDWR);
+        close(listen_fd_);
+        listen_fd_ = -1;
+    }
+    if (rx_.joinable()) rx_.join();
+    if (tx_.joinable()) tx_.join();
+    for (auto& kv : open_out_) close(kv.second);
+    open_out_.clear();
+}
+
+void NetLayer::handle_frame(std::shared_ptr<std::string> text, int fd, bool* keep) {
+    (void)fd;
+    Message m;
+    std::string err;
+    // Parse the header without copying the archive: decode a view that stops before `values`.
+    const size_t vpos = text->find("values : ");
+    std::string head = vpos == std::string::npos ? *text : text->substr(0, vpos) + "values : ,\n}";
+    if (!decode(head, &m, &err)) {
+        std::cerr << "[net] dropping malformed frame: " << err << "\n";
+        return;
+    }
+    *keep = m.save_connection == 1;
+    if (m.type == OPERATION) {
+        Receipt r;
+        r.client_id = m.client_id;
+        r.prev_node = m.prev_node;
+        r.model_part = m.model_part;
+        r.type_op = m.type_op;
+        r.t_start = m.t_start;
+        if (vpos != std::string::npos) {
+            r.blob_off = vpos + 9;
+            r.blob_len = text->size() >= r.blob_off + 3 ? text->size() - 3 - r.blob_off : 0;
+        }
+        if (link_mbps_ > 0) {  // network_layer.cpp:654-665, opt-in
+            const long due = r.t_start + (long)(text->size() * 8.0 / (link_mbps_ * 1e6) * 1000.0);
+            const long now = now_ms();
+            if (due > now) std::this_thread::sleep_for(std::chrono::milliseconds(due - now));
+        }
+        r.frame = std::move(text);
+        {
+            std::lock_guard<std::mutex> lk(m_rx_);
+            receipts_.push_back(std::move(r));
+        }
+        cv_rx_.notify_all();
+    } else {
+        if (m.read_table == 1) routes_.apply(m.rooting_table);
+        {
+            std::lock_guard<std::mutex> lk(m_rx_);
+            refactors_.push_back(std::move(m));
+        }
+        cv_rx_.notify_all();
+    }
+}
+
+void NetLayer::receiver_loop() {
+    std::vector<int> open;  // connections kept open by save_connection == 1
+    while (running_) {
+        fd_set rs;
+        FD_ZERO(&rs);
+        int maxfd = listen_fd_;
+        if (listen_fd_ < 0) break;
+        FD_SET(listen_fd_, &rs);
+        for (int fd : open) {
+            FD_SET(fd, &rs);
+            maxfd = std::max(maxfd, fd);
+        }
+        timeval tv{0, 200000};
+        int n = select(maxfd + 1, &rs, nullptr, nullptr, &tv);
+        if (n <= 0) continue;
+        for (size_t i = 0; i < open.size();) {
+            int fd = open[i];
+            if (FD_ISSET(fd, &rs)) {
+                auto text = std::make_shared<std::string>();
+                bool keep = true;
+                if (!recv_frame(fd, text.get()) || text->empty()) {
+                    close(fd);
+                    open.erase(open.begin() + (long)i);
+                    continue;
+                }
+                bytes_rx_ += text->size() + 4;
+                handle_frame(text, fd, &keep);
+            }
+            ++i;
+        }
+        if (listen_fd_ >= 0 && FD_ISSET(listen_fd_, &rs)) {
+            int fd = accept(listen_fd_, nullptr, nullptr);
+            if (fd < 0) continue;
+            auto text = std::make_shared<std::string>();
+            bool keep = false;
+            if (recv_frame(fd, text.get()) && !text->empty()) {
+                bytes_rx_ += text->size() + 4;
+                handle_frame(text, fd, &keep);
+            }
+            if (keep) open.push_back(fd);
+            else close(fd);
+        }
+    }
+    for (int fd : open) close(fd);
+}
+
+void NetLayer::sender_loop() {
+    while (true) {
+        Out o;
+        {
+            std::unique_lock<std::mutex> lk(m_tx_);
+            cv_tx_.wait(lk, [&] { return !outq_.empty() || !running_; });
+            if (outq_.empty()) break;
+            o = outq_.front();
+            outq_.pop_front();
+            tx_busy_ = true;
+        }
+        int fd = -1;
+        auto it = open_out_.find(o.dest);
+        if (it != open_out_.end()) fd = it->second;
+        if (fd < 0) fd = connect_to(routes_.host_for(o.dest), routes_.port_for(o.dest), 100, 200);
+        if (fd < 0) {
+            std::cerr << "[net] cannot reach node " << o.dest << " at " << routes_.host_for(o.dest) << ":"
+                      << routes_.port_for(o.dest) << "\n";
+        } else if (!send_all(fd, o.bytes->data(), o.bytes->size())) {
+            std::cerr << "[net] send to node " << o.dest << " failed\n";
+            close(fd);
+            open_out_.erase(o.dest);
+        } else if (o.keep) {
+            open_out_[o.dest] = fd;
+        } else {
+            close(fd);
+            open_out_.erase(o.dest);
+        }
+        {
+            std::lock_guard<std::mutex> lk(m_tx_);
+            tx_busy_ = false;
+        }
+        cv_tx_idle_.notify_all();
+    }
+}
+
+void NetLayer::send(int dest, std::shared_ptr<const std::string> framed, bool keep_open) {
+    {
+        std::lock_guard<std::mutex> lk(m_tx_);
+        outq_.push_back({dest, std::move(framed), keep_open});
+    }
+    cv_tx_.notify_one();
+}
+
+void NetLayer::flush() {
+    std::unique_lock<std::mutex> lk(m_tx_);
+    cv_tx_idle_.wait(lk, [&] { return outq_.empty() && !tx_busy_; });
+}
+
+Receipt NetLayer::next_receipt() {
+    std::unique_lock<std::mutex> lk(m_rx_);
+    cv_rx_.wait(lk, [&] { return !receipts_.empty(); });
+    Receipt r = std::move(receipts_.front());
+    receipts_.pop_front();
+    return r;
+}
+
+bool NetLayer::try_next_receipt(Receipt* r, int timeout_ms) {
+    std::unique_lock<std::mutex> lk(m_rx_);
+    if (!cv_rx_.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return !receipts_.empty(); })) return false;
+    *r = std::move(receipts_.front());
+    receipts_.pop_front();
+    return true;
+}
+
+Message NetLayer::next_refactor() {
+    std::unique_lock<std::mutex> lk(m_rx_);
+    cv_rx_.wait(lk, [&] { return !refactors_.empty(); });
+    Message m = std::move(refactors_.front());
+    refactors_.pop_front();
+    return m;
+}
+
+bool NetLayer::find_init(int timeout_s, std::string* err) {
+    // Announce (network_layer.cpp:215-227).
+    int u = socket(AF_INET, SOCK_DGRAM, 0);
+    if (u < 0) return *err = "udp socket", false;
+    sockaddr_in g{};
+    g.sin_family = AF_INET;
+    g.sin_addr.s_addr = inet_addr("224.0.0.0");
+    g.sin_port = htons(4321);
+    int id = my_id_;
+    sendto(u, &id, sizeof id, 0, (sockaddr*)&g, sizeof g);
+    close(u);
+    // The init node connects to my port and sends "ACK" (findPeers, :164-186); its address is the init's.
+    int s = socket(AF_INET, SOCK_STREAM, 0);
+    int one = 1;
+    setsockopt(s, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_addr.s_addr = INADDR_ANY;
+    a.sin_port = htons((uint16_t)routes_.port_for(my_id_));
+    if (bind(s, (sockaddr*)&a, sizeof a) < 0 || listen(s, 4) < 0) {
+        close(s);
+        return *err = "bind for discovery", false;
+    }
+    fd_set rs;
+    FD_ZERO(&rs);
+    FD_SET(s, &rs);
+    timeval tv{timeout_s, 0};
+    if (select(s + 1, &rs, nullptr, nullptr, &tv) <= 0) {
+        close(s);
+        return *err = "no init node connected", false;
+    }
+    sockaddr_in c{};
+    socklen_t cl = sizeof c;
+    int fd = accept(s, (sockaddr*)&c, &cl);
+    if (fd >= 0) {
+        char ip[INET_ADDRSTRLEN];
+        inet_ntop(AF_INET, &c.sin_addr, ip, sizeof ip);
+        routes_.set_host(0, ip);
+        char buf[256];
+        (void)::recv(fd, buf, sizeof buf, 0);
+        close(fd);
+    }
+    close(s);
+    return fd >= 0;
+}
+
+}  // namespace fahost

@@ -1,0 +1,114 @@
+// net.h -- the aggregator's side of the reference's task-delivery layer
+// (pipeline_simulation/network_layer.{h,cpp}), wire-compatible.
+//
+// Threading model kept from the reference (network_layer.h:49-63, .cpp:372-480):
+// one receiver thread (select/accept, frames -> FIFO task queue under a mutex +
+// condvar), one sender thread (queue of outgoing frames, connect with retries,
+// close unless save_connection), and the main thread as the single consumer.
+// Differences, all deliberate:
+//  * a receipt keeps the frame bytes it arrived in and points at the archive
+//    inside them (the reference makes ~10 full copies);
+//  * an outgoing frame is built once and shared by every destination (the
+//    reference re-serializes per destination, network_layer.cpp:305-313);
+//  * the 8 Mbit/s link emulation (network_layer.cpp:654-665) is opt-in.
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "wire.h"
+
+namespace fahost {
+
+// network_layer.h:80-86 plus the port rules of network_layer.cpp:510-538 and systemAPI.cpp:222-251.
+// `base` shifts every default port (reference: base 8079 -> id -2 on 8079, -1 on 8080, 0 on 8081).
+class RoutingTable {
+public:
+    explicit RoutingTable(int base = 8079);
+    int port_for(int id) const;
+    std::string host_for(int id) const;
+    void set_host(int id, const std::string& host);
+    // systemAPI::refactor's update from the refactor message's rooting table.
+    void apply(const std::vector<std::pair<int, std::string>>& table);
+
+private:
+    std::map<int, std::pair<std::string, int>> t_;
+};
+
+struct Receipt {  // Task.h:30-51, the fields the aggregation path uses
+    int client_id = -1, prev_node = -1, model_part = 1, type_op = -1;
+    long t_start = 0;
+    std::shared_ptr<const std::string> frame;  // owns the bytes
+    size_t blob_off = 0, blob_len = 0;         // the torch::save archive inside `frame`
+    const uint8_t* blob() const { return (const uint8_t*)frame->data() + blob_off; }
+};
+
+class NetLayer {
+public:
+    NetLayer(int my_id, RoutingTable routes) : my_id_(my_id), routes_(std::move(routes)) {}
+    ~NetLayer();
+
+    // Receiver thread on routes.port_for(my_id) (or `port` when >= 0).  Returns false if bind fails.
+    bool start(int port = -1);
+    void stop();
+    int listen_port() const { return port_; }
+
+    // findInit (network_layer.cpp:197-291): announce my id on 224.0.0.0:4321 and accept the init
+    // node's TCP connection on my port to learn its address.  Optional (loopback runs skip it).
+    bool find_init(int timeout_s, std::string* err);
+
+    // Link emulation: receipts are held until t_start + bytes*8/(mbps*1e6) s (0 = off).
+    void set_link_mbps(double mbps) { link_mbps_ = mbps; }
+
+    Receipt next_receipt();      // blocking FIFO pop (check_new_task for a data owner, :392-409)
+    Message next_refactor();     // blocking (check_new_refactor_task, :481-493)
+    bool try_next_receipt(Receipt* r, int timeout_ms);
+
+    // Queue a length-prefixed frame for `dest` (shared across destinations).
+    void send(int dest, std::shared_ptr<const std::string> framed, bool keep_open = false);
+    void flush();                // wait until the send queue is empty
+
+    RoutingTable& routes() { return routes_; }
+    uint64_t bytes_received() const { return bytes_rx_; }
+
+private:
+    void receiver_loop();
+    void sender_loop();
+    void handle_frame(std::shared_ptr<std::string> text, int fd, bool* keep);
+
+    int my_id_;
+    RoutingTable routes_;
+    int port_ = -1, listen_fd_ = -1;
+    double link_mbps_ = 0;
+    std::atomic<bool> running_{false};
+    std::atomic<uint64_t> bytes_rx_{0};
+    std::thread rx_, tx_;
+    std::mutex m_rx_;
+    std::condition_variable cv_rx_;
+    std::deque<Receipt> receipts_;
+    std::deque<Message> refactors_;
+    struct Out {
+        int dest;
+        std::shared_ptr<const std::string> bytes;
+        bool keep;
+    };
+    std::mutex m_tx_;
+    std::condition_variable cv_tx_, cv_tx_idle_;
+    std::deque<Out> outq_;
+    bool tx_busy_ = false;
+    std::map<int, int> open_out_;  // dest -> socket kept open (save_connection)
+};
+
+// Blocking helpers shared with the test tools.
+bool send_all(int fd, const void* p, size_t n);
+bool recv_frame(int fd, std::string* text);  // [int32 len][len bytes]; false on EOF / error
+int connect_to(const std::string& host, int port, int tries, int wait_ms);
+
+}  // namespace fahost

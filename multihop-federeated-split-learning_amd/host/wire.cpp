@@ -1,0 +1,158 @@
+// wire.cpp -- Message.h frame encoder/decoder (see wire.h for the grammar).
+#include "wire.h"
+
+#include <cstring>
+#include <map>
+#include <sstream>
+
+namespace fahost {
+
+namespace {
+
+std::string ints_str(const std::vector<int>& v) {  // getStr<std::vector<int>>, Message.h:181-190
+    std::string t = "[ ";
+    for (int x : v) t += std::to_string(x) + " ";
+    return t + "]";
+}
+
+std::string table_str(const std::vector<std::pair<int, std::string>>& v) {  // Message.h:202-211
+    std::string t = "[ ";
+    for (auto& e : v) t += std::to_string(e.first) + "," + e.second + " ";
+    return t + "]";
+}
+
+std::vector<int> parse_ints(const std::string& s) {  // getValue<std::vector<int>>, Message.h:268-280
+    std::vector<int> out;
+    std::stringstream ss(s);
+    std::string tok;
+    while (std::getline(ss, tok, ' '))
+        if (tok != "[" && tok != "]" && !tok.empty()) out.push_back(std::stoi(tok));
+    return out;
+}
+
+std::vector<std::pair<int, std::string>> parse_table(const std::string& s) {  // Message.h:296-316
+    std::vector<std::pair<int, std::string>> out;
+    std::stringstream ss(s);
+    std::string tok;
+    while (std::getline(ss, tok, ' ')) {
+        if (tok == "[" || tok == "]" || tok.empty()) continue;
+        const size_t c = tok.find(',');
+        out.emplace_back(std::stoi(tok.substr(0, c)), c == std::string::npos ? "" : tok.substr(c + 1, tok.find(',', c + 1) - c - 1));
+    }
+    return out;
+}
+
+void field(std::string& t, const char* name, const std::string& v) {
+    t += name;
+    t += " : ";
+    t += v;
+    t += ",\n";
+}
+
+}  // namespace
+
+std::string encode(const Message& m) {
+    std::string t = "{,\n";
+    field(t, "save_connection", std::to_string(m.save_connection));
+    field(t, "type", std::to_string(m.type));
+    if (m.type == OPERATION) {
+        field(t, "client_id", std::to_string(m.client_id));
+        field(t, "prev_node", std::to_string(m.prev_node));
+        field(t, "size_", std::to_string(m.size_));
+        field(t, "type_op", std::to_string(m.type_op));
+        field(t, "model_part", std::to_string(m.model_part));
+        field(t, "t_start", std::to_string(m.t_start));
+        field(t, "batch0", std::to_string(m.batch0));
+        t.reserve(t.size() + m.values.size() + 16);
+        field(t, "values", m.values);
+    } else {
+        field(t, "start", std::to_string(m.start));
+        field(t, "end", std::to_string(m.end));
+        field(t, "prev", std::to_string(m.prev));
+        field(t, "next", std::to_string(m.next));
+        field(t, "dataset", std::to_string(m.dataset));
+        field(t, "num_classes", std::to_string(m.num_classes));
+        field(t, "model_name", std::to_string(m.model_name));
+        field(t, "model_type", std::to_string(m.model_type));
+        field(t, "data_owners", ints_str(m.data_owners));
+        field(t, "rooting_table", table_str(m.rooting_table));
+        field(t, "read_table", std::to_string(m.read_table));
+    }
+    return t + "}";
+}
+
+std::string frame(const Message& m) {
+    const std::string text = encode(m);
+    std::string f(4, '\0');
+    const int32_t len = (int32_t)text.size();
+    std::memcpy(&f[0], &len, 4);  // native-endian int, as my_send does (network_layer.cpp:16)
+    return f + text;
+}
+
+bool decode(const std::string& text, Message* m, std::string* err) {
+    // fromStr_toJson (Message.h:499-569): split on ",\n", name/value on " : "; `values`
+    // swallows the rest of the text minus the closing ",\n}".
+    std::map<std::string, std::string> kv;
+    size_t pos = 0;
+    while (pos < text.size()) {
+        if (text.compare(pos, 6, "values") == 0) {
+            const size_t sep = text.find(" : ", pos);
+            if (sep == std::string::npos || text.size() < pos + 3) break;
+            const size_t vb = sep + 3, ve = text.size() >= 3 ? text.size() - 3 : vb;
+            kv["values"] = ve > vb ? text.substr(vb, ve - vb) : std::string();
+            break;
+        }
+        size_t nl = text.find(",\n", pos);
+        std::string tok = text.substr(pos, nl == std::string::npos ? std::string::npos : nl - pos);
+        pos = nl == std::string::npos ? text.size() : nl + 2;
+        if (tok == "{" || tok == "}" || tok.empty()) continue;
+        const size_t sep = tok.find(" : ");
+        if (sep == std::string::npos) continue;
+        kv[tok.substr(0, sep)] = tok.substr(sep + 3);
+    }
+    auto geti = [&](const char* k, int* out) -> bool {
+        auto it = kv.find(k);
+        if (it == kv.end()) {
+            if (err) *err = std::string("missing field ") + k;
+            return false;
+        }
+        try {
+            *out = std::stoi(it->second);
+        } catch (...) {
+            if (err) *err = std::string("bad integer in ") + k;
+            return false;
+        }
+        return true;
+    };
+    Message r;
+    if (!geti("save_connection", &r.save_connection) || !geti("type", &r.type)) return false;
+    if (r.type == OPERATION) {
+        if (!geti("client_id", &r.client_id) || !geti("prev_node", &r.prev_node) || !geti("size_", &r.size_) ||
+            !geti("type_op", &r.type_op) || !geti("model_part", &r.model_part) || !geti("batch0", &r.batch0))
+            return false;
+        auto t = kv.find("t_start");
+        if (t == kv.end()) {
+            if (err) *err = "missing field t_start";
+            return false;
+        }
+        r.t_start = std::stol(t->second);
+        auto v = kv.find("values");
+        if (v == kv.end()) {
+            if (err) *err = "missing field values";
+            return false;
+        }
+        r.values = std::move(v->second);
+    } else {
+        if (!geti("start", &r.start) || !geti("end", &r.end) || !geti("prev", &r.prev) || !geti("next", &r.next) ||
+            !geti("dataset", &r.dataset) || !geti("num_classes", &r.num_classes) ||
+            !geti("model_name", &r.model_name) || !geti("model_type", &r.model_type) ||
+            !geti("read_table", &r.read_table))
+            return false;
+        r.data_owners = parse_ints(kv["data_owners"]);
+        r.rooting_table = parse_table(kv["rooting_table"]);
+    }
+    *m = std::move(r);
+    return true;
+}
+
+}  // namespace fahost

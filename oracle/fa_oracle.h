@@ -19,7 +19,7 @@
  *     `.to(bf16)`).
  *
  * Parity pin: tests/golden/ holds vectors produced by oracle/_ref/ref_harness,
- * a harness linking the reference's own model builders (models/*.cpp) and
+ * a harness linking the reference's own model builders (models/{resnet,vgg,lenet5}) and
  * libtorch ops (tools/gen_golden.py); tests/test_oracle.py checks this file
  * against them bit-for-bit.
  */

@@ -17,7 +17,7 @@
 //
 // Modes (all write JSON to stdout):
 //   layout  <name> <type> <start> <end> <nc>
-//   golden  <name> <type> <start> <end> <nc> <D> <seed> <wseed> <outdir> [blob_mp]
+//   golden  <name> <type> <start> <end> <nc> <D> <seed> <wseed> <outdir> [blob_mp; -1 = every bucket <= 200k]
 //   bench-fedavg <n> <D> <threads> <reps>
 //   bench-literal <name> <type> <start> <end> <nc> <D> <threads> <model_part>
 #include <chrono>
@@ -199,7 +199,7 @@ int cmd_golden(int argc, char** argv) {
             auto cm = client_module(name, type, start, end, nc, b.model_part);
             fill_client(cm, sb, k);
             std::string blob = save_blob(cm);
-            if (k == 0 && blob_mp == b.model_part)
+            if (k == 0 && (blob_mp == b.model_part || (blob_mp < 0 && param_numel(cm) <= 200000)))
                 write_bin(outdir + "/mp" + std::to_string(b.model_part) + "_client0.pt", blob.data(), blob.size());
             auto x = flat_params(cm);
             if (k == 0) {

@@ -1,0 +1,225 @@
+// fake_owners.cpp -- TEST TOOL: the init node + D data owners of the reference,
+// as far as the aggregator sees them (data_owner.cpp:96-112 refactor, :224-253
+// aggregation exchange), in one process.  Each owner sends synthetic model
+// parts built from template archives (tests/golden/<cfg>/mp<m>_client0.pt, made
+// by the reference's own builders) with parameters from the oracle's generator,
+// collects the aggregator's replies and checks them bit-for-bit against the
+// oracle (oracle/fa_oracle.c: links the checker, never the product).
+//
+//   fa_fake_owners --blobs DIR --parts 1,2,3 -d D -c C [--rounds R] [--mode fedavg|literal]
+//                  [--port-base P] [--model-name N --model-type T --start S --end E] [--seed X]
+// Prints one JSON line: {"ok": bool, "rounds": R, "checked_elems": ..., "round_ms": [...]}.
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <map>
+#include <set>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "archive.h"
+#include "fa_oracle.h"
+#include "net.h"
+
+using namespace fahost;
+
+namespace {
+
+std::string read_file(const std::string& p) {
+    std::ifstream f(p, std::ios::binary);
+    std::stringstream ss;
+    ss << f.rdbuf();
+    return ss.str();
+}
+
+long now_ms() {
+    return std::chrono::duration_cast<std::chrono::milliseconds>(
+               std::chrono::system_clock::now().time_since_epoch())
+        .count();
+}
+
+struct Part {
+    int mp;
+    std::string blob;
+    TorchArchive ar;
+    size_t n = 0;
+};
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    std::string blobs, parts_s = "1,2,3", mode = "fedavg";
+    int D = 2, C = 1, rounds = 1, port_base = 8079, model_name = 2, model_type = 0, start = 6, end = 1;
+    uint64_t seed = 0x5EED;
+    float divisor = 1000.0f;
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i];
+        const char* v = i + 1 < argc ? argv[i + 1] : "";
+        if (a == "--blobs") blobs = v, ++i;
+        else if (a == "--parts") parts_s = v, ++i;
+        else if (a == "-d") D = std::atoi(v), ++i;
+        else if (a == "-c") C = std::atoi(v), ++i;
+        else if (a == "--rounds") rounds = std::atoi(v), ++i;
+        else if (a == "--mode") mode = v, ++i;
+        else if (a == "--port-base") port_base = std::atoi(v), ++i;
+        else if (a == "--model-name") model_name = std::atoi(v), ++i;
+        else if (a == "--model-type") model_type = std::atoi(v), ++i;
+        else if (a == "--start") start = std::atoi(v), ++i;
+        else if (a == "--end") end = std::atoi(v), ++i;
+        else if (a == "--seed") seed = std::strtoull(v, nullptr, 0), ++i;
+        else if (a == "--divisor") divisor = (float)std::atof(v), ++i;
+        else {
+            std::cerr << "unknown argument " << a << "\n";
+            return 2;
+        }
+    }
+    // template archives
+    std::vector<Part> parts;
+    {
+        std::stringstream ss(parts_s);
+        std::string t;
+        while (std::getline(ss, t, ',')) {
+            Part p;
+            p.mp = std::atoi(t.c_str());
+            p.blob = read_file(blobs + "/mp" + t + "_client0.pt");
+            parts.push_back(std::move(p));
+        }
+    }
+    for (auto& p : parts) {
+        std::string err;
+        if (!p.ar.parse((const uint8_t*)p.blob.data(), p.blob.size(), &err)) {
+            std::cerr << "template mp" << p.mp << ": " << err << "\n";
+            return 1;
+        }
+        p.n = (size_t)p.ar.param_numel();
+    }
+    // data owner ids: the init node 0 and the ids the aggregator replies to (aggregator.cpp:103-105)
+    std::vector<int> ids = {0};
+    for (int i = 0; i < D - 1; ++i) ids.push_back(i + C + 1);
+    RoutingTable routes(port_base);
+    std::map<int, std::unique_ptr<NetLayer>> listeners;  // port -> listener
+    for (int id : ids) {
+        const int port = routes.port_for(id);
+        if (listeners.count(port)) continue;
+        auto nl = std::make_unique<NetLayer>(id, routes);
+        if (!nl->start(port)) {
+            std::cerr << "cannot listen on " << port << "\n";
+            return 1;
+        }
+        listeners[port] = std::move(nl);
+    }
+    NetLayer& tx = *listeners.begin()->second;
+
+    // refactor message from the init node (data_owner.cpp:96-112)
+    Message rf;
+    rf.type = REFACTOR_DATA_OWNER;
+    rf.model_name = model_name;
+    rf.model_type = model_type;
+    rf.start = start;
+    rf.end = end;
+    rf.num_classes = 10;
+    rf.dataset = 0;
+    rf.data_owners = ids;
+    rf.read_table = 0;
+    tx.send(-1, std::make_shared<const std::string>(frame(rf)));
+
+    std::vector<float> w(D, 1.0f / (float)D);  // the aggregator's default weights
+    bool ok = true;
+    size_t checked = 0;
+    std::vector<long> round_ms;
+    auto collect = [&](int want, std::vector<Receipt>* got) {
+        const long t_end = now_ms() + 600000;
+        while ((int)got->size() < want && now_ms() < t_end) {
+            for (auto& kv : listeners) {
+                Receipt r;
+                while (kv.second->try_next_receipt(&r, 5)) got->push_back(r);
+            }
+        }
+        return (int)got->size() == want;
+    };
+    for (int round = 0; round < rounds; ++round) {
+        const long t0 = now_ms();
+        std::map<int, std::vector<std::vector<float>>> values;  // mp -> per client
+        std::map<int, std::vector<std::string>> archives;
+        for (auto& p : parts) {
+            for (int k = 0; k < D; ++k) {
+                std::vector<float> x(p.n);
+                fa_oracle_fill_f32(seed ^ ((uint64_t)round << 48) ^ ((uint64_t)p.mp << 32), (uint32_t)k, 0, p.n, x.data());
+                std::string blob, err;
+                if (!p.ar.with_params(x.data(), &blob, &err)) {
+                    std::cerr << err << "\n";
+                    return 1;
+                }
+                values[p.mp].push_back(std::move(x));
+                archives[p.mp].push_back(std::move(blob));
+            }
+        }
+        for (int phase = 1; phase <= 2; ++phase) {
+            int sent = 0;
+            for (int k = 0; k < D; ++k)
+                for (auto& p : parts) {
+                    if ((phase == 1) != (p.mp == 1)) continue;
+                    Message m;  // Task(myID, aggregation_, -1), data_owner.cpp:225-231
+                    m.type = OPERATION;
+                    m.client_id = ids[k];
+                    m.prev_node = -1;
+                    m.type_op = AGGREGATION;
+                    m.model_part = p.mp;
+                    m.t_start = now_ms();
+                    m.values = archives[p.mp][k];
+                    tx.send(-1, std::make_shared<const std::string>(frame(m)));
+                    ++sent;
+                }
+            std::vector<Receipt> replies;
+            if (!collect(sent, &replies)) {
+                std::cerr << "timed out waiting for phase " << phase << " replies\n";
+                ok = false;
+                break;
+            }
+            for (auto& r : replies) {
+                const Part* p = nullptr;
+                for (auto& q : parts)
+                    if (q.mp == r.model_part) p = &q;
+                TorchArchive ar;
+                std::string err;
+                if (!p || !ar.parse(r.blob(), r.blob_len, &err) || (size_t)ar.param_numel() != p->n) {
+                    std::cerr << "bad reply for part " << r.model_part << ": " << err << "\n";
+                    ok = false;
+                    continue;
+                }
+                std::vector<float> got(p->n), want(p->n);
+                ar.gather_params(got.data(), &err);
+                const auto& xs = values[p->mp];
+                if (mode == "literal") {
+                    fa_oracle_literal_f32(xs[D - 1].data(), p->n, divisor, want.data());
+                } else {
+                    std::vector<const float*> ptrs;
+                    for (auto& x : xs) ptrs.push_back(x.data());
+                    fa_oracle_fedavg_f32(ptrs.data(), w.data(), D, p->n, nullptr, want.data(), 1);
+                }
+                if (std::memcmp(got.data(), want.data(), p->n * 4) != 0) {
+                    size_t bad = 0;
+                    while (bad < p->n && std::memcmp(&got[bad], &want[bad], 4) == 0) ++bad;
+                    std::cerr << "part " << p->mp << " mismatch at " << bad << ": " << got[bad] << " vs " << want[bad]
+                              << "\n";
+                    ok = false;
+                }
+                checked += p->n;
+                // buffers are the last receipt's (template buffers are identical for every client here)
+                if (ar.buffers().size() != p->ar.buffers().size()) ok = false;
+            }
+        }
+        round_ms.push_back(now_ms() - t0);
+    }
+    printf("{\"ok\": %s, \"rounds\": %d, \"data_owners\": %d, \"checked_elems\": %zu, \"round_ms\": [", ok ? "true" : "false",
+           rounds, D, checked);
+    for (size_t i = 0; i < round_ms.size(); ++i) printf("%s%ld", i ? ", " : "", round_ms[i]);
+    printf("]}\n");
+    for (auto& kv : listeners) kv.second->stop();
+    return ok ? 0 : 1;
+}

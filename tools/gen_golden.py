@@ -38,8 +38,8 @@ WSEED = 7
 # (resnet.h:7-11); vgg19 = v19 = 6 (vgg_help.h:12-20).  start/end follow the
 # refactor message of data_owner.cpp:99-100: end = cut[0], start = cut[-1] + 1.
 CONFIGS = [
-    ("lenet5_c1", (2, 0, 6, 1, 10), 2, 2),        # C1: LeNet-5, 2 data owners
-    ("resnet18_c2", (1, 1, 9, 3, 10), 8, 0),      # C2: ResNet-18 split "3,8", 8 owners
+    ("lenet5_c1", (2, 0, 6, 1, 10), 2, -1),       # C1: LeNet-5, 2 data owners
+    ("resnet18_c2", (1, 1, 9, 3, 10), 8, -1),     # C2: ResNet-18 split "3,8", 8 owners
     ("resnet101_c3", (1, 4, 20, 10, 10), 4, 0),   # C3 layout (split "10,19"); D=4 pins the chain
     ("vgg19_c4", (0, 6, 20, 3, 10), 3, 0),        # C4 layout (split "3,19"); D=3 pins the chain
 ]
