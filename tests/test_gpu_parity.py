@@ -359,3 +359,18 @@ def test_slot_skew_does_not_change_bits(fa, O, torch_gpu, skew):
             assert_bits(agg.finalize(1), O.fedavg(xs, w))
     finally:
         fa.set_tuning(slot_skew=before["slot_skew"] or -1)
+
+
+def test_context_submit_gather_matches_flat(fa, O, torch_gpu):
+    """fa_submit_gather: a receipt split into ragged pieces (archive records) == the flat submit."""
+    n, D = 2_000_003, 3
+    w = O.weights(D)
+    xs = host_clients(O, 52, D, n, False)
+    cuts = [0, 1, 7, 1000, 65_536, 1_234_567, n]
+    with fa.Aggregator(1) as agg:
+        agg.define(1, n, fa.F32, fa.F32, D, fa.FEDAVG)
+        for k in range(D):
+            agg.submit_gather(1, k, [xs[k][a:b] for a, b in zip(cuts, cuts[1:])], w[k])
+        assert_bits(agg.finalize(1), O.fedavg(xs, w))
+        with pytest.raises(fa.FaError):
+            agg.submit_gather(1, 0, [xs[0][:10]], w[0])  # wrong total size
