@@ -167,9 +167,10 @@ def test_tuning_variants_same_bits(fa, O, torch_gpu, tuning):
             w = O.weights(D)
             xs = host_clients(O, 8, D, n, bf16)
             clients = [filled(fa, torch, n, bf16, 8, k) for k in range(D)]
-            ref = O.fedavg(xs, w, out_dtype="bf16" if bf16_out else "f32")
-            if bf16_out and not bf16:
+            if bf16_out and not bf16:  # f32 inputs, bf16 output: one rounding of the fp32 chain
                 ref = O.f32_to_bf16(O.fedavg(xs, w))
+            else:
+                ref = O.fedavg(xs, w, out_dtype="bf16" if bf16_out else "f32")
             assert_bits(run_fedavg(fa, torch, clients, w, n, bf16, bf16_out), ref)
     finally:
         restore = dict(before)
