@@ -206,6 +206,7 @@ def main():
     ap.add_argument("--chunks", type=int, default=16, help="chain layout: pipeline chunks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL over xGMI) or gloo (rehearsal only)")
     ap.add_argument("--tune", default="", help="block,max_blocks,unroll,load_policy,store_policy (fa_tuning)")
     args = ap.parse_args()
 
@@ -224,13 +225,17 @@ def main():
     import torch.distributed as dist
     fa = load_pkg()
     shard = load_shard()
-    torch.cuda.set_device(local_rank)
+    device = local_rank % max(1, torch.cuda.device_count())  # == local_rank on a node with one GPU per rank
+    torch.cuda.set_device(device)
     fa.lib()
     if args.tune:
         b, mb, u, lp, sp = [int(x) for x in args.tune.split(",")]
         fa.set_tuning(block=b, max_blocks=mb, unroll=u, load_policy=lp, store_policy=sp)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(args.dist_backend)
 
         def barrier():
             dist.barrier()
@@ -242,9 +247,9 @@ def main():
     # weak scaling: per-rank work is fixed -- range: a 256 MiB slice of every one of D buckets;
     # rs / chain: D whole 256 MiB buckets (global clients rank*D .. rank*D+D-1 of D*world).
     if args.layout == "range":
-        setup = Setup(fa, torch, D, n, in_dt, out_dt, rank * n, local_rank)
+        setup = Setup(fa, torch, D, n, in_dt, out_dt, rank * n, device)
     else:
-        setup = Setup(fa, torch, D, n, in_dt, out_dt, 0, local_rank, client0=rank * D)
+        setup = Setup(fa, torch, D, n, in_dt, out_dt, 0, device, client0=rank * D)
         setup.w = Setup._weights(D * world)[rank * D:(rank + 1) * D]
     torch.cuda.synchronize()
 
@@ -257,7 +262,7 @@ def main():
     else:
         reducer = shard.fa_reducer(fa, setup.in_dt, stream)
         cl = setup.clients()
-        dev = torch.device("cuda", local_rank)
+        dev = torch.device("cuda", device)
         npad = -(-n // (world * shard.UNIT)) * world * shard.UNIT
         assert npad == n, "workload size must be a multiple of world * 64"
 
@@ -328,7 +333,7 @@ def main():
             if name == args.workload:
                 continue
             sD, sn, si, so, sdesc = WORKLOADS[name]
-            s = Setup(fa, torch, sD, sn, si, so, 0, local_rank)
+            s = Setup(fa, torch, sD, sn, si, so, 0, device)
             torch.cuda.synchronize()
             w2, km = timed_loop(torch, s, max(10, args.steps), 3, stream, dist, barrier)
             ka = statistics.mean(km)

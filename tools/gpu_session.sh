@@ -50,6 +50,10 @@ for s in $STEPS; do
     outexp)
         timeout -k 10 600 python tools/exp_out.py 25 10 > "$OUT/exp_out.jsonl" 2> "$OUT/exp_out.err"
         rc=$?; cat "$OUT/exp_out.jsonl"; tail -2 "$OUT/exp_out.err"; ok_or_fail $rc outexp ;;
+    ranks)  # multi-rank rehearsal of the driver's N>1 launch: 2 ranks share the one GPU over gloo
+        timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+            --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2 --dist-backend gloo > "$OUT/bench_2ranks.json" 2> "$OUT/bench_2ranks.err"
+        rc=$?; cat "$OUT/bench_2ranks.json"; tail -3 "$OUT/bench_2ranks.err"; ok_or_fail $rc ranks ;;
     probe)
         hipcc --offload-arch=gfx950 -O3 tools/hbm_probe.hip -o "$OUT/hbm_probe" > "$OUT/probe_build.log" 2>&1 &&
         timeout -k 10 300 "$OUT/hbm_probe" > "$OUT/hbm_probe.json" 2> "$OUT/probe.err"
