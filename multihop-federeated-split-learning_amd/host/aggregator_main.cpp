@@ -169,14 +169,15 @@ public:
         b.last = r;  // template of the reply: the last receipt (its buffers travel back, as in the reference)
     }
 
-    // Reduces bucket mp and returns the framed reply (shared by every destination).
-    std::shared_ptr<const std::string> reduce(int mp) {
+    // Reduces bucket mp and returns the framed reply, built once and shared by every destination:
+    // the last receipt's archive with the reduced parameters written straight into the frame.
+    std::shared_ptr<const Bytes> reduce(int mp) {
         Bucket& b = buckets_[mp];
         std::vector<float> out(b.numel);
         FA_CHECK(fa_finalize(ctx_, mp, out.data()));
         TorchArchive ar;
-        std::string err, archive;
-        if (!ar.parse(b.last.blob(), b.last.blob_len, &err) || !ar.with_params(out.data(), &archive, &err)) {
+        std::string err;
+        if (!ar.parse(b.last.blob(), b.last.blob_len, &err)) {
             std::cerr << "[aggregator] reply for part " << mp << ": " << err << "\n";
             std::exit(1);
         }
@@ -187,13 +188,18 @@ public:
         m.type_op = AGGREGATION;
         m.model_part = mp;
         m.t_start = now_ms();
-        m.values = std::move(archive);
+        char* values = nullptr;
+        auto f = operation_frame(m, ar.size(), &values);
+        if (!ar.with_params_into(out.data(), (uint8_t*)values, &err)) {
+            std::cerr << "[aggregator] reply for part " << mp << ": " << err << "\n";
+            std::exit(1);
+        }
         b.bytes_in = 0;
-        return std::make_shared<const std::string>(frame(m));
+        return f;
     }
 
     // Fan-out to node 0 and the data owners i + c + 1, i < D - 1 (aggregator.cpp:102-106, :158-164).
-    void fan_out(const std::shared_ptr<const std::string>& f) {
+    void fan_out(const std::shared_ptr<const Bytes>& f) {
         net_->send(0, f);
         for (int i = 0; i < o_.data_owners - 1; ++i) net_->send(i + o_.compute_nodes + 1, f);
     }
@@ -303,7 +309,7 @@ int main(int argc, char** argv) {
         size_t in2 = 0;
         for (int mp = 2; mp <= L + 1; ++mp) in2 += agg.bytes_in(mp);
         auto t3 = std::chrono::steady_clock::now();
-        std::vector<std::shared_ptr<const std::string>> replies;
+        std::vector<std::shared_ptr<const Bytes>> replies;
         for (int mp = 2; mp <= L + 1; ++mp) replies.push_back(agg.reduce(mp));
         const double red2 = secs_since(t3);
         for (auto& f : replies) agg.fan_out(f);  // :153-166, in layer order

@@ -589,8 +589,12 @@ bool TorchArchive::gather_params(float* dst, std::string* err) const {
 }
 
 bool TorchArchive::with_params(const float* src, std::string* out, std::string* err) const {
-    out->assign((const char*)base_, size_);
-    uint8_t* o = (uint8_t*)&(*out)[0];
+    out->resize(size_);
+    return with_params_into(src, (uint8_t*)&(*out)[0], err);
+}
+
+bool TorchArchive::with_params_into(const float* src, uint8_t* o, std::string* err) const {
+    std::memcpy(o, base_, size_);
     std::vector<char> touched(entries_.size(), 0);
     for (auto& t : params_) {
         if (t.storage_type != "FloatStorage") return fail(err, "parameter " + t.name + " is not fp32");

@@ -63,6 +63,9 @@ public:
     // A copy of the archive bytes with every parameter replaced by src (fp32, named order) and
     // the CRC-32 of every rewritten record updated in its data descriptor and central directory.
     bool with_params(const float* src, std::string* out, std::string* err) const;
+    // Same, written into dst[0, size()) (e.g. straight into an outgoing frame).
+    bool with_params_into(const float* src, uint8_t* dst, std::string* err) const;
+    size_t size() const { return size_; }
 
 private:
     const uint8_t* base_ = nullptr;

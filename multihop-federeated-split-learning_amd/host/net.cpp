@@ -21,6 +21,12 @@ long now_ms() {
                std::chrono::system_clock::now().time_since_epoch())
         .count();
 }
+
+void big_buffers(int fd) {
+    int sz = 8 << 20;
+    setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &sz, sizeof sz);
+    setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &sz, sizeof sz);
+}
 }  // namespace
 
 // ------------------------------------------------------------------ routing
@@ -86,11 +92,12 @@ static bool recv_all(int fd, void* p, size_t n) {
     return true;
 }
 
-bool recv_frame(int fd, std::string* text) {
+std::shared_ptr<Bytes> recv_frame(int fd) {
     int32_t len = 0;
-    if (!recv_all(fd, &len, 4) || len < 0) return false;
-    text->resize((size_t)len);
-    return len == 0 || recv_all(fd, &(*text)[0], (size_t)len);
+    if (!recv_all(fd, &len, 4) || len <= 0) return nullptr;
+    auto b = std::make_shared<Bytes>((size_t)len);
+    if (!recv_all(fd, b->data(), (size_t)len)) return nullptr;
+    return b;
 }
 
 int connect_to(const std::string& host, int port, int tries, int wait_ms) {
@@ -101,6 +108,7 @@ int connect_to(const std::string& host, int port, int tries, int wait_ms) {
         if (getaddrinfo(host == "localhost" ? "127.0.0.1" : host.c_str(), std::to_string(port).c_str(), &hints,
                         &res) == 0) {
             int fd = socket(AF_INET, SOCK_STREAM, 0);
+            if (fd >= 0) big_buffers(fd);
             if (fd >= 0 && ::connect(fd, res->ai_addr, res->ai_addrlen) == 0) {
                 freeaddrinfo(res);
                 int one = 1;
@@ -125,6 +133,7 @@ bool NetLayer::start(int port) {
     if (listen_fd_ < 0) return false;
     int one = 1;
     setsockopt(listen_fd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+    big_buffers(listen_fd_);
     sockaddr_in a{};
     a.sin_family = AF_INET;
     a.sin_addr.s_addr = INADDR_ANY;
@@ -136,12 +145,18 @@ bool NetLayer::start(int port) {
     }
     running_ = true;
     rx_ = std::thread(&NetLayer::receiver_loop, this);
-    tx_ = std::thread(&NetLayer::sender_loop, this);
+    for (int i = 0; i < n_senders_; ++i) {
+        senders_.emplace_back(new Sender());
+    }
+    for (int i = 0; i < n_senders_; ++i) senders_[i]->th = std::thread(&NetLayer::sender_loop, this, i);
     return true;
 }
 
 void NetLayer::stop() {
     if (!running_.exchange(false)) return;
+    {
+        std::lock_guard<std::mutex> lk(m_tx_);
+    }
     cv_tx_.notify_all();
     if (listen_fd_ >= 0) {
         shutdown(listen_fd_, SHUT_RDWR);
@@ -149,18 +164,26 @@ void NetLayer::stop() {
         listen_fd_ = -1;
     }
     if (rx_.joinable()) rx_.join();
-    if (tx_.joinable()) tx_.join();
-    for (auto& kv : open_out_) close(kv.second);
-    open_out_.clear();
+    for (auto& s : senders_) {
+        if (s->th.joinable()) s->th.join();
+        for (auto& kv : s->open) close(kv.second);
+    }
+    senders_.clear();
 }
 
-void NetLayer::handle_frame(std::shared_ptr<std::string> text, int fd, bool* keep) {
-    (void)fd;
+void NetLayer::handle_frame(std::shared_ptr<Bytes> text, bool* keep) {
+    // Parse the header without touching the archive: the header is the text before "values : ".
+    const size_t scan = std::min<size_t>(text->size(), 4096);
+    const char* base = text->data();
+    const char* v = nullptr;
+    for (size_t i = 0; i + 9 <= scan; ++i)
+        if (std::memcmp(base + i, "values : ", 9) == 0 && (i == 0 || base[i - 1] == '\n')) {
+            v = base + i;
+            break;
+        }
+    std::string head = v ? std::string(base, v - base) + "values : ,\n}" : std::string(base, scan);
     Message m;
     std::string err;
-    // Parse the header without copying the archive: decode a view that stops before `values`.
-    const size_t vpos = text->find("values : ");
-    std::string head = vpos == std::string::npos ? *text : text->substr(0, vpos) + "values : ,\n}";
     if (!decode(head, &m, &err)) {
         std::cerr << "[net] dropping malformed frame: " << err << "\n";
         return;
@@ -173,8 +196,8 @@ void NetLayer::handle_frame(std::shared_ptr<std::string> text, int fd, bool* kee
         r.model_part = m.model_part;
         r.type_op = m.type_op;
         r.t_start = m.t_start;
-        if (vpos != std::string::npos) {
-            r.blob_off = vpos + 9;
+        if (v) {
+            r.blob_off = (size_t)(v - base) + 9;
             r.blob_len = text->size() >= r.blob_off + 3 ? text->size() - 3 - r.blob_off : 0;
         }
         if (link_mbps_ > 0) {  // network_layer.cpp:654-665, opt-in
@@ -216,26 +239,26 @@ void NetLayer::receiver_loop() {
         for (size_t i = 0; i < open.size();) {
             int fd = open[i];
             if (FD_ISSET(fd, &rs)) {
-                auto text = std::make_shared<std::string>();
+                auto text = recv_frame(fd);
                 bool keep = true;
-                if (!recv_frame(fd, text.get()) || text->empty()) {
+                if (!text) {
                     close(fd);
                     open.erase(open.begin() + (long)i);
                     continue;
                 }
                 bytes_rx_ += text->size() + 4;
-                handle_frame(text, fd, &keep);
+                handle_frame(text, &keep);
             }
             ++i;
         }
         if (listen_fd_ >= 0 && FD_ISSET(listen_fd_, &rs)) {
             int fd = accept(listen_fd_, nullptr, nullptr);
             if (fd < 0) continue;
-            auto text = std::make_shared<std::string>();
+            auto text = recv_frame(fd);
             bool keep = false;
-            if (recv_frame(fd, text.get()) && !text->empty()) {
+            if (text) {
                 bytes_rx_ += text->size() + 4;
-                handle_frame(text, fd, &keep);
+                handle_frame(text, &keep);
             }
             if (keep) open.push_back(fd);
             else close(fd);
@@ -244,20 +267,21 @@ void NetLayer::receiver_loop() {
     for (int fd : open) close(fd);
 }
 
-void NetLayer::sender_loop() {
+void NetLayer::sender_loop(int i) {
+    Sender& me = *senders_[i];
     while (true) {
         Out o;
         {
             std::unique_lock<std::mutex> lk(m_tx_);
-            cv_tx_.wait(lk, [&] { return !outq_.empty() || !running_; });
-            if (outq_.empty()) break;
-            o = outq_.front();
-            outq_.pop_front();
-            tx_busy_ = true;
+            cv_tx_.wait(lk, [&] { return !me.q.empty() || !running_; });
+            if (me.q.empty()) break;
+            o = me.q.front();
+            me.q.pop_front();
+            me.busy = true;
         }
         int fd = -1;
-        auto it = open_out_.find(o.dest);
-        if (it != open_out_.end()) fd = it->second;
+        auto it = me.open.find(o.dest);
+        if (it != me.open.end()) fd = it->second;
         if (fd < 0) fd = connect_to(routes_.host_for(o.dest), routes_.port_for(o.dest), 100, 200);
         if (fd < 0) {
             std::cerr << "[net] cannot reach node " << o.dest << " at " << routes_.host_for(o.dest) << ":"
@@ -265,32 +289,38 @@ void NetLayer::sender_loop() {
         } else if (!send_all(fd, o.bytes->data(), o.bytes->size())) {
             std::cerr << "[net] send to node " << o.dest << " failed\n";
             close(fd);
-            open_out_.erase(o.dest);
+            me.open.erase(o.dest);
         } else if (o.keep) {
-            open_out_[o.dest] = fd;
+            me.open[o.dest] = fd;
         } else {
             close(fd);
-            open_out_.erase(o.dest);
+            me.open.erase(o.dest);
         }
         {
             std::lock_guard<std::mutex> lk(m_tx_);
-            tx_busy_ = false;
+            me.busy = false;
         }
         cv_tx_idle_.notify_all();
     }
 }
 
-void NetLayer::send(int dest, std::shared_ptr<const std::string> framed, bool keep_open) {
+void NetLayer::send(int dest, std::shared_ptr<const Bytes> framed, bool keep_open) {
     {
         std::lock_guard<std::mutex> lk(m_tx_);
-        outq_.push_back({dest, std::move(framed), keep_open});
+        // one sender per destination keeps that destination's frames in order
+        const size_t k = (size_t)(dest + 1024) % senders_.size();
+        senders_[k]->q.push_back({dest, std::move(framed), keep_open});
     }
-    cv_tx_.notify_one();
+    cv_tx_.notify_all();
 }
 
 void NetLayer::flush() {
     std::unique_lock<std::mutex> lk(m_tx_);
-    cv_tx_idle_.wait(lk, [&] { return outq_.empty() && !tx_busy_; });
+    cv_tx_idle_.wait(lk, [&] {
+        for (auto& s : senders_)
+            if (!s->q.empty() || s->busy) return false;
+        return true;
+    });
 }
 
 Receipt NetLayer::next_receipt() {

@@ -2,14 +2,17 @@
 // (pipeline_simulation/network_layer.{h,cpp}), wire-compatible.
 //
 // Threading model kept from the reference (network_layer.h:49-63, .cpp:372-480):
-// one receiver thread (select/accept, frames -> FIFO task queue under a mutex +
-// condvar), one sender thread (queue of outgoing frames, connect with retries,
+// a receiver thread (select/accept, frames -> FIFO task queue under a mutex +
+// condvar), sender threads (queue of outgoing frames, connect with retries,
 // close unless save_connection), and the main thread as the single consumer.
 // Differences, all deliberate:
-//  * a receipt keeps the frame bytes it arrived in and points at the archive
-//    inside them (the reference makes ~10 full copies);
+//  * a receipt keeps the frame bytes it arrived in (read once, not zero-filled)
+//    and points at the archive inside them -- the reference makes ~10 full
+//    copies of every blob;
 //  * an outgoing frame is built once and shared by every destination (the
-//    reference re-serializes per destination, network_layer.cpp:305-313);
+//    reference re-serializes per destination, network_layer.cpp:305-313), and
+//    destinations are served by several sender threads (the reference has one,
+//    :742-829); frames to one destination keep their order;
 //  * the 8 Mbit/s link emulation (network_layer.cpp:654-665) is opt-in.
 #pragma once
 
@@ -45,14 +48,15 @@ private:
 struct Receipt {  // Task.h:30-51, the fields the aggregation path uses
     int client_id = -1, prev_node = -1, model_part = 1, type_op = -1;
     long t_start = 0;
-    std::shared_ptr<const std::string> frame;  // owns the bytes
-    size_t blob_off = 0, blob_len = 0;         // the torch::save archive inside `frame`
+    std::shared_ptr<const Bytes> frame;  // owns the bytes (the frame text, without the length prefix)
+    size_t blob_off = 0, blob_len = 0;   // the torch::save archive inside `frame`
     const uint8_t* blob() const { return (const uint8_t*)frame->data() + blob_off; }
 };
 
 class NetLayer {
 public:
-    NetLayer(int my_id, RoutingTable routes) : my_id_(my_id), routes_(std::move(routes)) {}
+    NetLayer(int my_id, RoutingTable routes, int senders = 4)
+        : my_id_(my_id), routes_(std::move(routes)), n_senders_(senders < 1 ? 1 : senders) {}
     ~NetLayer();
 
     // Receiver thread on routes.port_for(my_id) (or `port` when >= 0).  Returns false if bind fails.
@@ -71,44 +75,49 @@ public:
     Message next_refactor();     // blocking (check_new_refactor_task, :481-493)
     bool try_next_receipt(Receipt* r, int timeout_ms);
 
-    // Queue a length-prefixed frame for `dest` (shared across destinations).
-    void send(int dest, std::shared_ptr<const std::string> framed, bool keep_open = false);
-    void flush();                // wait until the send queue is empty
+    // Queue a length-prefixed frame for `dest`; the same frame may be queued for many destinations.
+    void send(int dest, std::shared_ptr<const Bytes> framed, bool keep_open = false);
+    void flush();                // wait until every queued frame has been sent
 
     RoutingTable& routes() { return routes_; }
     uint64_t bytes_received() const { return bytes_rx_; }
 
 private:
+    struct Out {
+        int dest;
+        std::shared_ptr<const Bytes> bytes;
+        bool keep;
+    };
+    struct Sender {
+        std::thread th;
+        std::deque<Out> q;
+        bool busy = false;
+        std::map<int, int> open;  // dest -> socket kept open (save_connection)
+    };
     void receiver_loop();
-    void sender_loop();
-    void handle_frame(std::shared_ptr<std::string> text, int fd, bool* keep);
+    void sender_loop(int i);
+    void handle_frame(std::shared_ptr<Bytes> text, bool* keep);
 
     int my_id_;
     RoutingTable routes_;
+    int n_senders_;
     int port_ = -1, listen_fd_ = -1;
     double link_mbps_ = 0;
     std::atomic<bool> running_{false};
     std::atomic<uint64_t> bytes_rx_{0};
-    std::thread rx_, tx_;
+    std::thread rx_;
     std::mutex m_rx_;
     std::condition_variable cv_rx_;
     std::deque<Receipt> receipts_;
     std::deque<Message> refactors_;
-    struct Out {
-        int dest;
-        std::shared_ptr<const std::string> bytes;
-        bool keep;
-    };
     std::mutex m_tx_;
     std::condition_variable cv_tx_, cv_tx_idle_;
-    std::deque<Out> outq_;
-    bool tx_busy_ = false;
-    std::map<int, int> open_out_;  // dest -> socket kept open (save_connection)
+    std::vector<std::unique_ptr<Sender>> senders_;
 };
 
 // Blocking helpers shared with the test tools.
 bool send_all(int fd, const void* p, size_t n);
-bool recv_frame(int fd, std::string* text);  // [int32 len][len bytes]; false on EOF / error
+std::shared_ptr<Bytes> recv_frame(int fd);  // [int32 len][len bytes] -> the len bytes; null on EOF / error
 int connect_to(const std::string& host, int port, int tries, int wait_ms);
 
 }  // namespace fahost

@@ -81,12 +81,50 @@ std::string encode(const Message& m) {
     return t + "}";
 }
 
-std::string frame(const Message& m) {
+std::string operation_header(const Message& m) {
+    std::string t = "{,\n";
+    field(t, "save_connection", std::to_string(m.save_connection));
+    field(t, "type", std::to_string(m.type));
+    field(t, "client_id", std::to_string(m.client_id));
+    field(t, "prev_node", std::to_string(m.prev_node));
+    field(t, "size_", std::to_string(m.size_));
+    field(t, "type_op", std::to_string(m.type_op));
+    field(t, "model_part", std::to_string(m.model_part));
+    field(t, "t_start", std::to_string(m.t_start));
+    field(t, "batch0", std::to_string(m.batch0));
+    return t + "values : ";
+}
+
+std::shared_ptr<Bytes> operation_frame(const Message& m, size_t values_len, char** values) {
+    const std::string head = operation_header(m);
+    const size_t text = head.size() + values_len + 3;
+    auto b = std::make_shared<Bytes>(4 + text);
+    const int32_t len = (int32_t)text;
+    std::memcpy(b->data(), &len, 4);  // native-endian int, as my_send does (network_layer.cpp:16)
+    std::memcpy(b->data() + 4, head.data(), head.size());
+    *values = b->data() + 4 + head.size();
+    std::memcpy(*values + values_len, ",\n}", 3);
+    return b;
+}
+
+std::shared_ptr<Bytes> frame_bytes(const Message& m) {
+    if (m.type == OPERATION) {
+        char* v = nullptr;
+        auto b = operation_frame(m, m.values.size(), &v);
+        std::memcpy(v, m.values.data(), m.values.size());
+        return b;
+    }
     const std::string text = encode(m);
-    std::string f(4, '\0');
+    auto b = std::make_shared<Bytes>(4 + text.size());
     const int32_t len = (int32_t)text.size();
-    std::memcpy(&f[0], &len, 4);  // native-endian int, as my_send does (network_layer.cpp:16)
-    return f + text;
+    std::memcpy(b->data(), &len, 4);
+    std::memcpy(b->data() + 4, text.data(), text.size());
+    return b;
+}
+
+std::string frame(const Message& m) {
+    auto b = frame_bytes(m);
+    return std::string(b->data(), b->size());
 }
 
 bool decode(const std::string& text, Message* m, std::string* err) {

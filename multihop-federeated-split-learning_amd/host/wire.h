@@ -12,6 +12,7 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <utility>
 #include <vector>
@@ -35,11 +36,27 @@ struct Message {  // Message.h:571-616 field for field
     std::string values;
 };
 
+// A heap byte buffer that is NOT zero-filled (frames are hundreds of MB).
+struct Bytes {
+    std::unique_ptr<char[]> p;
+    size_t n = 0;
+    explicit Bytes(size_t size) : p(new char[size]), n(size) {}
+    char* data() { return p.get(); }
+    const char* data() const { return p.get(); }
+    size_t size() const { return n; }
+};
+
 // Text of a frame (without the length prefix).
 std::string encode(const Message& m);
+// The text of an OPERATION frame up to and including "values : " (the archive follows, then ",\n}").
+std::string operation_header(const Message& m);
+// Allocates a length-prefixed OPERATION frame with `values_len` bytes reserved for the archive;
+// *values points at them (the caller writes the archive in place, e.g. TorchArchive::with_params_into).
+std::shared_ptr<Bytes> operation_frame(const Message& m, size_t values_len, char** values);
 // Parses the text of a frame; false (with *err) when a field is missing or malformed.
 bool decode(const std::string& text, Message* m, std::string* err);
-// Length-prefixed frame as it goes on the socket.
+// Length-prefixed frame as it goes on the socket (one copy of m.values).
 std::string frame(const Message& m);
+std::shared_ptr<Bytes> frame_bytes(const Message& m);
 
 }  // namespace fahost

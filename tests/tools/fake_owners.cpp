@@ -126,7 +126,7 @@ int main(int argc, char** argv) {
     rf.dataset = 0;
     rf.data_owners = ids;
     rf.read_table = 0;
-    tx.send(-1, std::make_shared<const std::string>(frame(rf)));
+    tx.send(-1, frame_bytes(rf));
 
     std::vector<float> w(D, 1.0f / (float)D);  // the aggregator's default weights
     bool ok = true;
@@ -172,7 +172,7 @@ int main(int argc, char** argv) {
                     m.model_part = p.mp;
                     m.t_start = now_ms();
                     m.values = archives[p.mp][k];
-                    tx.send(-1, std::make_shared<const std::string>(frame(m)));
+                    tx.send(-1, frame_bytes(m));
                     ++sent;
                 }
             std::vector<Receipt> replies;

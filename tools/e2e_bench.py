@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""End-to-end rounds of the drop-in aggregator process (GPU box tool).
+
+Builds model-part archives shaped like BASELINE.json C4 (VGG-19 split "3,19":
+part 1 = 38 720, last part = 2 359 808 + 119 586 826 fp32 parameters) with
+torch.jit.save (the same zip/pickle format as the reference's C++ torch::save),
+starts fa_aggregator and the fake data owners (tests/tools) on loopback TCP and
+reports the data owners' round time and the aggregator's per-phase split.
+Beside it, oracle/_ref/ref_harness times the reference-literal receive loop
+(torch::load + (p+p)/1000 + copy_, aggregator.cpp:63-88) on the VGG FC part.
+
+  python tools/e2e_bench.py [D] [rounds]
+"""
+import json
+import os
+import random
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+AGG = os.path.join(ROOT, "multihop-federeated-split-learning_amd", "bin", "fa_aggregator")
+OWNERS = os.path.join(ROOT, "tests", "tools", "bin", "fa_fake_owners")
+REF = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+
+
+def vgg_c4_parts(d):
+    import torch
+    import torch.nn as nn
+    torch.manual_seed(0)
+    parts = {
+        1: nn.Sequential(nn.Conv2d(3, 64, 3, padding=1), nn.ReLU(), nn.Conv2d(64, 64, 3, padding=1), nn.ReLU()),
+        2: nn.Sequential(nn.Conv2d(512, 512, 3, padding=1), nn.ReLU(), nn.MaxPool2d(2)),
+        3: nn.Sequential(nn.Linear(512 * 7 * 7, 4096), nn.ReLU(), nn.Dropout(), nn.Linear(4096, 4096), nn.ReLU(),
+                         nn.Dropout(), nn.Linear(4096, 10)),
+    }
+    sizes = {}
+    for mp, m in parts.items():
+        torch.jit.save(torch.jit.script(m), os.path.join(d, "mp%d_client0.pt" % mp))
+        sizes[mp] = sum(p.numel() for p in m.parameters())
+    return sizes
+
+
+def main():
+    D = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+    out = {"workload": "VGG-19 C4 model parts (split 3,19), %d data owners, loopback TCP" % D}
+    with tempfile.TemporaryDirectory() as d:
+        sizes = vgg_c4_parts(d)
+        out["params_per_part"] = sizes
+        base = random.randrange(20000, 60000, 100)
+        agg = subprocess.Popen([AGG, "-i", "-1", "-d", str(D), "-c", "1", "--rounds", str(rounds), "--port-base",
+                                str(base)], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        time.sleep(0.5)
+        t0 = time.perf_counter()
+        r = subprocess.run([OWNERS, "--blobs", d, "--parts", "1,2,3", "-d", str(D), "-c", "1", "--rounds",
+                            str(rounds), "--port-base", str(base), "--model-name", "0", "--start", "20", "--end", "3"],
+                           capture_output=True, text=True, timeout=900)
+        wall = time.perf_counter() - t0
+        a_out, a_err = agg.communicate(timeout=120)
+        if r.returncode != 0 or agg.returncode != 0:
+            print(json.dumps({"error": (r.stderr + a_err)[-3000:]}))
+            sys.exit(1)
+        owners = json.loads(r.stdout.strip().splitlines()[-1])
+        phases = [json.loads(l) for l in a_out.splitlines() if l.startswith("{")]
+        in_bytes = sum(p["phase1"]["bytes_in"] + p["phase2"]["bytes_in"] for p in phases) / len(phases)
+        out.update({"ok": owners["ok"], "round_ms_owner_view": owners["round_ms"], "aggregator_phases": phases,
+                    "bytes_in_per_round": in_bytes, "wall_s": round(wall, 3),
+                    "ingest_GBs_per_round": [round(in_bytes / (ms / 1e3) / 1e9, 2) for ms in owners["round_ms"]]})
+    if os.access(REF, os.X_OK):
+        threads = str(min(16, len(os.sched_getaffinity(0))))
+        lit = subprocess.run([REF, "bench-literal", "0", "6", "20", "3", "10", str(D), threads, "3"],
+                             capture_output=True, text=True, timeout=900)
+        if lit.returncode == 0:
+            out["reference_literal_receive_loop"] = json.loads(lit.stdout.strip().splitlines()[-1])
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
