@@ -132,6 +132,7 @@ public:
 
     // Consumes one receipt of bucket `mp` into its client slot.
     void absorb(const Receipt& r) {
+        const auto t0 = std::chrono::steady_clock::now();
         TorchArchive ar;
         std::string err;
         if (!ar.parse(r.blob(), r.blob_len, &err)) {
@@ -167,14 +168,18 @@ public:
         }
         b.bytes_in += r.blob_len;
         b.last = r;  // template of the reply: the last receipt (its buffers travel back, as in the reference)
+        st_.absorb_s += secs_since(t0);
     }
 
     // Reduces bucket mp and returns the framed reply, built once and shared by every destination:
     // the last receipt's archive with the reduced parameters written straight into the frame.
     std::shared_ptr<const Bytes> reduce(int mp) {
         Bucket& b = buckets_[mp];
+        const auto t0 = std::chrono::steady_clock::now();
         std::vector<float> out(b.numel);
         FA_CHECK(fa_finalize(ctx_, mp, out.data()));
+        const auto t1 = std::chrono::steady_clock::now();
+        st_.finalize_s += std::chrono::duration<double>(t1 - t0).count();
         TorchArchive ar;
         std::string err;
         if (!ar.parse(b.last.blob(), b.last.blob_len, &err)) {
@@ -195,6 +200,7 @@ public:
             std::exit(1);
         }
         b.bytes_in = 0;
+        st_.frame_s += secs_since(t1);
         return f;
     }
 
@@ -205,6 +211,17 @@ public:
     }
 
     size_t bytes_in(int mp) { return buckets_[mp].bytes_in; }
+
+    // Host-side time split since the last call: archive parse + slot staging (absorb), the GPU
+    // reduction incl. its D2H copy (finalize), the reply archive + frame (frame).
+    struct Stats {
+        double absorb_s = 0, finalize_s = 0, frame_s = 0;
+    };
+    Stats take_stats() {
+        Stats s = st_;
+        st_ = Stats{};
+        return s;
+    }
 
 private:
     struct Bucket {
@@ -238,6 +255,7 @@ private:
     fa_ctx* ctx_ = nullptr;
     std::map<int, Bucket> buckets_;
     std::map<int, int> slots_;
+    Stats st_;
 };
 
 }  // namespace
@@ -286,6 +304,7 @@ int main(int argc, char** argv) {
         auto t1 = std::chrono::steady_clock::now();
         auto reply1 = agg.reduce(1);
         const double red1 = secs_since(t1);
+        const auto s1 = agg.take_stats();
         agg.fan_out(reply1);
 
         // phase 2: every last-part layer from every data owner (:108-150)
@@ -312,11 +331,17 @@ int main(int argc, char** argv) {
         std::vector<std::shared_ptr<const Bytes>> replies;
         for (int mp = 2; mp <= L + 1; ++mp) replies.push_back(agg.reduce(mp));
         const double red2 = secs_since(t3);
+        const auto s2 = agg.take_stats();
+        auto t4 = std::chrono::steady_clock::now();
         for (auto& f : replies) agg.fan_out(f);  // :153-166, in layer order
         net.flush();
-        printf("{\"round\":%d,\"phase1\":{\"receive_s\":%.6f,\"reduce_s\":%.6f,\"bytes_in\":%zu},"
-               "\"phase2\":{\"receive_s\":%.6f,\"reduce_s\":%.6f,\"bytes_in\":%zu,\"layers\":%d}}\n",
-               round, recv1, red1, in1, recv2, red2, in2, L);
+        const double send2 = secs_since(t4);
+        printf("{\"round\":%d,\"phase1\":{\"receive_s\":%.6f,\"reduce_s\":%.6f,\"bytes_in\":%zu,"
+               "\"absorb_s\":%.6f,\"finalize_s\":%.6f,\"frame_s\":%.6f},"
+               "\"phase2\":{\"receive_s\":%.6f,\"reduce_s\":%.6f,\"bytes_in\":%zu,\"layers\":%d,"
+               "\"absorb_s\":%.6f,\"finalize_s\":%.6f,\"frame_s\":%.6f,\"send_s\":%.6f}}\n",
+               round, recv1, red1, in1, s1.absorb_s, s1.finalize_s, s1.frame_s, recv2, red2, in2, L, s2.absorb_s,
+               s2.finalize_s, s2.frame_s, send2);
         fflush(stdout);
     }
     net.stop();

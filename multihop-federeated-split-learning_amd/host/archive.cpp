@@ -7,6 +7,7 @@
 #include <functional>
 #include <map>
 #include <memory>
+#include <thread>
 #include <unordered_map>
 
 #include <zlib.h>
@@ -593,14 +594,53 @@ bool TorchArchive::with_params(const float* src, std::string* out, std::string* 
     return with_params_into(src, (uint8_t*)&(*out)[0], err);
 }
 
+namespace {
+// Runs fn(lo, hi) over [0, n) split across up to 16 threads (inline below `grain` per part).
+void parallel_ranges(size_t n, size_t grain, const std::function<void(size_t, size_t)>& fn) {
+    static const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const size_t parts = std::min<size_t>(hw, std::max<size_t>(1, n / grain));
+    if (parts <= 1) {
+        fn(0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const size_t per = (n + parts - 1) / parts;
+    for (size_t p = 1; p < parts; ++p) {
+        const size_t lo = std::min(n, p * per), hi = std::min(n, lo + per);
+        th.emplace_back([&fn, lo, hi] { fn(lo, hi); });
+    }
+    fn(0, std::min(n, per));
+    for (auto& t : th) t.join();
+}
+
+// CRC-32 of a large buffer: per-chunk CRCs in parallel, joined with zlib's crc32_combine.
+uint32_t crc32_parallel(const uint8_t* p, size_t n) {
+    const size_t grain = 8u << 20;
+    if (n < 2 * grain) return crc32(p, n);
+    const size_t chunks = (n + grain - 1) / grain;
+    std::vector<uint32_t> part(chunks);
+    parallel_ranges(chunks, 1, [&](size_t lo, size_t hi) {
+        for (size_t c = lo; c < hi; ++c) {
+            const size_t a = c * grain, len = std::min(grain, n - a);
+            part[c] = crc32(p + a, len);
+        }
+    });
+    uint32_t c = part[0];
+    for (size_t k = 1; k < chunks; ++k) c = (uint32_t)crc32_combine(c, part[k], (z_off_t)std::min(grain, n - k * grain));
+    return c;
+}
+}  // namespace
+
 bool TorchArchive::with_params_into(const float* src, uint8_t* o, std::string* err) const {
-    std::memcpy(o, base_, size_);
+    parallel_ranges(size_, 16u << 20, [&](size_t lo, size_t hi) { std::memcpy(o + lo, base_ + lo, hi - lo); });
     std::vector<char> touched(entries_.size(), 0);
     for (auto& t : params_) {
         if (t.storage_type != "FloatStorage") return fail(err, "parameter " + t.name + " is not fp32");
         uint8_t* d = o + (t.data - base_);
         if (t.contiguous) {
-            std::memcpy(d, src, (size_t)t.numel * 4);
+            const uint8_t* s0 = (const uint8_t*)src;
+            parallel_ranges((size_t)t.numel * 4, 16u << 20,
+                            [&](size_t lo, size_t hi) { std::memcpy(d + lo, s0 + lo, hi - lo); });
         } else {
             std::vector<int64_t> idx(t.sizes.size(), 0);
             for (int64_t e = 0; e < t.numel; ++e) {
@@ -619,7 +659,7 @@ bool TorchArchive::with_params_into(const float* src, uint8_t* o, std::string* e
     for (size_t k = 0; k < entries_.size(); ++k) {
         if (!touched[k]) continue;
         const ZipEntry& z = entries_[k];
-        const uint32_t c = crc32(o + z.data_offset, z.size);
+        const uint32_t c = crc32_parallel(o + z.data_offset, z.size);
         wr32(o + z.cd_offset + 16, c);
         if (z.desc_offset) wr32(o + z.desc_offset, c);   // flag bit 3: CRC lives in the data descriptor
         else wr32(o + z.local_offset + 14, c);           // otherwise in the local header
