@@ -9,6 +9,7 @@
 //   fa_fake_owners --blobs DIR --parts 1,2,3 -d D -c C [--rounds R] [--mode fedavg|literal]
 //                  [--port-base P] [--model-name N --model-type T --start S --end E] [--seed X]
 // Prints one JSON line: {"ok": bool, "rounds": R, "checked_elems": ..., "round_ms": [...]}.
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -20,6 +21,7 @@
 #include <set>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "archive.h"
@@ -142,79 +144,94 @@ int main(int argc, char** argv) {
         }
         return (int)got->size() == want;
     };
+    const int threads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    auto fill = [&](uint64_t sd, uint32_t k, size_t n, float* x) {  // the oracle's generator, in chunks
+        std::vector<std::thread> th;
+        const size_t per = (n + threads - 1) / threads;
+        for (int t = 0; t < threads; ++t) {
+            const size_t lo = std::min(n, t * per), hi = std::min(n, lo + per);
+            if (lo < hi) th.emplace_back([=] { fa_oracle_fill_f32(sd, k, lo, hi - lo, x + lo); });
+        }
+        for (auto& t : th) t.join();
+    };
     for (int round = 0; round < rounds; ++round) {
-        const long t0 = now_ms();
+        // The data owners' side of a round (their training) is not timed: values and frames are made
+        // first, then the clock runs from the first phase-1 send to the last phase-2 reply.
         std::map<int, std::vector<std::vector<float>>> values;  // mp -> per client
-        std::map<int, std::vector<std::string>> archives;
+        std::map<int, std::vector<std::shared_ptr<const Bytes>>> frames;
         for (auto& p : parts) {
             for (int k = 0; k < D; ++k) {
                 std::vector<float> x(p.n);
-                fa_oracle_fill_f32(seed ^ ((uint64_t)round << 48) ^ ((uint64_t)p.mp << 32), (uint32_t)k, 0, p.n, x.data());
-                std::string blob, err;
-                if (!p.ar.with_params(x.data(), &blob, &err)) {
+                fill(seed ^ ((uint64_t)round << 48) ^ ((uint64_t)p.mp << 32), (uint32_t)k, p.n, x.data());
+                Message m;  // Task(myID, aggregation_, -1), data_owner.cpp:225-231
+                m.type = OPERATION;
+                m.client_id = ids[k];
+                m.prev_node = -1;
+                m.type_op = AGGREGATION;
+                m.model_part = p.mp;
+                m.t_start = now_ms();
+                char* vals = nullptr;
+                auto f = operation_frame(m, p.ar.size(), &vals);
+                std::string err;
+                if (!p.ar.with_params_into(x.data(), (uint8_t*)vals, &err)) {
                     std::cerr << err << "\n";
                     return 1;
                 }
                 values[p.mp].push_back(std::move(x));
-                archives[p.mp].push_back(std::move(blob));
+                frames[p.mp].push_back(std::move(f));
             }
         }
-        for (int phase = 1; phase <= 2; ++phase) {
+        const auto t0 = std::chrono::steady_clock::now();
+        std::vector<Receipt> replies;
+        for (int phase = 1; phase <= 2 && ok; ++phase) {
             int sent = 0;
             for (int k = 0; k < D; ++k)
                 for (auto& p : parts) {
                     if ((phase == 1) != (p.mp == 1)) continue;
-                    Message m;  // Task(myID, aggregation_, -1), data_owner.cpp:225-231
-                    m.type = OPERATION;
-                    m.client_id = ids[k];
-                    m.prev_node = -1;
-                    m.type_op = AGGREGATION;
-                    m.model_part = p.mp;
-                    m.t_start = now_ms();
-                    m.values = archives[p.mp][k];
-                    tx.send(-1, frame_bytes(m));
+                    tx.send(-1, frames[p.mp][k]);
                     ++sent;
                 }
-            std::vector<Receipt> replies;
-            if (!collect(sent, &replies)) {
+            std::vector<Receipt> got;
+            if (!collect(sent, &got)) {
                 std::cerr << "timed out waiting for phase " << phase << " replies\n";
                 ok = false;
-                break;
             }
-            for (auto& r : replies) {
-                const Part* p = nullptr;
-                for (auto& q : parts)
-                    if (q.mp == r.model_part) p = &q;
-                TorchArchive ar;
-                std::string err;
-                if (!p || !ar.parse(r.blob(), r.blob_len, &err) || (size_t)ar.param_numel() != p->n) {
-                    std::cerr << "bad reply for part " << r.model_part << ": " << err << "\n";
-                    ok = false;
-                    continue;
-                }
-                std::vector<float> got(p->n), want(p->n);
-                ar.gather_params(got.data(), &err);
-                const auto& xs = values[p->mp];
-                if (mode == "literal") {
-                    fa_oracle_literal_f32(xs[D - 1].data(), p->n, divisor, want.data());
-                } else {
-                    std::vector<const float*> ptrs;
-                    for (auto& x : xs) ptrs.push_back(x.data());
-                    fa_oracle_fedavg_f32(ptrs.data(), w.data(), D, p->n, nullptr, want.data(), 1);
-                }
-                if (std::memcmp(got.data(), want.data(), p->n * 4) != 0) {
-                    size_t bad = 0;
-                    while (bad < p->n && std::memcmp(&got[bad], &want[bad], 4) == 0) ++bad;
-                    std::cerr << "part " << p->mp << " mismatch at " << bad << ": " << got[bad] << " vs " << want[bad]
-                              << "\n";
-                    ok = false;
-                }
-                checked += p->n;
-                // buffers are the last receipt's (template buffers are identical for every client here)
-                if (ar.buffers().size() != p->ar.buffers().size()) ok = false;
-            }
+            for (auto& r : got) replies.push_back(std::move(r));
         }
-        round_ms.push_back(now_ms() - t0);
+        round_ms.push_back((long)std::llround(
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count()));
+        for (auto& r : replies) {
+            const Part* p = nullptr;
+            for (auto& q : parts)
+                if (q.mp == r.model_part) p = &q;
+            TorchArchive ar;
+            std::string err;
+            if (!p || !ar.parse(r.blob(), r.blob_len, &err) || (size_t)ar.param_numel() != p->n) {
+                std::cerr << "bad reply for part " << r.model_part << ": " << err << "\n";
+                ok = false;
+                continue;
+            }
+            std::vector<float> got(p->n), want(p->n);
+            ar.gather_params(got.data(), &err);
+            const auto& xs = values[p->mp];
+            if (mode == "literal") {
+                fa_oracle_literal_f32(xs[D - 1].data(), p->n, divisor, want.data());
+            } else {
+                std::vector<const float*> ptrs;
+                for (auto& x : xs) ptrs.push_back(x.data());
+                fa_oracle_fedavg_f32(ptrs.data(), w.data(), D, p->n, nullptr, want.data(), threads);
+            }
+            if (std::memcmp(got.data(), want.data(), p->n * 4) != 0) {
+                size_t bad = 0;
+                while (bad < p->n && std::memcmp(&got[bad], &want[bad], 4) == 0) ++bad;
+                std::cerr << "part " << p->mp << " mismatch at " << bad << ": " << got[bad] << " vs " << want[bad]
+                          << "\n";
+                ok = false;
+            }
+            checked += p->n;
+            // buffers are the last receipt's (template buffers are identical for every client here)
+            if (ar.buffers().size() != p->ar.buffers().size()) ok = false;
+        }
     }
     printf("{\"ok\": %s, \"rounds\": %d, \"data_owners\": %d, \"checked_elems\": %zu, \"round_ms\": [", ok ? "true" : "false",
            rounds, D, checked);
