@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 1
+#define FA_ABI_VERSION 2
 
 typedef struct fa_ctx fa_ctx; /* opaque: device slots, streams, pinned staging */
 
@@ -91,11 +91,29 @@ int fa_submit_pinned(fa_ctx* ctx, int part_id, int client_slot, const void* host
  * the pinned staging chunks, no intermediate flat copy. */
 int fa_submit_gather(fa_ctx* ctx, int part_id, int client_slot, int n_segments, const void* const* srcs,
                      const size_t* bytes, float weight);
+/* Zero-copy ingest: the segments lie in pinned memory (fa_host_alloc), e.g. the
+ * parameter records of an archive inside a frame the network layer received
+ * into a pinned buffer, and stay unchanged until fa_finalize* returns.  The
+ * H2D DMA runs from them directly, no staging copy. */
+int fa_submit_gather_pinned(fa_ctx* ctx, int part_id, int client_slot, int n_segments, const void* const* srcs,
+                            const size_t* bytes, float weight);
 
 /* Replaces the end of a phase: the reduced module handed to new_message()
  * (aggregator.cpp:96-106 / :153-166).  Waits for the submits, reduces on every
  * GPU, copies the result (out dtype) to host_dst and resets the round. */
 int fa_finalize(fa_ctx* ctx, int part_id, void* host_dst);
+/* Same, scattering the result over n_segments host pieces (e.g. the parameter
+ * records of the reply archive inside the outgoing frame, aggregator.cpp:96-101
+ * + network_layer.cpp:305-313).  flags: FA_HOST_PINNED = every segment is pinned
+ * memory, DMA'd into directly; 0 = pageable, copied through the pinned chunks. */
+#define FA_HOST_PINNED 0x1
+int fa_finalize_gather(fa_ctx* ctx, int part_id, int n_segments, void* const* dsts, const size_t* bytes,
+                       int flags);
+
+/* Pinned (page-locked, every device can DMA it) host memory, for frame buffers
+ * that feed fa_submit_gather_pinned / fa_finalize_gather(FA_HOST_PINNED). */
+int fa_host_alloc(size_t bytes, void** out);
+int fa_host_free(void* p);
 
 /* Device-resident round (the data path with buckets already in HBM, e.g. a
  * zero-copy ingest that lands receipts straight in the slots): reduce the

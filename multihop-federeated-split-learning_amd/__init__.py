@@ -70,7 +70,11 @@ def lib():
         "fa_submit": (I, [P, I, I, P, F]),
         "fa_submit_pinned": (I, [P, I, I, P, F]),
         "fa_submit_gather": (I, [P, I, I, I, P, P, F]),
+        "fa_submit_gather_pinned": (I, [P, I, I, I, P, P, F]),
         "fa_finalize": (I, [P, I, P]),
+        "fa_finalize_gather": (I, [P, I, I, P, P, I]),
+        "fa_host_alloc": (I, [S, ctypes.POINTER(P)]),
+        "fa_host_free": (I, [P]),
         "fa_reduce_device": (I, [P, I, P, P, I, S, I, P, I, I, P, P]),
         "fa_fill_uniform": (I, [P, S, I, U64, U32, U64, P]),
         "fa_set_tuning": (I, [ctypes.POINTER(_Tuning)]),
@@ -154,6 +158,42 @@ def set_tuning(block=0, max_blocks=0, unroll=0, load_policy=0, store_policy=0, s
     check(lib().fa_set_tuning(ctypes.byref(t)))
 
 
+HOST_PINNED = 0x1
+
+
+class PinnedBuffer:
+    """fa_host_alloc'd page-locked host memory, viewed as a numpy array (freed on close / GC)."""
+
+    def __init__(self, nbytes):
+        p = ctypes.c_void_p()
+        check(lib().fa_host_alloc(nbytes, ctypes.byref(p)))
+        self.ptr, self.nbytes = p.value, nbytes
+
+    def view(self, dtype=np.uint8, count=-1, offset=0):
+        if not self.ptr:
+            return np.empty(0, dtype)
+        raw = (ctypes.c_char * self.nbytes).from_address(self.ptr)
+        return np.frombuffer(raw, dtype=dtype, count=count, offset=offset)
+
+    def close(self):
+        if self.ptr:
+            check(lib().fa_host_free(self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _segments(pieces):
+    pieces = [np.ascontiguousarray(x) for x in pieces]
+    ptrs = (ctypes.c_void_p * len(pieces))(*[x.ctypes.data for x in pieces])
+    sizes = (ctypes.c_size_t * len(pieces))(*[x.nbytes for x in pieces])
+    return pieces, ptrs, sizes
+
+
 class Aggregator:
     """fa_ctx: the aggregator's global parts on 1..G GPUs (range-sharded when G > 1).
 
@@ -191,12 +231,20 @@ class Aggregator:
         fn = lib().fa_submit_pinned if pinned else lib().fa_submit
         check(fn(self.handle, part_id, slot, host.ctypes.data, float(weight)))
 
-    def submit_gather(self, part_id, slot, pieces, weight=1.0):
-        """fa_submit_gather: `pieces` (host arrays) concatenate to the bucket."""
-        pieces = [np.ascontiguousarray(x) for x in pieces]
-        ptrs = (ctypes.c_void_p * len(pieces))(*[x.ctypes.data for x in pieces])
-        sizes = (ctypes.c_size_t * len(pieces))(*[x.nbytes for x in pieces])
-        check(lib().fa_submit_gather(self.handle, part_id, slot, len(pieces), ptrs, sizes, float(weight)))
+    def submit_gather(self, part_id, slot, pieces, weight=1.0, pinned=False):
+        """fa_submit_gather(_pinned): `pieces` (host arrays) concatenate to the bucket.  pinned: views of
+        PinnedBuffers the caller keeps unchanged until finalize returns."""
+        pieces, ptrs, sizes = _segments(pieces)
+        fn = lib().fa_submit_gather_pinned if pinned else lib().fa_submit_gather
+        check(fn(self.handle, part_id, slot, len(pieces), ptrs, sizes, float(weight)))
+
+    def finalize_gather(self, part_id, pieces, pinned=False):
+        """fa_finalize_gather: the reduced bucket scattered over `pieces` (writable host arrays)."""
+        for x in pieces:
+            if not (isinstance(x, np.ndarray) and x.flags.c_contiguous and x.flags.writeable):
+                raise ValueError("finalize_gather needs writable contiguous arrays")
+        _, ptrs, sizes = _segments(pieces)
+        check(lib().fa_finalize_gather(self.handle, part_id, len(pieces), ptrs, sizes, HOST_PINNED if pinned else 0))
 
     def finalize(self, part_id, out=None):
         if part_id not in self.parts:  # let the library report it (FA_ERR_ARG)

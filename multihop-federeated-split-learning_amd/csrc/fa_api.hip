@@ -314,26 +314,46 @@ int reduce_part(fa_ctx* ctx, Part& p, const float* w, hipStream_t s) {
     return FA_OK;
 }
 
-// A host source for one receipt: the concatenation of `n` segments (one segment for a flat buffer,
-// one per parameter record for an archive mapped in place).
+// A host buffer given as the concatenation of `n` segments (one segment for a flat buffer, one per
+// parameter record for an archive mapped in place): the source of a receipt or the destination of a
+// reduced bucket.
 struct Gather {
     int n;
-    const void* const* src;
+    const void* const* seg;
     const size_t* bytes;
-    // Copies bytes [a, a + len) of the concatenation to dst.
-    void copy(size_t a, size_t len, char* dst) const {
-        size_t seg_lo = 0;
+    // fn(piece, rel, take) for each piece of bytes [a, a + len) of the concatenation; rel = offset of
+    // the piece from a.
+    template <class F>
+    void pieces(size_t a, size_t len, F&& fn) const {
+        size_t seg_lo = 0, rel = 0;
         for (int k = 0; k < n && len > 0; ++k) {
             const size_t seg_hi = seg_lo + bytes[k];
             if (a < seg_hi) {
                 const size_t off = a - seg_lo, take = std::min(len, seg_hi - a);
-                std::memcpy(dst, static_cast<const char*>(src[k]) + off, take);
-                dst += take;
+                fn(const_cast<char*>(static_cast<const char*>(seg[k])) + off, rel, take);
                 a += take;
+                rel += take;
                 len -= take;
             }
             seg_lo = seg_hi;
         }
+    }
+    void copy_out(size_t a, size_t len, char* dst) const {  // concatenation[a, a+len) -> dst
+        pieces(a, len, [&](char* p, size_t rel, size_t take) { std::memcpy(dst + rel, p, take); });
+    }
+    void copy_in(size_t a, size_t len, const char* src) const {  // src -> concatenation[a, a+len)
+        pieces(a, len, [&](char* p, size_t rel, size_t take) { std::memcpy(p, src + rel, take); });
+    }
+    size_t total() const {
+        size_t t = 0;
+        for (int k = 0; k < n; ++k) t += bytes[k];
+        return t;
+    }
+    int check(const char* what) const {
+        if (n < 0 || (n > 0 && (!seg || !bytes))) return fail(FA_ERR_ARG, "bad %s segment list", what);
+        for (int k = 0; k < n; ++k)
+            if (!seg[k] && bytes[k]) return fail(FA_ERR_ARG, "%s segment %d is null", what, k);
+        return FA_OK;
     }
 };
 
@@ -342,12 +362,8 @@ int submit_impl(fa_ctx* ctx, int part_id, int slot, const Gather& src, float wei
     int rc = check_part(ctx, part_id, &p);
     if (rc) return rc;
     if (slot < 0 || slot >= p->D) return fail(FA_ERR_ARG, "client slot %d out of range [0,%d)", slot, p->D);
-    const size_t si = dsize(p->in);
-    size_t total = 0;
-    for (int k = 0; k < src.n; ++k) {
-        if (!src.src[k] && src.bytes[k]) return fail(FA_ERR_ARG, "host source segment %d is null", k);
-        total += src.bytes[k];
-    }
+    if ((rc = src.check("host source"))) return rc;
+    const size_t si = dsize(p->in), total = src.total();
     if (total != p->n * si)
         return fail(FA_ERR_ARG, "part %d expects %zu bytes per receipt, got %zu", part_id, p->n * si, total);
     for (int g = 0; g < ctx->G; ++g) {
@@ -356,9 +372,12 @@ int submit_impl(fa_ctx* ctx, int part_id, int slot, const Gather& src, float wei
         const size_t base = p->off[g] * si;
         char* ds = slot_ptr(*p, g, slot);
         const size_t bytes = p->cnt[g] * si;
-        if (pinned) {  // one flat pinned buffer: DMA straight from it
-            if (bytes) FA_HIP(hipMemcpyAsync(ds, static_cast<const char*>(src.src[0]) + base, bytes,
-                                             hipMemcpyHostToDevice, r.copy));
+        if (pinned) {  // pinned segments: DMA straight from them, one copy per piece of this GPU's range
+            hipError_t e = hipSuccess;
+            src.pieces(base, bytes, [&](char* piece, size_t rel, size_t take) {
+                if (e == hipSuccess) e = hipMemcpyAsync(ds + rel, piece, take, hipMemcpyHostToDevice, r.copy);
+            });
+            FA_HIP(e);
             continue;
         }
         // Double-buffered staging: fill one pinned chunk while the other is in flight.
@@ -367,7 +386,7 @@ int submit_impl(fa_ctx* ctx, int part_id, int slot, const Gather& src, float wei
             const int i = r.stage_i;
             r.stage_i ^= 1;
             FA_HIP(hipEventSynchronize(r.stage_ev[i]));
-            ctx->pool->copy(r.stage[i], b, [&](size_t lo, size_t len, char* d) { src.copy(base + o + lo, len, d); });
+            ctx->pool->copy(r.stage[i], b, [&](size_t lo, size_t len, char* d) { src.copy_out(base + o + lo, len, d); });
             FA_HIP(hipMemcpyAsync(ds + o, r.stage[i], b, hipMemcpyHostToDevice, r.copy));
             FA_HIP(hipEventRecord(r.stage_ev[i], r.copy));
         }
@@ -381,17 +400,29 @@ int submit_impl(fa_ctx* ctx, int part_id, int slot, const Gather& src, float wei
     return FA_OK;
 }
 
-// D2H of the part's device output through the pinned chunks (the result leaves for new_message()).
-// Waits for all work on the device first (the reduction may have run on a caller's stream).
-int copy_output(fa_ctx* ctx, Part& p, void* host_dst) {
+// D2H of the part's device output (the result leaves for new_message()) into `dst`: straight into
+// pinned segments, else through the pinned chunks, double-buffered.  Waits for all work on the
+// device first (the reduction may have run on a caller's stream).
+int copy_output(fa_ctx* ctx, Part& p, const Gather& dst, bool pinned) {
     const size_t so = dsize(p.out);
+    if (dst.total() != p.n * so)
+        return fail(FA_ERR_ARG, "output of %zu bytes expected, destination holds %zu", p.n * so, dst.total());
     for (int g = 0; g < ctx->G; ++g) {
         GpuRes& r = ctx->gpu[g];
         DeviceGuard dg(r.dev);
         FA_HIP(hipDeviceSynchronize());
         const char* src = static_cast<const char*>(p.dout[g]);
-        char* dst = static_cast<char*>(host_dst) + p.off[g] * so;
+        const size_t base = p.off[g] * so;
         const size_t bytes = p.cnt[g] * so;
+        if (pinned) {
+            hipError_t e = hipSuccess;
+            dst.pieces(base, bytes, [&](char* piece, size_t rel, size_t take) {
+                if (e == hipSuccess) e = hipMemcpyAsync(piece, src + rel, take, hipMemcpyDeviceToHost, r.compute);
+            });
+            FA_HIP(e);
+            FA_HIP(hipStreamSynchronize(r.compute));
+            continue;
+        }
         const size_t chunks = (bytes + kStageBytes - 1) / kStageBytes;
         // double-buffered: the D2H of chunk c+1 overlaps the host copy-out of chunk c
         auto issue = [&](size_t c) -> int {
@@ -411,11 +442,46 @@ int copy_output(fa_ctx* ctx, Part& p, void* host_dst) {
                 if (rc) return rc;
             }
             const size_t o = c * kStageBytes, b = std::min(kStageBytes, bytes - o);
-            const char* st = r.stage[c & 1];
-            ctx->pool->copy(dst + o, b, [&](size_t lo, size_t len, char* d) { std::memcpy(d, st + lo, len); });
+            char* st = r.stage[c & 1];
+            // the pool partitions [0, b); each worker scatters its share of the chunk
+            ctx->pool->copy(st, b, [&](size_t lo, size_t len, char*) { dst.copy_in(base + o + lo, len, st + lo); });
         }
         FA_HIP(hipStreamSynchronize(r.compute));
     }
+    return FA_OK;
+}
+
+int copy_output_flat(fa_ctx* ctx, Part& p, void* host_dst) {
+    const size_t bytes = p.n * dsize(p.out);
+    const void* segs[1] = {host_dst};
+    return copy_output(ctx, p, Gather{1, segs, &bytes}, false);
+}
+
+// The end of a phase: wait for the submits, reduce on every GPU, copy the result out, reset the round.
+int finalize_impl(fa_ctx* ctx, int part_id, const Gather& dst, bool pinned) {
+    Part* p;
+    int rc = check_part(ctx, part_id, &p);
+    if (rc) return rc;
+    if (p->mode == FA_FEDAVG && p->n_submitted != p->D)
+        return fail(FA_ERR_STATE, "part %d: %d of %d clients submitted", part_id, p->n_submitted, p->D);
+    if (p->n_submitted == 0) return fail(FA_ERR_STATE, "part %d: nothing submitted", part_id);
+    if ((rc = dst.check("host destination"))) return rc;
+    for (int g = 0; g < ctx->G; ++g) {  // the reduction waits for this round's H2D copies
+        GpuRes& r = ctx->gpu[g];
+        DeviceGuard dg(r.dev);
+        hipEvent_t ev;
+        FA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        FA_HIP(hipEventRecord(ev, r.copy));
+        FA_HIP(hipStreamWaitEvent(r.compute, ev, 0));
+        FA_HIP(hipEventDestroy(ev));
+    }
+    rc = reduce_part(ctx, *p, p->w.data(), nullptr);
+    if (rc) return rc;
+    rc = copy_output(ctx, *p, dst, pinned);
+    if (rc) return rc;
+    std::fill(p->submitted.begin(), p->submitted.end(), 0);
+    p->n_submitted = 0;
+    p->last_slot = -1;
     return FA_OK;
 }
 
@@ -630,8 +696,13 @@ int fa_submit_pinned(fa_ctx* ctx, int part_id, int client_slot, const void* host
 int fa_submit_gather(fa_ctx* ctx, int part_id, int client_slot, int n_segments, const void* const* srcs,
                      const size_t* bytes, float weight) {
     g_err.clear();
-    if (n_segments < 0 || (n_segments > 0 && (!srcs || !bytes))) return fail(FA_ERR_ARG, "bad segment list");
     return submit_impl(ctx, part_id, client_slot, Gather{n_segments, srcs, bytes}, weight, false);
+}
+
+int fa_submit_gather_pinned(fa_ctx* ctx, int part_id, int client_slot, int n_segments, const void* const* srcs,
+                            const size_t* bytes, float weight) {
+    g_err.clear();
+    return submit_impl(ctx, part_id, client_slot, Gather{n_segments, srcs, bytes}, weight, true);
 }
 
 int fa_finalize(fa_ctx* ctx, int part_id, void* host_dst) {
@@ -639,26 +710,35 @@ int fa_finalize(fa_ctx* ctx, int part_id, void* host_dst) {
     Part* p;
     int rc = check_part(ctx, part_id, &p);
     if (rc) return rc;
-    if (p->mode == FA_FEDAVG && p->n_submitted != p->D)
-        return fail(FA_ERR_STATE, "part %d: %d of %d clients submitted", part_id, p->n_submitted, p->D);
-    if (p->n_submitted == 0) return fail(FA_ERR_STATE, "part %d: nothing submitted", part_id);
     if (!host_dst && p->n) return fail(FA_ERR_ARG, "host_dst is null");
-    for (int g = 0; g < ctx->G; ++g) {  // the reduction waits for this round's H2D copies
-        GpuRes& r = ctx->gpu[g];
-        DeviceGuard dg(r.dev);
-        hipEvent_t ev;
-        FA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        FA_HIP(hipEventRecord(ev, r.copy));
-        FA_HIP(hipStreamWaitEvent(r.compute, ev, 0));
-        FA_HIP(hipEventDestroy(ev));
+    const size_t bytes = p->n * dsize(p->out);
+    const void* segs[1] = {host_dst};
+    return finalize_impl(ctx, part_id, Gather{1, segs, &bytes}, false);
+}
+
+int fa_finalize_gather(fa_ctx* ctx, int part_id, int n_segments, void* const* dsts, const size_t* bytes,
+                       int flags) {
+    g_err.clear();
+    if (flags & ~FA_HOST_PINNED) return fail(FA_ERR_ARG, "unknown flags 0x%x", flags);
+    return finalize_impl(ctx, part_id, Gather{n_segments, (const void* const*)dsts, bytes}, (flags & FA_HOST_PINNED) != 0);
+}
+
+int fa_host_alloc(size_t bytes, void** out) {
+    g_err.clear();
+    if (!out) return fail(FA_ERR_ARG, "out is null");
+    *out = nullptr;
+    if (bytes == 0) return FA_OK;
+    if (hipHostMalloc(out, bytes, hipHostMallocPortable) != hipSuccess) {
+        (void)hipGetLastError();
+        *out = nullptr;
+        return fail(FA_ERR_NOMEM, "pinned host alloc of %zu B failed", bytes);
     }
-    rc = reduce_part(ctx, *p, p->w.data(), nullptr);
-    if (rc) return rc;
-    rc = copy_output(ctx, *p, host_dst);
-    if (rc) return rc;
-    std::fill(p->submitted.begin(), p->submitted.end(), 0);
-    p->n_submitted = 0;
-    p->last_slot = -1;
+    return FA_OK;
+}
+
+int fa_host_free(void* p) {
+    g_err.clear();
+    if (p) FA_HIP(hipHostFree(p));
     return FA_OK;
 }
 
@@ -701,7 +781,7 @@ int fa_copy_output(fa_ctx* ctx, int part_id, void* host_dst) {
     int rc = check_part(ctx, part_id, &p);
     if (rc) return rc;
     if (!host_dst && p->n) return fail(FA_ERR_ARG, "host_dst is null");
-    return copy_output(ctx, *p, host_dst);
+    return copy_output_flat(ctx, *p, host_dst);
 }
 
 int fa_sync(fa_ctx* ctx) {

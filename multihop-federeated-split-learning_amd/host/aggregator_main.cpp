@@ -5,13 +5,19 @@
 //   refactor  <- the init node's REFACTOR_DATA_OWNER message (:52-53)
 //   phase 1   <- D receipts of model_part 1, reduced, reply to 0 and i+c+1 (:59-106)
 //   phase 2   <- D*L receipts of model_parts 2..L+1, reduced, reply per layer (:108-166)
-// What changes is only how a receipt is consumed: the archive is mapped in
-// place (host/archive.h) and its parameter records are gathered into pinned
-// staging and DMA'd to the client's device slot (fa_submit_gather); at the end
-// of a phase one ordered FMA chain per bucket runs on the MI355X (fa_finalize)
-// and the reply archive is the last receipt's with the reduced parameters
-// written in (buffers stay the last receipt's, as in the reference), built
-// once and sent to every data owner.
+// What changes is only how a receipt is consumed: frames are received into
+// pooled pinned buffers (one reader thread per connection), the archive is
+// mapped in place (host/archive.h) and its parameter records are DMA'd straight
+// from the frame to the client's device slot (fa_submit_gather_pinned); at the
+// end of a phase one ordered FMA chain per bucket runs on the MI355X and the
+// result is DMA'd straight into the parameter records of the reply frame
+// (fa_finalize_gather).  The reply archive is the last receipt's with the
+// reduced parameters (buffers stay the last receipt's, as in the reference),
+// built once and sent to every data owner.
+//
+// Client slots (the FMA chain order) are fixed, not arrival-ordered: the
+// refactor message's data-owner list when it has D entries, else the reply
+// convention of aggregator.cpp:102-106 (owner ids 0, C+1, ..., C+D-1).
 //
 // --mode literal reproduces the reference's arithmetic bit-for-bit
 // (fl(fl(x_last + x_last) / 1000)); --mode fedavg (default) is
@@ -40,7 +46,7 @@ struct Options {
     int gpus = 1, rounds = -1, port_base = 8079, last_layers = -1;
     fa_mode mode = FA_FEDAVG;
     float divisor = 1000.0f;  // kTrainSize_10, aggregator.cpp:48
-    bool discover = false;
+    bool discover = false, pinned = true;
     double link_mbps = 0;
     std::map<int, double> samples;  // client id -> n_k
 };
@@ -48,7 +54,7 @@ struct Options {
 void usage() {
     std::cerr << "usage: fa_aggregator -i ID -d DATA_OWNERS -c COMPUTE_NODES [--mode fedavg|literal] [--gpus G]\n"
                  "       [--rounds R] [--port-base P] [--discover] [--link-mbps M] [--samples id:n,...]\n"
-                 "       [--divisor K] [--last-layers L]\n";
+                 "       [--divisor K] [--last-layers L] [--no-pinned]\n";
 }
 
 bool parse_args(int argc, char** argv, Options* o) {
@@ -70,6 +76,7 @@ bool parse_args(int argc, char** argv, Options* o) {
         else if (a == "--last-layers") o->last_layers = std::atoi(val("--last-layers"));
         else if (a == "--divisor") o->divisor = (float)std::atof(val("--divisor"));
         else if (a == "--discover") o->discover = true;
+        else if (a == "--no-pinned") o->pinned = false;
         else if (a == "--link-mbps") o->link_mbps = std::atof(val("--link-mbps"));
         else if (a == "--mode") {
             std::string m = val("--mode");
@@ -124,9 +131,16 @@ double secs_since(std::chrono::steady_clock::time_point t) {
 
 class Aggregator {
 public:
-    Aggregator(const Options& o, NetLayer* net) : o_(o), net_(net) {
+    Aggregator(const Options& o, NetLayer* net, const std::vector<int>& owners) : o_(o), net_(net) {
         FA_CHECK(fa_create(&ctx_, o.gpus, o.gpus > 1 ? FA_SHARD_RANGE : 0));
         FA_CHECK(fa_set_literal_divisor(ctx_, -1, o.divisor));
+        std::vector<int> order = owners;
+        if ((int)order.size() != o.data_owners) {
+            order = {0};
+            for (int i = 0; i < o.data_owners - 1; ++i) order.push_back(i + o.compute_nodes + 1);
+        }
+        for (int k = 0; k < (int)order.size(); ++k) slots_.insert({order[k], k});
+        claimed_.assign(o.data_owners, 0);
     }
     ~Aggregator() { fa_destroy(ctx_); }
 
@@ -156,8 +170,14 @@ public:
         std::vector<const void*> ptrs;
         std::vector<size_t> bytes;
         if (ar.param_segments(&ptrs, &bytes)) {
-            FA_CHECK(fa_submit_gather(ctx_, r.model_part, slot, (int)ptrs.size(), ptrs.data(), bytes.data(),
-                                      weight_of(r.client_id)));
+            if (r.frame->pinned) {  // DMA from the frame itself; it is held until the bucket is finalized
+                FA_CHECK(fa_submit_gather_pinned(ctx_, r.model_part, slot, (int)ptrs.size(), ptrs.data(),
+                                                 bytes.data(), weight_of(r.client_id)));
+                b.held.push_back(r.frame);
+            } else {
+                FA_CHECK(fa_submit_gather(ctx_, r.model_part, slot, (int)ptrs.size(), ptrs.data(), bytes.data(),
+                                          weight_of(r.client_id)));
+            }
         } else {  // strided parameters: flatten first
             std::vector<float> flat(b.numel);
             if (!ar.gather_params(flat.data(), &err)) {
@@ -172,14 +192,11 @@ public:
     }
 
     // Reduces bucket mp and returns the framed reply, built once and shared by every destination:
-    // the last receipt's archive with the reduced parameters written straight into the frame.
+    // the last receipt's archive around the reduced parameters, which the D2H copy writes straight
+    // into the frame's parameter records.
     std::shared_ptr<const Bytes> reduce(int mp) {
         Bucket& b = buckets_[mp];
         const auto t0 = std::chrono::steady_clock::now();
-        std::vector<float> out(b.numel);
-        FA_CHECK(fa_finalize(ctx_, mp, out.data()));
-        const auto t1 = std::chrono::steady_clock::now();
-        st_.finalize_s += std::chrono::duration<double>(t1 - t0).count();
         TorchArchive ar;
         std::string err;
         if (!ar.parse(b.last.blob(), b.last.blob_len, &err)) {
@@ -195,12 +212,29 @@ public:
         m.t_start = now_ms();
         char* values = nullptr;
         auto f = operation_frame(m, ar.size(), &values);
-        if (!ar.with_params_into(out.data(), (uint8_t*)values, &err)) {
-            std::cerr << "[aggregator] reply for part " << mp << ": " << err << "\n";
-            std::exit(1);
+        std::vector<void*> dsts;
+        std::vector<size_t> bytes;
+        double t_fin;
+        if (ar.layout_into((uint8_t*)values, &dsts, &bytes, nullptr)) {
+            const auto t1 = std::chrono::steady_clock::now();
+            FA_CHECK(fa_finalize_gather(ctx_, mp, (int)dsts.size(), dsts.data(), bytes.data(),
+                                        f->pinned ? FA_HOST_PINNED : 0));
+            t_fin = secs_since(t1);
+            ar.seal_params((uint8_t*)values);
+        } else {  // strided parameters: through a flat copy
+            const auto t1 = std::chrono::steady_clock::now();
+            std::vector<float> out(b.numel);
+            FA_CHECK(fa_finalize(ctx_, mp, out.data()));
+            t_fin = secs_since(t1);
+            if (!ar.with_params_into(out.data(), (uint8_t*)values, &err)) {
+                std::cerr << "[aggregator] reply for part " << mp << ": " << err << "\n";
+                std::exit(1);
+            }
         }
+        b.held.clear();
         b.bytes_in = 0;
-        st_.frame_s += secs_since(t1);
+        st_.finalize_s += t_fin;
+        st_.frame_s += secs_since(t0) - t_fin;
         return f;
     }
 
@@ -228,18 +262,23 @@ private:
         bool defined = false;
         size_t numel = 0, bytes_in = 0;
         Receipt last;
+        std::vector<std::shared_ptr<const Bytes>> held;  // pinned frames DMA'd from, until finalize
     };
 
     int slot_of(int client) {
         auto it = slots_.find(client);
-        if (it != slots_.end()) return it->second;
-        const int s = (int)slots_.size();
-        if (s >= o_.data_owners) {
-            std::cerr << "[aggregator] more distinct clients than -d " << o_.data_owners << "\n";
-            std::exit(1);
+        if (it == slots_.end()) {  // an id outside the expected list takes the first slot nobody claimed
+            int s = 0;
+            while (s < o_.data_owners && claimed_[s]) ++s;
+            if (s == o_.data_owners) {
+                std::cerr << "[aggregator] more distinct clients than -d " << o_.data_owners << "\n";
+                std::exit(1);
+            }
+            for (auto kv = slots_.begin(); kv != slots_.end();) kv = kv->second == s ? slots_.erase(kv) : std::next(kv);
+            it = slots_.insert({client, s}).first;
         }
-        slots_[client] = s;
-        return s;
+        claimed_[it->second] = 1;
+        return it->second;
     }
 
     float weight_of(int client) const {
@@ -254,7 +293,8 @@ private:
     NetLayer* net_;
     fa_ctx* ctx_ = nullptr;
     std::map<int, Bucket> buckets_;
-    std::map<int, int> slots_;
+    std::map<int, int> slots_;  // client id -> slot
+    std::vector<char> claimed_;  // slot -> an arrived client holds it
     Stats st_;
 };
 
@@ -265,6 +305,16 @@ int main(int argc, char** argv) {
     if (!parse_args(argc, argv, &o)) {
         usage();
         return 2;
+    }
+    std::shared_ptr<BufferPool> pool;  // pinned frame buffers: receipts DMA'd from, replies DMA'd into
+    if (o.pinned) {
+        pool = BufferPool::create(
+            [](size_t n) -> char* {
+                void* p = nullptr;
+                return fa_host_alloc(n, &p) == FA_OK ? (char*)p : nullptr;
+            },
+            [](char* p) { fa_host_free(p); }, true);
+        set_frame_allocator([pool](size_t n) { return pool->get(n); });
     }
     NetLayer net(o.id, RoutingTable(o.port_base));
     net.set_link_mbps(o.link_mbps);
@@ -283,7 +333,7 @@ int main(int argc, char** argv) {
     const int L = o.last_layers > 0 ? o.last_layers : last_part_layers(refactor.model_name, refactor.start);
     std::cerr << "[aggregator] refactor: model " << refactor.model_name << "/" << refactor.model_type << " start "
               << refactor.start << " end " << refactor.end << " -> " << L << " last-part layer(s)\n";
-    Aggregator agg(o, &net);
+    Aggregator agg(o, &net, refactor.data_owners);
 
     for (int round = 0; o.rounds < 0 || round < o.rounds; ++round) {
         // phase 1: model part 1 from every data owner (aggregator.cpp:59-93)

@@ -632,30 +632,68 @@ uint32_t crc32_parallel(const uint8_t* p, size_t n) {
 }  // namespace
 
 bool TorchArchive::with_params_into(const float* src, uint8_t* o, std::string* err) const {
+    std::vector<void*> dsts;
+    std::vector<size_t> bytes;
+    if (layout_into(o, &dsts, &bytes, nullptr)) {  // contiguous fp32 parameters: copy the gaps, then the values
+        for (size_t k = 0; k < dsts.size(); ++k) {
+            uint8_t* d = (uint8_t*)dsts[k];
+            const uint8_t* s0 = (const uint8_t*)src;
+            parallel_ranges(bytes[k], 16u << 20, [&](size_t lo, size_t hi) { std::memcpy(d + lo, s0 + lo, hi - lo); });
+            src += bytes[k] / 4;
+        }
+        seal_params(o);
+        return true;
+    }
     parallel_ranges(size_, 16u << 20, [&](size_t lo, size_t hi) { std::memcpy(o + lo, base_ + lo, hi - lo); });
-    std::vector<char> touched(entries_.size(), 0);
     for (auto& t : params_) {
         if (t.storage_type != "FloatStorage") return fail(err, "parameter " + t.name + " is not fp32");
         uint8_t* d = o + (t.data - base_);
-        if (t.contiguous) {
-            const uint8_t* s0 = (const uint8_t*)src;
-            parallel_ranges((size_t)t.numel * 4, 16u << 20,
-                            [&](size_t lo, size_t hi) { std::memcpy(d + lo, s0 + lo, hi - lo); });
-        } else {
-            std::vector<int64_t> idx(t.sizes.size(), 0);
-            for (int64_t e = 0; e < t.numel; ++e) {
-                int64_t off = 0;
-                for (size_t k = 0; k < idx.size(); ++k) off += idx[k] * t.strides[k];
-                std::memcpy(d + off * 4, src + e, 4);
-                for (size_t k = idx.size(); k-- > 0;) {
-                    if (++idx[k] < t.sizes[k]) break;
-                    idx[k] = 0;
-                }
+        std::vector<int64_t> idx(t.sizes.size(), 0);
+        for (int64_t e = 0; e < t.numel; ++e) {
+            int64_t off = 0;
+            for (size_t k = 0; k < idx.size(); ++k) off += idx[k] * t.strides[k];
+            std::memcpy(d + off * 4, src + e, 4);
+            for (size_t k = idx.size(); k-- > 0;) {
+                if (++idx[k] < t.sizes[k]) break;
+                idx[k] = 0;
             }
         }
         src += t.numel;
-        touched[t.record] = 1;
     }
+    seal_params(o);
+    return true;
+}
+
+bool TorchArchive::layout_into(uint8_t* o, std::vector<void*>* dsts, std::vector<size_t>* bytes,
+                               std::string* err) const {
+    std::vector<std::pair<size_t, size_t>> holes;  // [lo, hi) of each parameter's values
+    for (auto& t : params_) {
+        if (t.storage_type != "FloatStorage") return fail(err, "parameter " + t.name + " is not fp32");
+        if (!t.contiguous) return fail(err, "parameter " + t.name + " is strided");
+        holes.push_back({(size_t)(t.data - base_), (size_t)(t.data - base_) + (size_t)t.numel * 4});
+    }
+    std::vector<std::pair<size_t, size_t>> sorted = holes;
+    std::sort(sorted.begin(), sorted.end());
+    for (size_t k = 1; k < sorted.size(); ++k)
+        if (sorted[k].first < sorted[k - 1].second) return fail(err, "parameters share storage bytes");
+    size_t at = 0;  // everything outside the holes comes from the template
+    for (auto& h : sorted) {
+        if (h.first > at) std::memcpy(o + at, base_ + at, h.first - at);
+        at = std::max(at, h.second);
+    }
+    if (size_ > at) std::memcpy(o + at, base_ + at, size_ - at);
+    dsts->clear();
+    bytes->clear();
+    for (auto& h : holes) {
+        dsts->push_back(o + h.first);
+        bytes->push_back(h.second - h.first);
+    }
+    return true;
+}
+
+void TorchArchive::seal_params(uint8_t* o) const {
+    std::vector<char> touched(entries_.size(), 0);
+    for (auto& t : params_) touched[t.record] = 1;
     for (size_t k = 0; k < entries_.size(); ++k) {
         if (!touched[k]) continue;
         const ZipEntry& z = entries_[k];
@@ -664,7 +702,6 @@ bool TorchArchive::with_params_into(const float* src, uint8_t* o, std::string* e
         if (z.desc_offset) wr32(o + z.desc_offset, c);   // flag bit 3: CRC lives in the data descriptor
         else wr32(o + z.local_offset + 14, c);           // otherwise in the local header
     }
-    return true;
 }
 
 }  // namespace fahost

@@ -65,6 +65,13 @@ public:
     bool with_params(const float* src, std::string* out, std::string* err) const;
     // Same, written into dst[0, size()) (e.g. straight into an outgoing frame).
     bool with_params_into(const float* src, uint8_t* dst, std::string* err) const;
+    // The same in two steps, for a producer that writes the values itself (e.g. a D2H copy straight
+    // into the outgoing frame): layout_into copies everything but the parameter values into dst and
+    // returns where each parameter's values go (named_parameters order; false when a parameter is
+    // strided or not fp32); seal_params then recomputes the CRC-32 of the parameter records.
+    bool layout_into(uint8_t* dst, std::vector<void*>* param_dsts, std::vector<size_t>* param_bytes,
+                     std::string* err) const;
+    void seal_params(uint8_t* dst) const;
     size_t size() const { return size_; }
 
 private:

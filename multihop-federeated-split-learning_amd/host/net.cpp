@@ -5,13 +5,14 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
-#include <sys/select.h>
+#include <poll.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
 #include <chrono>
 #include <cstring>
 #include <iostream>
+#include <list>
 
 namespace fahost {
 
@@ -95,7 +96,7 @@ static bool recv_all(int fd, void* p, size_t n) {
 std::shared_ptr<Bytes> recv_frame(int fd) {
     int32_t len = 0;
     if (!recv_all(fd, &len, 4) || len <= 0) return nullptr;
-    auto b = std::make_shared<Bytes>((size_t)len);
+    auto b = new_frame_buffer((size_t)len);
     if (!recv_all(fd, b->data(), (size_t)len)) return nullptr;
     return b;
 }
@@ -171,7 +172,8 @@ void NetLayer::stop() {
     senders_.clear();
 }
 
-void NetLayer::handle_frame(std::shared_ptr<Bytes> text, bool* keep) {
+NetLayer::Item NetLayer::parse_frame(std::shared_ptr<Bytes> text, bool* keep) {
+    Item it;
     // Parse the header without touching the archive: the header is the text before "values : ".
     const size_t scan = std::min<size_t>(text->size(), 4096);
     const char* base = text->data();
@@ -186,11 +188,12 @@ void NetLayer::handle_frame(std::shared_ptr<Bytes> text, bool* keep) {
     std::string err;
     if (!decode(head, &m, &err)) {
         std::cerr << "[net] dropping malformed frame: " << err << "\n";
-        return;
+        return it;
     }
     *keep = m.save_connection == 1;
     if (m.type == OPERATION) {
-        Receipt r;
+        Receipt& r = it.r;
+        it.kind = 1;
         r.client_id = m.client_id;
         r.prev_node = m.prev_node;
         r.model_part = m.model_part;
@@ -206,65 +209,102 @@ void NetLayer::handle_frame(std::shared_ptr<Bytes> text, bool* keep) {
             if (due > now) std::this_thread::sleep_for(std::chrono::milliseconds(due - now));
         }
         r.frame = std::move(text);
-        {
-            std::lock_guard<std::mutex> lk(m_rx_);
-            receipts_.push_back(std::move(r));
-        }
-        cv_rx_.notify_all();
     } else {
-        if (m.read_table == 1) routes_.apply(m.rooting_table);
-        {
-            std::lock_guard<std::mutex> lk(m_rx_);
-            refactors_.push_back(std::move(m));
+        it.kind = 2;
+        if (m.read_table == 1) {
+            std::lock_guard<std::mutex> g(m_routes_);
+            routes_.apply(m.rooting_table);
         }
-        cv_rx_.notify_all();
+        it.m = std::move(m);
     }
+    return it;
+}
+
+uint64_t NetLayer::take_seq() {
+    std::lock_guard<std::mutex> lk(m_rx_);
+    return next_seq_++;
+}
+
+void NetLayer::publish(uint64_t seq, Item item) {
+    {
+        std::lock_guard<std::mutex> lk(m_rx_);
+        pending_.emplace(seq, std::move(item));
+        for (auto it = pending_.find(next_pub_); it != pending_.end(); it = pending_.find(next_pub_)) {
+            if (it->second.kind == 1) receipts_.push_back(std::move(it->second.r));
+            else if (it->second.kind == 2) refactors_.push_back(std::move(it->second.m));
+            pending_.erase(it);
+            ++next_pub_;
+        }
+    }
+    cv_rx_.notify_all();
 }
 
 void NetLayer::receiver_loop() {
-    std::vector<int> open;  // connections kept open by save_connection == 1
+    std::list<std::unique_ptr<Conn>> conns;
+    auto reap = [&](bool all) {
+        for (auto it = conns.begin(); it != conns.end();) {
+            Conn& c = **it;
+            if (all && !c.done) {
+                std::lock_guard<std::mutex> g(c.m);
+                if (c.fd >= 0) shutdown(c.fd, SHUT_RDWR);  // unblocks a reader inside recv
+            }
+            if (all || c.done) {
+                c.th.join();
+                it = conns.erase(it);
+            } else {
+                ++it;
+            }
+        }
+    };
     while (running_) {
-        fd_set rs;
-        FD_ZERO(&rs);
-        int maxfd = listen_fd_;
         if (listen_fd_ < 0) break;
-        FD_SET(listen_fd_, &rs);
-        for (int fd : open) {
-            FD_SET(fd, &rs);
-            maxfd = std::max(maxfd, fd);
+        pollfd p{listen_fd_, POLLIN, 0};
+        if (poll(&p, 1, 200) <= 0) {
+            reap(false);
+            continue;
         }
-        timeval tv{0, 200000};
-        int n = select(maxfd + 1, &rs, nullptr, nullptr, &tv);
-        if (n <= 0) continue;
-        for (size_t i = 0; i < open.size();) {
-            int fd = open[i];
-            if (FD_ISSET(fd, &rs)) {
-                auto text = recv_frame(fd);
-                bool keep = true;
-                if (!text) {
-                    close(fd);
-                    open.erase(open.begin() + (long)i);
-                    continue;
-                }
-                bytes_rx_ += text->size() + 4;
-                handle_frame(text, &keep);
-            }
-            ++i;
-        }
-        if (listen_fd_ >= 0 && FD_ISSET(listen_fd_, &rs)) {
-            int fd = accept(listen_fd_, nullptr, nullptr);
-            if (fd < 0) continue;
-            auto text = recv_frame(fd);
-            bool keep = false;
-            if (text) {
-                bytes_rx_ += text->size() + 4;
-                handle_frame(text, &keep);
-            }
-            if (keep) open.push_back(fd);
-            else close(fd);
-        }
+        int fd = accept(listen_fd_, nullptr, nullptr);
+        if (fd < 0) continue;
+        big_buffers(fd);
+        conns.emplace_back(new Conn());
+        Conn* c = conns.back().get();
+        c->fd = fd;
+        c->seq0 = take_seq();  // accept order fixes the FIFO position of the connection's first frame
+        c->th = std::thread(&NetLayer::reader_loop, this, c);
+        reap(false);
     }
-    for (int fd : open) close(fd);
+    reap(true);
+}
+
+// One connection: one frame (the reference's default, save_connection 0), or frames until EOF when
+// the sender keeps the connection open (save_connection 1).
+void NetLayer::reader_loop(Conn* c) {
+    const int fd = c->fd;
+    uint64_t seq = c->seq0;
+    for (;;) {
+        auto text = recv_frame(fd);
+        if (!text) {
+            publish(seq, Item{});  // release the FIFO position
+            break;
+        }
+        bytes_rx_ += text->size() + 4;
+        bool keep = false;
+        publish(seq, parse_frame(text, &keep));
+        if (!keep) break;
+        bool ready = false;
+        while (running_ && !ready) {
+            pollfd p{fd, POLLIN, 0};
+            ready = poll(&p, 1, 200) > 0;
+        }
+        if (!ready) break;
+        seq = take_seq();  // the next frame on a kept-open connection queues from when it begins
+    }
+    {
+        std::lock_guard<std::mutex> g(c->m);
+        close(fd);
+        c->fd = -1;
+    }
+    c->done = true;
 }
 
 void NetLayer::sender_loop(int i) {
@@ -282,10 +322,16 @@ void NetLayer::sender_loop(int i) {
         int fd = -1;
         auto it = me.open.find(o.dest);
         if (it != me.open.end()) fd = it->second;
-        if (fd < 0) fd = connect_to(routes_.host_for(o.dest), routes_.port_for(o.dest), 100, 200);
+        std::string host;
+        int port;
+        {
+            std::lock_guard<std::mutex> g(m_routes_);
+            host = routes_.host_for(o.dest);
+            port = routes_.port_for(o.dest);
+        }
+        if (fd < 0) fd = connect_to(host, port, 100, 200);
         if (fd < 0) {
-            std::cerr << "[net] cannot reach node " << o.dest << " at " << routes_.host_for(o.dest) << ":"
-                      << routes_.port_for(o.dest) << "\n";
+            std::cerr << "[net] cannot reach node " << o.dest << " at " << host << ":" << port << "\n";
         } else if (!send_all(fd, o.bytes->data(), o.bytes->size())) {
             std::cerr << "[net] send to node " << o.dest << " failed\n";
             close(fd);

@@ -2,10 +2,20 @@
 // (pipeline_simulation/network_layer.{h,cpp}), wire-compatible.
 //
 // Threading model kept from the reference (network_layer.h:49-63, .cpp:372-480):
-// a receiver thread (select/accept, frames -> FIFO task queue under a mutex +
-// condvar), sender threads (queue of outgoing frames, connect with retries,
-// close unless save_connection), and the main thread as the single consumer.
+// a receiver thread (accept, frames -> FIFO task queue under a mutex + condvar),
+// sender threads (queue of outgoing frames, connect with retries, close unless
+// save_connection), and the main thread as the single consumer.
 // Differences, all deliberate:
+//  * every accepted connection is read by its own thread, so D data owners
+//    sending at once are received in parallel (the reference reads one frame at
+//    a time in its select loop, :372-480).  The FIFO still holds frames in the
+//    reference's order -- the order their connections were accepted (or, on a
+//    kept-open connection, the order the frames began): each frame takes a
+//    sequence number there and a reorder buffer publishes them in that order, so
+//    frames one node sends back to back are consumed in the order it sent them;
+//  * frame buffers come from new_frame_buffer (wire.h): the aggregator installs
+//    a pool of pinned buffers, so a receipt's records go to the GPU by DMA
+//    straight from the bytes they arrived in;
 //  * a receipt keeps the frame bytes it arrived in (read once, not zero-filled)
 //    and points at the archive inside them -- the reference makes ~10 full
 //    copies of every blob;
@@ -94,9 +104,24 @@ private:
         bool busy = false;
         std::map<int, int> open;  // dest -> socket kept open (save_connection)
     };
+    struct Conn {
+        std::thread th;
+        std::atomic<bool> done{false};
+        std::mutex m;
+        int fd = -1;         // -1 once the reader closed it
+        uint64_t seq0 = 0;   // sequence number of the connection's first frame (taken at accept)
+    };
+    struct Item {  // a parsed frame waiting for its turn in the FIFO
+        int kind = 0;  // 0 nothing (closed without a frame / malformed), 1 receipt, 2 refactor
+        Receipt r;
+        Message m;
+    };
+    uint64_t take_seq();
+    void publish(uint64_t seq, Item item);
     void receiver_loop();
+    void reader_loop(Conn* c);
     void sender_loop(int i);
-    void handle_frame(std::shared_ptr<Bytes> text, bool* keep);
+    Item parse_frame(std::shared_ptr<Bytes> text, bool* keep);
 
     int my_id_;
     RoutingTable routes_;
@@ -110,9 +135,12 @@ private:
     std::condition_variable cv_rx_;
     std::deque<Receipt> receipts_;
     std::deque<Message> refactors_;
+    uint64_t next_seq_ = 0, next_pub_ = 0;  // under m_rx_
+    std::map<uint64_t, Item> pending_;       // finished frames waiting for an earlier one
     std::mutex m_tx_;
     std::condition_variable cv_tx_, cv_tx_idle_;
     std::vector<std::unique_ptr<Sender>> senders_;
+    std::mutex m_routes_;  // routes_ is updated by readers (refactor) and read by senders
 };
 
 // Blocking helpers shared with the test tools.

@@ -95,10 +95,69 @@ std::string operation_header(const Message& m) {
     return t + "values : ";
 }
 
+namespace {
+FrameAllocator& frame_allocator() {
+    static FrameAllocator a;
+    return a;
+}
+}  // namespace
+
+void set_frame_allocator(FrameAllocator a) { frame_allocator() = std::move(a); }
+
+std::shared_ptr<Bytes> new_frame_buffer(size_t n) {
+    auto& a = frame_allocator();
+    return a ? a(n) : std::make_shared<Bytes>(n);
+}
+
+std::shared_ptr<BufferPool> BufferPool::create(AllocFn alloc, FreeFn free, bool pinned, size_t min_bytes) {
+    return std::shared_ptr<BufferPool>(new BufferPool(std::move(alloc), std::move(free), pinned, min_bytes));
+}
+
+BufferPool::~BufferPool() {
+    for (auto& kv : free_) free_fn_(kv.second);
+}
+
+std::shared_ptr<Bytes> BufferPool::get(size_t n) {
+    if (n < min_) return std::make_shared<Bytes>(n);
+    const size_t cls = (n + (2u << 20) - 1) / (2u << 20) * (2u << 20);
+    char* p = nullptr;
+    {
+        std::lock_guard<std::mutex> g(m_);
+        auto it = free_.find(cls);
+        if (it != free_.end()) {
+            p = it->second;
+            free_.erase(it);
+        }
+    }
+    if (!p) {
+        p = alloc_(cls);
+        if (!p) throw std::bad_alloc();
+        std::lock_guard<std::mutex> g(m_);
+        ++allocs_;
+    }
+    std::weak_ptr<BufferPool> self = shared_from_this();
+    FreeFn fallback = free_fn_;
+    return std::make_shared<Bytes>(p, n, pinned_, [self, cls, fallback](char* q) {
+        if (auto pool = self.lock()) {
+            std::lock_guard<std::mutex> g(pool->m_);
+            pool->free_.insert({cls, q});
+        } else {
+            fallback(q);
+        }
+    });
+}
+
+size_t BufferPool::cached_bytes() {
+    std::lock_guard<std::mutex> g(m_);
+    size_t t = 0;
+    for (auto& kv : free_) t += kv.first;
+    return t;
+}
+
 std::shared_ptr<Bytes> operation_frame(const Message& m, size_t values_len, char** values) {
     const std::string head = operation_header(m);
     const size_t text = head.size() + values_len + 3;
-    auto b = std::make_shared<Bytes>(4 + text);
+    auto b = new_frame_buffer(4 + text);
     const int32_t len = (int32_t)text;
     std::memcpy(b->data(), &len, 4);  // native-endian int, as my_send does (network_layer.cpp:16)
     std::memcpy(b->data() + 4, head.data(), head.size());
@@ -115,7 +174,7 @@ std::shared_ptr<Bytes> frame_bytes(const Message& m) {
         return b;
     }
     const std::string text = encode(m);
-    auto b = std::make_shared<Bytes>(4 + text.size());
+    auto b = new_frame_buffer(4 + text.size());
     const int32_t len = (int32_t)text.size();
     std::memcpy(b->data(), &len, 4);
     std::memcpy(b->data() + 4, text.data(), text.size());

@@ -12,7 +12,10 @@
 #pragma once
 
 #include <cstdint>
+#include <functional>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <utility>
 #include <vector>
@@ -36,14 +39,58 @@ struct Message {  // Message.h:571-616 field for field
     std::string values;
 };
 
-// A heap byte buffer that is NOT zero-filled (frames are hundreds of MB).
+// A byte buffer that is NOT zero-filled (frames are hundreds of MB).  Heap memory by default; a
+// buffer handed out by a pool carries the pool's release function (and `pinned` when the memory is
+// page-locked, i.e. a DMA engine can read or write it in place).
 struct Bytes {
-    std::unique_ptr<char[]> p;
+    char* p = nullptr;
     size_t n = 0;
+    bool pinned = false;
+    std::function<void(char*)> release;  // empty: delete[]
     explicit Bytes(size_t size) : p(new char[size]), n(size) {}
-    char* data() { return p.get(); }
-    const char* data() const { return p.get(); }
+    Bytes(char* mem, size_t size, bool is_pinned, std::function<void(char*)> rel)
+        : p(mem), n(size), pinned(is_pinned), release(std::move(rel)) {}
+    ~Bytes() {
+        if (release) release(p);
+        else delete[] p;
+    }
+    Bytes(const Bytes&) = delete;
+    Bytes& operator=(const Bytes&) = delete;
+    char* data() { return p; }
+    const char* data() const { return p; }
     size_t size() const { return n; }
+};
+
+// Where frame buffers come from (received frames, outgoing frames).  Process-wide; install before
+// any network thread starts.  Default: new_frame_buffer == make_shared<Bytes>(n).
+using FrameAllocator = std::function<std::shared_ptr<Bytes>(size_t)>;
+void set_frame_allocator(FrameAllocator a);
+std::shared_ptr<Bytes> new_frame_buffer(size_t n);
+
+// A recycling pool of large frame buffers over an allocator pair (e.g. fa_host_alloc/fa_host_free
+// for pinned memory).  Buffers of at least `min_bytes` are rounded up to 2 MiB classes and return to
+// the pool when their last reference goes; a round's frames have the same sizes as the last
+// round's, so the steady state allocates nothing.  Smaller requests use the heap.
+class BufferPool : public std::enable_shared_from_this<BufferPool> {
+public:
+    using AllocFn = std::function<char*(size_t)>;
+    using FreeFn = std::function<void(char*)>;
+    static std::shared_ptr<BufferPool> create(AllocFn alloc, FreeFn free, bool pinned, size_t min_bytes = 1u << 20);
+    ~BufferPool();
+    std::shared_ptr<Bytes> get(size_t n);
+    size_t cached_bytes();
+    size_t allocations() const { return allocs_; }
+
+private:
+    BufferPool(AllocFn a, FreeFn f, bool pinned, size_t min_bytes)
+        : alloc_(std::move(a)), free_fn_(std::move(f)), pinned_(pinned), min_(min_bytes) {}
+    AllocFn alloc_;
+    FreeFn free_fn_;
+    bool pinned_;
+    size_t min_;
+    std::mutex m_;
+    std::multimap<size_t, char*> free_;  // class size -> buffer
+    size_t allocs_ = 0;
 };
 
 // Text of a frame (without the length prefix).

@@ -52,7 +52,7 @@ def test_library_is_gfx950_code(fa, tmp_path):
 
 def test_version_and_errors_without_gpu(fa):
     L = fa.lib()
-    assert L.fa_version() == 1
+    assert L.fa_version() == 2
     # argument errors are reported before any device work
     rc = L.fa_reduce_device(None, 0, None, None, 0, 16, 0, None, 0, 0, None, None)
     assert rc == fa.ERR_ARG and "null" in fa.last_error()
@@ -61,6 +61,12 @@ def test_version_and_errors_without_gpu(fa):
     assert L.fa_set_tuning(ctypes.byref(t)) == fa.ERR_ARG
     assert L.fa_bucket_define(None, 1, 10, 0, 0, 1, 0) == fa.ERR_ARG
     assert fa.last_error() == "ctx is null"
+    assert L.fa_finalize_gather(None, 1, 0, None, None, 0) == fa.ERR_ARG
+    assert L.fa_finalize_gather(None, 1, 0, None, None, 4) == fa.ERR_ARG and "flags" in fa.last_error()
+    assert L.fa_submit_gather_pinned(None, 1, 0, 0, None, None, ctypes.c_float(1.0)) == fa.ERR_ARG
+    out = ctypes.c_void_p(1)
+    assert L.fa_host_alloc(ctypes.c_size_t(0), ctypes.byref(out)) == 0 and out.value is None
+    assert L.fa_host_free(None) == 0
 
 
 def test_tuning_roundtrip(fa):

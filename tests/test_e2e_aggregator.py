@@ -35,7 +35,7 @@ def ports_free(base, span=40):
 
 def pick_base():
     for _ in range(50):
-        b = random.randrange(20000, 60000, 100)
+        b = random.randrange(10000, 32000, 100)  # below the ephemeral port range
         if ports_free(b):
             return b
     pytest.skip("no free port range")
@@ -66,6 +66,49 @@ def test_lenet_rounds_over_tcp(torch_gpu, mode, D, rounds):
         assert agg.returncode == 0, err[-2000:]
         stats = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
         assert len(stats) == rounds and stats[0]["phase2"]["layers"] == 2
+    finally:
+        if agg.poll() is None:
+            agg.kill()
+
+
+def _large_parts(d):
+    """Model-part archives of a few MB (torch.jit.save: the same zip/pickle layout as torch::save), big
+    enough that the aggregator receives them into its pooled pinned buffers and replies from them."""
+    import torch
+    import torch.nn as nn
+    torch.manual_seed(1)
+    parts = {1: nn.Sequential(nn.Conv2d(3, 64, 3), nn.ReLU(), nn.Conv2d(64, 64, 3)),
+             2: nn.Sequential(nn.Linear(1024, 1536), nn.ReLU()),
+             3: nn.Sequential(nn.Linear(1536, 1000), nn.ReLU(), nn.Linear(1000, 10))}
+    for mp, m in parts.items():
+        torch.jit.save(torch.jit.script(m), os.path.join(d, "mp%d_client0.pt" % mp))
+    return {mp: sum(p.numel() for p in m.parameters()) for mp, m in parts.items()}
+
+
+@pytest.mark.parametrize("pinned,sequential", [(True, False), (False, False), (True, True)])
+def test_multi_mb_parts_concurrent_owners(torch_gpu, tmp_path, pinned, sequential):
+    """D=6 owners sending at once (or one after another) multi-MB parts: pinned zero-copy ingest
+    (fa_submit_gather_pinned from the received frame) and D2H into the reply frame
+    (fa_finalize_gather), or the pageable staging path with --no-pinned; bit-exact FedAvg every round."""
+    sizes = _large_parts(str(tmp_path))
+    D, rounds = 6, 2
+    base = pick_base()
+    cmd = [AGG, "-i", "-1", "-d", str(D), "-c", "1", "--rounds", str(rounds), "--port-base", str(base)]
+    agg = subprocess.Popen(cmd + ([] if pinned else ["--no-pinned"]), stdout=subprocess.PIPE,
+                           stderr=subprocess.PIPE, text=True)
+    try:
+        time.sleep(0.5)
+        r = subprocess.run([OWNERS, "--blobs", str(tmp_path), "--parts", "1,2,3", "-d", str(D), "-c", "1",
+                            "--rounds", str(rounds), "--port-base", str(base), "--model-name", "1", "--start", "9",
+                            "--end", "3"] + (["--sequential"] if sequential else []),
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res = json.loads(r.stdout.strip().splitlines()[-1])
+        assert res["ok"] and res["checked_elems"] == rounds * D * sum(sizes.values())
+        out, err = agg.communicate(timeout=60)
+        assert agg.returncode == 0, err[-2000:]
+        stats = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+        assert len(stats) == rounds
     finally:
         if agg.poll() is None:
             agg.kill()

@@ -375,3 +375,48 @@ def test_context_submit_gather_matches_flat(fa, O, torch_gpu):
         assert_bits(agg.finalize(1), O.fedavg(xs, w))
         with pytest.raises(fa.FaError):
             agg.submit_gather(1, 0, [xs[0][:10]], w[0])  # wrong total size
+
+
+@pytest.mark.parametrize("gpus", [1, 2])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_context_zero_copy_gather_in_and_out(fa, O, torch_gpu, pinned, gpus):
+    """fa_submit_gather_pinned + fa_finalize_gather: receipts as ragged records at odd byte offsets of one
+    pinned frame buffer (how the network layer hands them over), the result scattered into the records
+    of a reply buffer; == the flat path, bit for bit.  gpus=2 splits the ranges across record pieces."""
+    if gpus > fa.device_count():
+        gpus = 1
+    n, D = 3_000_017, 3
+    w = O.weights(D)
+    xs = host_clients(O, 53, D, n, False)
+    cuts = [0, 5, 4096, 777_777, 2_000_000, n]
+    hdr = 13  # the archive starts after a text header: records are not 16-byte aligned in host memory
+    frames = [fa.PinnedBuffer(hdr + 4 * n + 64 * len(cuts)) for _ in range(D)] if pinned else None
+    pieces = []
+    for k in range(D):
+        raw = frames[k].view() if pinned else np.empty(hdr + 4 * n + 64 * len(cuts), np.uint8)
+        ps, off = [], hdr
+        for a, b in zip(cuts, cuts[1:]):
+            seg = raw[off:off + 4 * (b - a)]
+            seg[:] = xs[k][a:b].view(np.uint8)
+            ps.append(seg)
+            off += 4 * (b - a) + 64 - (4 * (b - a)) % 64 + 3
+        pieces.append(ps)
+    reply = fa.PinnedBuffer(4 * n + 100) if pinned else None
+    rraw = reply.view() if pinned else np.zeros(4 * n + 100, np.uint8)
+    out_cuts = [0, 1, 333_333, n]
+    outs = [rraw[7 + 4 * a: 7 + 4 * b] for a, b in zip(out_cuts, out_cuts[1:])]
+    with fa.Aggregator(gpus) as agg:
+        agg.define(1, n, fa.F32, fa.F32, D, fa.FEDAVG)
+        for k in range(D):
+            agg.submit_gather(1, k, pieces[k], w[k], pinned=pinned)
+        agg.finalize_gather(1, outs, pinned=pinned)
+        got = np.concatenate([o.view(np.float32) if o.ctypes.data % 4 == 0 else o.copy().view(np.float32)
+                              for o in outs])
+        assert_bits(got, O.fedavg(xs, w))
+        assert not rraw[:7].any()  # nothing written outside the pieces
+        with pytest.raises(fa.FaError):
+            agg.finalize_gather(1, outs[:1], pinned=pinned)  # nothing submitted / wrong size
+    for f in frames or []:
+        f.close()
+    if reply:
+        reply.close()

@@ -13,7 +13,7 @@ import zipfile
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, PKG_DIR
+from conftest import GOLDEN, PKG_DIR, ROOT
 
 TOOL = os.path.join(PKG_DIR, "bin", "fa_archive_tool")
 BLOBS = [(cfg, mp) for cfg in ("lenet5_c1", "resnet18_c2") for mp in (1, 2, 3)
@@ -100,3 +100,17 @@ def test_archive_rejects_garbage(tmp_path):
     p.write_bytes(b"PK\x03\x04" + b"\x00" * 100)
     r = subprocess.run([TOOL, "dump", str(p)], capture_output=True, text=True)
     assert r.returncode != 0 and "zip" in r.stderr
+
+
+@pytest.mark.parametrize("cfg", ["lenet5_c1", "resnet18_c2"])
+def test_net_layer_and_buffer_pool_selftest(cfg):
+    """CPU: concurrent per-connection receive in accept order, pooled frame buffers recycled after
+    round 1, serialize-once fan-out in order per destination, and the split reply-archive copy
+    (layout_into + seal_params == with_params_into) on a reference-built archive."""
+    subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "tools")], check=True, capture_output=True)
+    exe = os.path.join(ROOT, "tests", "tools", "bin", "net_selftest")
+    r = subprocess.run([exe, os.path.join(GOLDEN, cfg, "mp1_client0.pt")], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["ok"] and res["archive_bytes"] > 0

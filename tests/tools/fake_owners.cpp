@@ -8,8 +8,13 @@
 //
 //   fa_fake_owners --blobs DIR --parts 1,2,3 -d D -c C [--rounds R] [--mode fedavg|literal]
 //                  [--port-base P] [--model-name N --model-type T --start S --end E] [--seed X]
+//                  [--sequential]   (owners send at once, one connection each, unless --sequential
+//                                    or --mode literal, whose result depends on the arrival order)
 // Prints one JSON line: {"ok": bool, "rounds": R, "checked_elems": ..., "round_ms": [...]}.
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -59,6 +64,7 @@ int main(int argc, char** argv) {
     int D = 2, C = 1, rounds = 1, port_base = 8079, model_name = 2, model_type = 0, start = 6, end = 1;
     uint64_t seed = 0x5EED;
     float divisor = 1000.0f;
+    bool concurrent = true;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
         const char* v = i + 1 < argc ? argv[i + 1] : "";
@@ -75,11 +81,13 @@ int main(int argc, char** argv) {
         else if (a == "--end") end = std::atoi(v), ++i;
         else if (a == "--seed") seed = std::strtoull(v, nullptr, 0), ++i;
         else if (a == "--divisor") divisor = (float)std::atof(v), ++i;
+        else if (a == "--sequential") concurrent = false;
         else {
             std::cerr << "unknown argument " << a << "\n";
             return 2;
         }
     }
+    if (mode == "literal") concurrent = false;
     // template archives
     std::vector<Part> parts;
     {
@@ -185,12 +193,34 @@ int main(int argc, char** argv) {
         std::vector<Receipt> replies;
         for (int phase = 1; phase <= 2 && ok; ++phase) {
             int sent = 0;
+            std::vector<std::vector<std::shared_ptr<const Bytes>>> by_owner(D);
             for (int k = 0; k < D; ++k)
                 for (auto& p : parts) {
                     if ((phase == 1) != (p.mp == 1)) continue;
-                    tx.send(-1, frames[p.mp][k]);
+                    by_owner[k].push_back(frames[p.mp][k]);
                     ++sent;
                 }
+            if (concurrent) {  // every owner is its own process in the reference: they send at once
+                std::vector<std::thread> th;
+                std::atomic<bool> send_ok{true};
+                for (int k = 0; k < D; ++k)
+                    th.emplace_back([&, k] {
+                        for (auto& f : by_owner[k]) {
+                            const int fd = connect_to(routes.host_for(-1), routes.port_for(-1), 100, 200);
+                            if (fd < 0 || !send_all(fd, f->data(), f->size())) send_ok = false;
+                            if (fd >= 0) close(fd);
+                        }
+                    });
+                for (auto& t : th) t.join();
+                if (!send_ok) {
+                    std::cerr << "send to the aggregator failed\n";
+                    ok = false;
+                    break;
+                }
+            } else {  // one after another, in owner order (literal mode: the last receipt is owner D-1's)
+                for (int k = 0; k < D; ++k)
+                    for (auto& f : by_owner[k]) tx.send(-1, f);
+            }
             std::vector<Receipt> got;
             if (!collect(sent, &got)) {
                 std::cerr << "timed out waiting for phase " << phase << " replies\n";

@@ -1,0 +1,182 @@
+// net_selftest.cpp -- TEST TOOL (CPU): the aggregator's network layer and frame buffers without a GPU.
+//  * D senders push frames at once (one connection each) into one NetLayer; every receipt arrives
+//    once, intact, with its header fields (concurrent per-connection readers);
+//  * frame buffers come from a BufferPool: after the first round no new allocation happens
+//    (recycling), and receipts carry the pool's `pinned` tag;
+//  * a frame queued for several destinations reaches each of them (serialize-once fan-out), in
+//    order per destination;
+//  * TorchArchive::layout_into + seal_params == with_params_into on a real archive (optional arg).
+// Prints one JSON line {"ok": ..., ...}; exit 0 iff ok.
+#include <unistd.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <sstream>
+#include <thread>
+#include <vector>
+
+#include "archive.h"
+#include "net.h"
+
+using namespace fahost;
+
+static std::shared_ptr<Bytes> make_frame(int client, int part, size_t payload, uint8_t fill) {
+    Message m;
+    m.type = OPERATION;
+    m.client_id = client;
+    m.prev_node = -1;
+    m.type_op = AGGREGATION;
+    m.model_part = part;
+    m.t_start = 1700000000000L + client;
+    char* v = nullptr;
+    auto f = operation_frame(m, payload, &v);
+    for (size_t i = 0; i < payload; ++i) v[i] = (char)(fill + i * 7);
+    return f;
+}
+
+int main(int argc, char** argv) {
+    const int D = 6, rounds = 3;
+    const size_t payload = 3u << 20;  // > the pool's 1 MiB floor
+    bool ok = true;
+    std::atomic<size_t> live_allocs{0};
+    auto pool = BufferPool::create(
+        [&](size_t n) -> char* {
+            ++live_allocs;
+            return (char*)std::malloc(n);
+        },
+        [&](char* p) {
+            --live_allocs;
+            std::free(p);
+        },
+        true);
+    set_frame_allocator([pool](size_t n) { return pool->get(n); });
+    const int base = 10000 + (int)(getpid() % 2000) * 10;  // below the ephemeral port range
+    RoutingTable routes(base);
+    NetLayer agg(-1, routes);
+    if (!agg.start()) {
+        std::cerr << "bind failed\n";
+        return 1;
+    }
+    size_t allocs_after_first = 0;
+    for (int r = 0; r < rounds; ++r) {
+        std::vector<std::shared_ptr<Bytes>> frames;
+        for (int k = 0; k < D; ++k) frames.push_back(make_frame(100 + k, 2 + (k % 2), payload, (uint8_t)(r * 31 + k)));
+        std::vector<std::thread> th;
+        for (int k = 0; k < D; ++k)
+            th.emplace_back([&, k] {
+                const int fd = connect_to("127.0.0.1", routes.port_for(-1), 50, 100);
+                if (fd < 0 || !send_all(fd, frames[k]->data(), frames[k]->size())) {
+                    std::cerr << "sender " << k << " failed\n";
+                    ok = false;
+                }
+                if (fd >= 0) close(fd);
+            });
+        for (auto& t : th) t.join();
+        std::vector<char> seen(D, 0);
+        for (int i = 0; i < D; ++i) {
+            Receipt rc;
+            if (!agg.try_next_receipt(&rc, 20000)) {
+                std::cerr << "round " << r << ": receipt " << i << " missing\n";
+                ok = false;
+                break;
+            }
+            const int k = rc.client_id - 100;
+            if (k < 0 || k >= D || seen[k]) {
+                ok = false;
+                continue;
+            }
+            seen[k] = 1;
+            if (!(rc.model_part == 2 + (k % 2) && rc.type_op == AGGREGATION && rc.blob_len == payload &&
+                  rc.t_start == 1700000000000L + 100 + k && rc.frame->pinned)) {
+                std::cerr << "round " << r << ": bad header fields for client " << k << "\n";
+                ok = false;
+            }
+            const char* v = (const char*)rc.blob();
+            for (size_t j = 0; j < payload; j += 4099)
+                if (v[j] != (char)((uint8_t)(r * 31 + k) + j * 7)) {
+                    std::cerr << "payload mismatch client " << k << " at " << j << "\n";
+                    ok = false;
+                    break;
+                }
+        }
+        if (r == 0) allocs_after_first = pool->allocations();
+    }
+    const size_t allocs = pool->allocations();
+    if (allocs != allocs_after_first) {  // rounds 2.. reuse the first round's buffers
+        std::cerr << "pool allocated " << allocs - allocs_after_first << " buffers after round 1\n";
+        ok = false;
+    }
+
+    // fan-out: one frame to three destinations, each one in order
+    std::vector<std::unique_ptr<NetLayer>> dests;
+    for (int id = 4; id < 7; ++id) {  // 3 < id < 18: port(0) + id + 3
+        dests.emplace_back(new NetLayer(id, routes));
+        if (!dests.back()->start()) {
+            std::cerr << "cannot listen for node " << id << "\n";
+            ok = false;
+        }
+    }
+    auto a = make_frame(-1, 2, payload, 1), b = make_frame(-1, 3, 1000, 2);
+    for (int id = 4; id < 7; ++id) {
+        agg.send(id, a);
+        agg.send(id, b);
+    }
+    agg.flush();
+    for (auto& d : dests) {
+        Receipt r1, r2;
+        if (!(d->try_next_receipt(&r1, 20000) && d->try_next_receipt(&r2, 20000) && r1.model_part == 2 &&
+              r2.model_part == 3 && r1.blob_len == payload && r2.blob_len == 1000)) {
+            std::cerr << "fan-out: destination missed a frame or got them out of order\n";
+            ok = false;
+        }
+        d->stop();
+    }
+    agg.stop();
+
+    // archive split copy: layout_into + values + seal_params == with_params_into
+    size_t checked_archive = 0;
+    if (argc > 1) {
+        std::ifstream f(argv[1], std::ios::binary);
+        std::stringstream ss;
+        ss << f.rdbuf();
+        const std::string blob = ss.str();
+        TorchArchive ar;
+        std::string err;
+        if (!ar.parse((const uint8_t*)blob.data(), blob.size(), &err)) {
+            std::cerr << err << "\n";
+            return 1;
+        }
+        std::vector<float> vals((size_t)ar.param_numel());
+        for (size_t i = 0; i < vals.size(); ++i) vals[i] = (float)i * 0.25f - 3.0f;
+        std::vector<uint8_t> one(ar.size()), two(ar.size(), 0xAB);
+        if (!ar.with_params_into(vals.data(), one.data(), &err)) {
+            std::cerr << "with_params_into: " << err << "\n";
+            ok = false;
+        }
+        std::vector<void*> dsts;
+        std::vector<size_t> bytes;
+        if (!ar.layout_into(two.data(), &dsts, &bytes, &err)) {
+            std::cerr << "layout_into: " << err << "\n";
+            ok = false;
+        }
+        const float* src = vals.data();
+        for (size_t k = 0; k < dsts.size(); ++k) {
+            std::memcpy(dsts[k], src, bytes[k]);
+            src += bytes[k] / 4;
+        }
+        ar.seal_params(two.data());
+        if (one != two) {
+            std::cerr << "layout_into + seal_params differs from with_params_into\n";
+            ok = false;
+        }
+        checked_archive = ar.size();
+    }
+    printf("{\"ok\": %s, \"rounds\": %d, \"senders\": %d, \"pool_allocations\": %zu, \"live_after\": %zu, "
+           "\"archive_bytes\": %zu}\n",
+           ok ? "true" : "false", rounds, D, allocs, (size_t)live_allocs, checked_archive);
+    return ok ? 0 : 1;
+}

@@ -49,7 +49,7 @@ def main():
     with tempfile.TemporaryDirectory() as d:
         sizes = vgg_c4_parts(d)
         out["params_per_part"] = sizes
-        base = random.randrange(20000, 60000, 100)
+        base = random.randrange(10000, 32000, 100)  # below the ephemeral port range
         agg = subprocess.Popen([AGG, "-i", "-1", "-d", str(D), "-c", "1", "--rounds", str(rounds), "--port-base",
                                 str(base)], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
         time.sleep(0.5)

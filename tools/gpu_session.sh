@@ -55,7 +55,7 @@ for s in $STEPS; do
             --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2 --dist-backend gloo > "$OUT/bench_2ranks.json" 2> "$OUT/bench_2ranks.err"
         rc=$?; cat "$OUT/bench_2ranks.json"; tail -3 "$OUT/bench_2ranks.err"; ok_or_fail $rc ranks ;;
     e2e)
-        timeout -k 10 900 python tools/e2e_bench.py 4 2 > "$OUT/e2e_bench.json" 2> "$OUT/e2e_bench.err"
+        timeout -k 10 900 python tools/e2e_bench.py 4 3 > "$OUT/e2e_bench.json" 2> "$OUT/e2e_bench.err"
         rc=$?; cat "$OUT/e2e_bench.json"; tail -3 "$OUT/e2e_bench.err"; ok_or_fail $rc e2e ;;
     probe)
         hipcc --offload-arch=gfx950 -O3 tools/hbm_probe.hip -o "$OUT/hbm_probe" > "$OUT/probe_build.log" 2>&1 &&
