@@ -145,6 +145,22 @@ int fa_sync(fa_ctx* ctx);
 int fa_reduce_device(fa_ctx* ctx, int gpu, const void* const* d_clients, const float* h_weights, int D, size_t n,
                      fa_dtype in, void* d_out, fa_dtype out, fa_mode mode, const float* d_init, void* hip_stream);
 
+/* Compute-node aggregation of an intermediate model part.
+ * A compute node keeps one State per client (systemAPI::init_state_vector,
+ * systemAPI.cpp:3-15; compute_node.cpp), and the paper (EdgeSys 3) aggregates
+ * them, which the reference code never does.  Here every client copy becomes
+ * sum_k w_k x_k, in place: the same ordered fp32 FMA chain as FA_FEDAVG,
+ * rounded once to the slot dtype and written back to all D slots, so each
+ * client continues training from the FedAvg model.  HBM traffic is D*s read +
+ * D*s written per element.
+ * fa_sync_device: raw device pointers, any D >= 1 (ctx needed only for D > 64).
+ * fa_sync_part: the part's own slots on every GPU of the ctx (range shards sync
+ * their ranges); h_weights NULL = the weights given to fa_submit.  Both are
+ * async on hip_stream (NULL = ctx compute stream). */
+int fa_sync_device(fa_ctx* ctx, int gpu, void* const* d_clients, const float* h_weights, int D, size_t n, fa_dtype dt,
+                   void* hip_stream);
+int fa_sync_part(fa_ctx* ctx, int part_id, const float* h_weights, void* hip_stream);
+
 /* Literal mode divisor used by fa_reduce_device when ctx == NULL. */
 #define FA_DEFAULT_DIVISOR 1000.0f
 

@@ -75,6 +75,8 @@ def lib():
         "fa_finalize_gather": (I, [P, I, I, P, P, I]),
         "fa_host_alloc": (I, [S, ctypes.POINTER(P)]),
         "fa_host_free": (I, [P]),
+        "fa_sync_device": (I, [P, I, P, P, I, S, I, P]),
+        "fa_sync_part": (I, [P, I, P, P]),
         "fa_reduce_device": (I, [P, I, P, P, I, S, I, P, I, I, P, P]),
         "fa_fill_uniform": (I, [P, S, I, U64, U32, U64, P]),
         "fa_set_tuning": (I, [ctypes.POINTER(_Tuning)]),
@@ -135,6 +137,17 @@ def reduce_device(clients, weights, n, in_dtype, out, out_dtype=F32, mode=FEDAVG
         raise ValueError("need one weight per client")
     check(lib().fa_reduce_device(ctx.handle if ctx is not None else None, gpu, arr, w.ctypes.data, D, n, in_dtype,
                                  _addr(out), out_dtype, mode, _addr(init), _stream(stream)))
+
+
+def sync_device(clients, weights, n, dtype, stream=None, gpu=0, ctx=None):
+    """fa_sync_device: every device bucket in `clients` := sum_k w_k clients[k] (in place, enqueued)."""
+    D = len(clients)
+    arr = (ctypes.c_void_p * D)(*[_addr(c) for c in clients])
+    w = np.ascontiguousarray(np.asarray(weights, np.float32).reshape(-1))
+    if w.size != D:
+        raise ValueError("need one weight per client")
+    check(lib().fa_sync_device(ctx.handle if ctx is not None else None, gpu, arr, w.ctypes.data, D, n, dtype,
+                               _stream(stream)))
 
 
 def fill_uniform(dst, n, dtype, seed, client, idx0=0, stream=None):
@@ -237,6 +250,15 @@ class Aggregator:
         pieces, ptrs, sizes = _segments(pieces)
         fn = lib().fa_submit_gather_pinned if pinned else lib().fa_submit_gather
         check(fn(self.handle, part_id, slot, len(pieces), ptrs, sizes, float(weight)))
+
+    def sync(self, part_id, weights=None, stream=None):
+        """fa_sync_part: every client slot of the part := the FedAvg of all slots (in place, async)."""
+        wp = None
+        if weights is not None:
+            w = np.ascontiguousarray(np.asarray(weights, np.float32))
+            self._w_keep = w
+            wp = w.ctypes.data
+        check(lib().fa_sync_part(self.handle, part_id, wp, _stream(stream)))
 
     def finalize_gather(self, part_id, pieces, pinned=False):
         """fa_finalize_gather: the reduced bucket scattered over `pieces` (writable host arrays)."""

@@ -265,6 +265,49 @@ int reduce_on(fa_ctx* ctx, int g, const void* const* clients, const float* w, in
     return FA_OK;
 }
 
+// In-place state sync on GPU g: every slot := sum_k w_k slot_k (rounded to dt).  D <= kMaxClients:
+// one fused launch; more: the chain into fp32 scratch, then broadcast launches of kMaxClients slots.
+int sync_on(fa_ctx* ctx, int g, void* const* slots, const float* w, int D, size_t n, fa_dtype dt, hipStream_t s) {
+    if (n == 0) return FA_OK;
+    const size_t si = dsize(dt);
+    const int V = (int)(16 / si);
+    for (int k = 0; k < D; ++k) {
+        if (!slots[k]) return fail(FA_ERR_ARG, "client slot pointer %d is null", k);
+        if (!aligned(slots[k], si)) return fail(FA_ERR_ALIGN, "client slot %d not %zu-byte aligned", k, si);
+    }
+    if (D > fa::kMaxClients) {
+        if (!ctx) return fail(FA_ERR_ARG, "state sync of more than %d slots needs a ctx for scratch", fa::kMaxClients);
+        int rc = ensure_scratch(ctx, g, n * 4);
+        if (rc) return rc;
+        float* acc = static_cast<float*>(ctx->gpu[g].scratch);
+        rc = reduce_on(ctx, g, (const void* const*)slots, w, D, n, dt, acc, FA_F32, FA_FEDAVG, 0.0f, nullptr, s);
+        if (rc) return rc;
+        for (int k0 = 0; k0 < D; k0 += fa::kMaxClients) {
+            fa::ClientTable t;
+            const int nc = std::min(fa::kMaxClients, D - k0);
+            for (int k = 0; k < nc; ++k) {
+                t.src[k] = slots[k0 + k];
+                t.w[k] = 0.0f;
+            }
+            FA_HIP(fa::launch_broadcast(t, nc, dt, acc, (int64_t)n, g_tuning, s));
+        }
+        return FA_OK;
+    }
+    const size_t phase = ((uintptr_t)slots[0] % 16) / si;
+    int64_t head = (int64_t)((V - phase) % V);
+    if ((size_t)head > n) head = (int64_t)n;
+    const int64_t nvec = (int64_t)(n - (size_t)head) / V;
+    bool vec = true;
+    for (int k = 0; k < D; ++k) vec = vec && (((uintptr_t)slots[k] % 16) / si == phase);
+    fa::ClientTable t;
+    for (int k = 0; k < D; ++k) {
+        t.src[k] = slots[k];
+        t.w[k] = w[k];
+    }
+    FA_HIP(fa::launch_sync(t, D, dt, nullptr, head, nvec, (int64_t)n, vec, g_tuning, s));
+    return FA_OK;
+}
+
 int check_part(fa_ctx* ctx, int part_id, Part** out) {
     if (!ctx) return fail(FA_ERR_ARG, "ctx is null");
     auto it = ctx->parts.find(part_id);
@@ -809,6 +852,41 @@ int fa_reduce_device(fa_ctx* ctx, int gpu, const void* const* d_clients, const f
     DeviceGuard dg(dev);
     return reduce_on(ctx, ctx ? gpu : 0, d_clients, h_weights, D, n, in, d_out, out, mode,
                      ctx ? ctx->divisor : FA_DEFAULT_DIVISOR, d_init, s);
+}
+
+int fa_sync_device(fa_ctx* ctx, int gpu, void* const* d_clients, const float* h_weights, int D, size_t n, fa_dtype dt,
+                   void* hip_stream) {
+    g_err.clear();
+    if (!d_clients || !h_weights) return fail(FA_ERR_ARG, "client or weight array is null");
+    if (D < 1) return fail(FA_ERR_ARG, "D must be >= 1");
+    if (!dvalid(dt)) return fail(FA_ERR_ARG, "bad dtype");
+    if (ctx && (gpu < 0 || gpu >= ctx->G)) return fail(FA_ERR_ARG, "gpu %d out of range", gpu);
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    if (!s && ctx) s = ctx->gpu[gpu].compute;
+    if (ctx) {
+        DeviceGuard dg(ctx->gpu[gpu].dev);
+        return sync_on(ctx, gpu, d_clients, h_weights, D, n, dt, s);
+    }
+    return sync_on(nullptr, gpu, d_clients, h_weights, D, n, dt, s);
+}
+
+int fa_sync_part(fa_ctx* ctx, int part_id, const float* h_weights, void* hip_stream) {
+    g_err.clear();
+    Part* p;
+    int rc = check_part(ctx, part_id, &p);
+    if (rc) return rc;
+    if (p->mode != FA_FEDAVG) return fail(FA_ERR_ARG, "part %d is not a FedAvg part", part_id);
+    if (hip_stream && ctx->G != 1) return fail(FA_ERR_ARG, "an explicit stream needs a single-GPU ctx");
+    const float* w = h_weights ? h_weights : p->w.data();
+    std::vector<void*> ptrs(p->D);
+    for (int g = 0; g < ctx->G; ++g) {
+        GpuRes& r = ctx->gpu[g];
+        DeviceGuard dg(r.dev);
+        for (int k = 0; k < p->D; ++k) ptrs[k] = slot_ptr(*p, g, k);
+        hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : r.compute;
+        if ((rc = sync_on(ctx, g, ptrs.data(), w, p->D, p->cnt[g], p->in, st))) return rc;
+    }
+    return FA_OK;
 }
 
 int fa_fill_uniform(void* d_dst, size_t n, fa_dtype dt, uint64_t seed, uint32_t client, uint64_t idx0,

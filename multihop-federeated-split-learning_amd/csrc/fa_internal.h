@@ -28,6 +28,12 @@ hipError_t launch_chain(const ClientTable& t, int nc, fa_dtype in, fa_dtype out,
                         int64_t head, int64_t nvec, int64_t n, bool vector_ok, const Tuning& tu, hipStream_t s);
 hipError_t launch_literal(const void* x, fa_dtype in, void* dst, fa_dtype out, float divisor, int64_t head,
                           int64_t nvec, int64_t n, bool vector_ok, const Tuning& tu, hipStream_t s);
+// In-place state sync: every slot t.src[0..nc) := the chain over them (continuing `init` if given).
+hipError_t launch_sync(const ClientTable& t, int nc, fa_dtype dt, const float* init, int64_t head, int64_t nvec,
+                       int64_t n, bool vector_ok, const Tuning& tu, hipStream_t s);
+// slots t.src[0..nc) := acc (rounded to dt).
+hipError_t launch_broadcast(const ClientTable& t, int nc, fa_dtype dt, const float* acc, int64_t n,
+                            const Tuning& tu, hipStream_t s);
 hipError_t launch_fill(void* dst, int64_t n, fa_dtype dt, uint64_t seed, uint32_t client, uint64_t idx0,
                        hipStream_t s);
 

@@ -199,6 +199,94 @@ __global__ __launch_bounds__(256) void fedavg_chain_scalar_kernel(const ClientTa
     }
 }
 
+// ---------------------------------------------------------------- state sync (compute nodes)
+//
+// Compute-node aggregation of an intermediate model part: a compute node keeps
+// one State per client (systemAPI::init_state_vector, systemAPI.cpp:3-15); after a round every
+// client's copy becomes the FedAvg of all copies.  In place: a lane reads its 16-byte vector of all
+// nc client slots, runs the same ordered FMA chain, and writes the rounded result back to every
+// slot (all reads of a vector precede its writes, so aliasing input and output is safe).
+// Per element: nc*s reads + nc*s writes.
+
+template <typename T, bool INIT>
+__device__ __forceinline__ void sync_scalar_edges(const ClientTable& t, int nc, const float* init, int64_t head,
+                                                  int64_t tail0, int64_t n) {
+    if (blockIdx.x != 0) return;
+    const int64_t n_tail = n - tail0;
+    for (int64_t s = threadIdx.x; s < head + n_tail; s += blockDim.x) {
+        const int64_t i = s < head ? s : tail0 + (s - head);
+        float acc = INIT ? init[i] : 0.0f;
+        for (int k = 0; k < nc; ++k) acc = __builtin_fmaf(In<T>::scalar(t.src[k], i), t.w[k], acc);
+        for (int k = 0; k < nc; ++k) Out<T>::scalar(const_cast<void*>(t.src[k]), i, acc);
+    }
+}
+
+template <typename T, int U, int SP, bool INIT>
+__global__ __launch_bounds__(256) void fedavg_sync_kernel(const ClientTable t, int nc, const float* init,
+                                                          int64_t head, int64_t nvec, int64_t n) {
+    constexpr int V = In<T>::kVec;
+    sync_scalar_edges<T, INIT>(t, nc, init, head, head + nvec * V, n);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+        const int64_t e = head + v * V;
+        float acc[V];
+        if constexpr (INIT) {
+#pragma unroll
+            for (int j = 0; j < V; j += 4) {
+                u32x4 r = ld16<true>(init + e + j);
+                acc[j] = __uint_as_float(r.x); acc[j + 1] = __uint_as_float(r.y);
+                acc[j + 2] = __uint_as_float(r.z); acc[j + 3] = __uint_as_float(r.w);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < V; ++j) acc[j] = 0.0f;
+        }
+        int k = 0;
+        for (; k + U <= nc; k += U) {
+            u32x4 raw[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) raw[u] = ld16<true>(reinterpret_cast<const T*>(t.src[k + u]) + e);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                float x[V];
+                In<T>::widen(raw[u], x);
+                const float w = t.w[k + u];
+#pragma unroll
+                for (int j = 0; j < V; ++j) acc[j] = __builtin_fmaf(x[j], w, acc[j]);
+            }
+        }
+        for (; k < nc; ++k) {
+            float x[V];
+            In<T>::widen(ld16<true>(reinterpret_cast<const T*>(t.src[k]) + e), x);
+            const float w = t.w[k];
+#pragma unroll
+            for (int j = 0; j < V; ++j) acc[j] = __builtin_fmaf(x[j], w, acc[j]);
+        }
+        for (int k2 = 0; k2 < nc; ++k2) Out<T>::template store<V, SP>(const_cast<void*>(t.src[k2]), e, acc);
+    }
+}
+
+template <typename T, bool INIT>
+__global__ __launch_bounds__(256) void fedavg_sync_scalar_kernel(const ClientTable t, int nc, const float* init,
+                                                                 int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        float acc = INIT ? init[i] : 0.0f;
+        for (int k = 0; k < nc; ++k) acc = __builtin_fmaf(In<T>::scalar(t.src[k], i), t.w[k], acc);
+        for (int k = 0; k < nc; ++k) Out<T>::scalar(const_cast<void*>(t.src[k]), i, acc);
+    }
+}
+
+// More than kMaxClients slots: the chain ran into an fp32 accumulator; write it (rounded) to nc slots.
+template <typename T>
+__global__ __launch_bounds__(256) void broadcast_kernel(const ClientTable t, int nc, const float* acc, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const float a = acc[i];
+        for (int k = 0; k < nc; ++k) Out<T>::scalar(const_cast<void*>(t.src[k]), i, a);
+    }
+}
+
 // ---------------------------------------------------------------- literal mode
 
 template <typename IN, typename OUT, bool LNT, int SP>
@@ -354,6 +442,58 @@ hipError_t launch_literal(const void* x, fa_dtype in, void* out, fa_dtype outdt,
     if (in == FA_BF16 && outdt == FA_F32)
         return launch_literal_t<uint16_t, float>(x, out, divisor, head, nvec, n, vector_ok, tu, s);
     return launch_literal_t<uint16_t, uint16_t>(x, out, divisor, head, nvec, n, vector_ok, tu, s);
+}
+
+namespace {
+template <typename T, int SP>
+hipError_t launch_sync_sp(const ClientTable& t, int nc, const float* init, int64_t head, int64_t nvec, int64_t n,
+                          const Tuning& tu, hipStream_t s) {
+    const int64_t g = grid_for(nvec > 0 ? nvec : 1, tu);
+    if (init)
+        hipLaunchKernelGGL((fedavg_sync_kernel<T, 8, SP, true>), dim3((unsigned)g), dim3(tu.block), 0, s, t, nc, init,
+                           head, nvec, n);
+    else
+        hipLaunchKernelGGL((fedavg_sync_kernel<T, 8, SP, false>), dim3((unsigned)g), dim3(tu.block), 0, s, t, nc,
+                           init, head, nvec, n);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_sync_t(const ClientTable& t, int nc, const float* init, int64_t head, int64_t nvec, int64_t n,
+                         bool vector_ok, const Tuning& tu, hipStream_t s) {
+    if (!vector_ok) {
+        const int64_t g = grid_for(n, tu);
+        if (init)
+            hipLaunchKernelGGL((fedavg_sync_scalar_kernel<T, true>), dim3((unsigned)g), dim3(tu.block), 0, s, t, nc,
+                               init, n);
+        else
+            hipLaunchKernelGGL((fedavg_sync_scalar_kernel<T, false>), dim3((unsigned)g), dim3(tu.block), 0, s, t, nc,
+                               init, n);
+        return hipGetLastError();
+    }
+    switch (tu.store_policy) {
+        case kStNt: return launch_sync_sp<T, kStNt>(t, nc, init, head, nvec, n, tu, s);
+        case kStSc1: return launch_sync_sp<T, kStSc1>(t, nc, init, head, nvec, n, tu, s);
+        case kStSc01: return launch_sync_sp<T, kStSc01>(t, nc, init, head, nvec, n, tu, s);
+        default: return launch_sync_sp<T, kStPlain>(t, nc, init, head, nvec, n, tu, s);
+    }
+}
+}  // namespace
+
+hipError_t launch_sync(const ClientTable& t, int nc, fa_dtype dt, const float* init, int64_t head, int64_t nvec,
+                       int64_t n, bool vector_ok, const Tuning& tu, hipStream_t s) {
+    if (dt == FA_F32) return launch_sync_t<float>(t, nc, init, head, nvec, n, vector_ok, tu, s);
+    return launch_sync_t<uint16_t>(t, nc, init, head, nvec, n, vector_ok, tu, s);
+}
+
+hipError_t launch_broadcast(const ClientTable& t, int nc, fa_dtype dt, const float* acc, int64_t n,
+                            const Tuning& tu, hipStream_t s) {
+    const int64_t g = grid_for(n, tu);
+    if (dt == FA_F32)
+        hipLaunchKernelGGL((broadcast_kernel<float>), dim3((unsigned)g), dim3(tu.block), 0, s, t, nc, acc, n);
+    else
+        hipLaunchKernelGGL((broadcast_kernel<uint16_t>), dim3((unsigned)g), dim3(tu.block), 0, s, t, nc, acc, n);
+    return hipGetLastError();
 }
 
 hipError_t launch_fill(void* dst, int64_t n, fa_dtype dt, uint64_t seed, uint32_t client, uint64_t idx0,
