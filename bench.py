@@ -170,6 +170,17 @@ class Setup:
         return self.D * self.n * self.s_in
 
 
+class SyncSetup(Setup):
+    """Compute-node state sync (fa_sync_part): every client slot := the FedAvg of all, in place.
+    Algorithmic bytes per launch = D*n*s read + D*n*s written."""
+
+    def launch(self, step, stream):
+        self.agg.sync(step % self.nsets, self.w, stream=stream)
+
+    def algo_bytes(self):
+        return 2 * self.D * self.n * self.s_in
+
+
 def timed_loop(torch, setup, steps, warmup, stream, dist, barrier):
     for i in range(warmup):
         setup.launch(i, stream)
@@ -343,6 +354,19 @@ def main():
                          "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          "input_sets_rotated": s.nsets}
             s.close()
+        # compute-node aggregation on the C2 shape: 8 client copies synced in place
+        sD, sn, si, so, _ = WORKLOADS["c2"]
+        s = SyncSetup(fa, torch, sD, sn, si, so, 0, device)
+        torch.cuda.synchronize()
+        w2, km = timed_loop(torch, s, max(10, args.steps), 3, stream, dist, barrier)
+        ka = statistics.mean(km)
+        sec["sync_c2"] = {"description": "compute-node state sync, 8 client copies of the ResNet-18 buckets, fp32, "
+                                         "in place (D reads + D writes per element)",
+                          "kernel_ms_avg": round(ka, 4),
+                          "achieved_GBs": round(s.algo_bytes() / (ka * 1e-3) / 1e9, 1),
+                          "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                          "input_sets_rotated": s.nsets}
+        s.close()
         line["secondary"] = sec
 
     if rank == 0:
