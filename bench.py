@@ -175,7 +175,7 @@ class SyncSetup(Setup):
     Algorithmic bytes per launch = D*n*s read + D*n*s written."""
 
     def launch(self, step, stream):
-        self.agg.sync(step % self.nsets, self.w, stream=stream)
+        self.agg.sync_states(step % self.nsets, self.w, stream=stream)
 
     def algo_bytes(self):
         return 2 * self.D * self.n * self.s_in

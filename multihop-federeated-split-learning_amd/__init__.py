@@ -251,7 +251,7 @@ class Aggregator:
         fn = lib().fa_submit_gather_pinned if pinned else lib().fa_submit_gather
         check(fn(self.handle, part_id, slot, len(pieces), ptrs, sizes, float(weight)))
 
-    def sync(self, part_id, weights=None, stream=None):
+    def sync_states(self, part_id, weights=None, stream=None):
         """fa_sync_part: every client slot of the part := the FedAvg of all slots (in place, async)."""
         wp = None
         if weights is not None:

@@ -353,9 +353,11 @@ void NetLayer::sender_loop(int i) {
 void NetLayer::send(int dest, std::shared_ptr<const Bytes> framed, bool keep_open) {
     {
         std::lock_guard<std::mutex> lk(m_tx_);
-        // one sender per destination keeps that destination's frames in order
-        const size_t k = (size_t)(dest + 1024) % senders_.size();
-        senders_[k]->q.push_back({dest, std::move(framed), keep_open});
+        // one sender per destination keeps that destination's frames in order; destinations are dealt
+        // to the senders round-robin at first use, so a fan-out to S destinations uses S senders
+        auto it = sender_of_.find(dest);
+        if (it == sender_of_.end()) it = sender_of_.insert({dest, (int)(sender_of_.size() % senders_.size())}).first;
+        senders_[(size_t)it->second]->q.push_back({dest, std::move(framed), keep_open});
     }
     cv_tx_.notify_all();
 }

@@ -65,7 +65,7 @@ struct Receipt {  // Task.h:30-51, the fields the aggregation path uses
 
 class NetLayer {
 public:
-    NetLayer(int my_id, RoutingTable routes, int senders = 4)
+    NetLayer(int my_id, RoutingTable routes, int senders = 8)
         : my_id_(my_id), routes_(std::move(routes)), n_senders_(senders < 1 ? 1 : senders) {}
     ~NetLayer();
 
@@ -140,6 +140,7 @@ private:
     std::mutex m_tx_;
     std::condition_variable cv_tx_, cv_tx_idle_;
     std::vector<std::unique_ptr<Sender>> senders_;
+    std::map<int, int> sender_of_;  // destination -> sender index (under m_tx_)
     std::mutex m_routes_;  // routes_ is updated by readers (refactor) and read by senders
 };
 

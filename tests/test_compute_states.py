@@ -138,7 +138,7 @@ def test_sync_part_on_context_slots(fa, O, torch_gpu):
         for k in range(D):
             agg.submit(5, k, xs[k], w[k])
         fa.check(fa.lib().fa_sync(agg.handle))
-        agg.sync(5)
+        agg.sync_states(5)
         fa.check(fa.lib().fa_sync(agg.handle))
         for g in range(gpus):
             for k in range(D):
@@ -146,7 +146,7 @@ def test_sync_part_on_context_slots(fa, O, torch_gpu):
                 got = _read_device(torch, ptr, cnt, "cuda:%d" % agg.devices[g])
                 assert np.array_equal(got.view(np.uint32), want[off:off + cnt].view(np.uint32))
         with pytest.raises(fa.FaError):
-            agg.sync(99)
+            agg.sync_states(99)
 
 
 @pytest.mark.gpu

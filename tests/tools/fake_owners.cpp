@@ -111,6 +111,11 @@ int main(int argc, char** argv) {
     // data owner ids: the init node 0 and the ids the aggregator replies to (aggregator.cpp:103-105)
     std::vector<int> ids = {0};
     for (int i = 0; i < D - 1; ++i) ids.push_back(i + C + 1);
+    // frame buffers recycled across rounds (the owners' side of a loopback run should not page-fault
+    // hundreds of MB per round; separate machines in a real deployment)
+    auto pool = BufferPool::create([](size_t n) { return (char*)std::malloc(n); }, [](char* p) { std::free(p); },
+                                   false);
+    set_frame_allocator([pool](size_t n) { return pool->get(n); });
     RoutingTable routes(port_base);
     std::map<int, std::unique_ptr<NetLayer>> listeners;  // port -> listener
     for (int id : ids) {
