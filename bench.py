@@ -216,7 +216,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="northstar", choices=sorted(WORKLOADS))
     ap.add_argument("--layout", default="range", choices=["range", "rs", "chain"])
-    ap.add_argument("--chunks", type=int, default=16, help="chain layout: pipeline chunks")
+    ap.add_argument("--chunks", type=int, default=16,
+                    help="rs / chain layouts: chunks (reduce of chunk c+1 overlaps the exchange of chunk c)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL over xGMI) or gloo (rehearsal only)")
@@ -282,8 +283,8 @@ def main():
         def step():
             with torch.cuda.stream(stream):
                 if args.layout == "rs":
-                    return shard.reduce_rs(reducer, dist, cl, setup.w, n, dev) if world > 1 else reducer(
-                        cl, setup.w, n)
+                    return shard.reduce_rs(reducer, dist, cl, setup.w, n, dev, chunks=args.chunks,
+                                           itemsize=setup.s_in) if world > 1 else reducer(cl, setup.w, n)
                 return shard.reduce_chain(reducer, dist, cl, setup.w, n, dev, chunks=args.chunks,
                                           itemsize=setup.s_in) if world > 1 else reducer(cl, setup.w, n)
         for _ in range(args.warmup):
@@ -299,7 +300,8 @@ def main():
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
         layout_desc = ("client-sharded: each rank reduces its %d whole clients into fp32 partials, RCCL "
-                       "reduce-scatter over xGMI" % D if args.layout == "rs" else
+                       "reduce-scatter over xGMI in %d chunks overlapped with the reduction" % (D, args.chunks)
+                       if args.layout == "rs" else
                        "client-sharded, bit-exact: the fp32 chain is handed rank to rank over RCCL p2p in %d "
                        "chunks, last rank scatters the ranges" % args.chunks)
     units_bytes = setup.input_bytes() * world

@@ -57,22 +57,45 @@ def reduce_range(reduce, clients, weights, lo, hi):
     return reduce(clients, weights, hi - lo)
 
 
-def reduce_rs(reduce, dist, clients, weights, n, device):
+def reduce_rs(reduce, dist, clients, weights, n, device, chunks=1, itemsize=4):
     """Client-sharded partial + reduce-scatter; returns this rank's [lo, hi) of the sum.
 
     `n` must be a multiple of world * UNIT (pad the bucket) so that reduce-scatter
-    shards are equal and line up with range_bounds.
+    shards are equal and line up with range_bounds.  With chunks > 1 the ranges are
+    cut into chunks: chunk c of EVERY rank's range is reduced into one contiguous
+    buffer (one launch per rank range) and reduce-scattered asynchronously while
+    chunk c+1 is reduced, so the RCCL transfer over xGMI overlaps the HBM-bound
+    local reduction (~G*min(1, D/39) instead of G*D/(D+39)).
+    `clients` are tensors or raw device addresses (itemsize bytes per element).
     """
     import torch
     world, rank = dist.get_world_size(), dist.get_rank()
     assert n % (world * UNIT) == 0, "pad the bucket to a multiple of world * %d" % UNIT
-    if clients:
-        partial = reduce(clients, weights, n)
-    else:  # a rank without clients contributes zeros
-        partial = torch.zeros(n, dtype=torch.float32, device=device)
+    per = n // world
     lo, hi = range_bounds(n, world, rank)
-    shard = torch.empty(hi - lo, dtype=torch.float32, device=device)
-    dist.reduce_scatter_tensor(shard, partial, op=dist.ReduceOp.SUM)
+    assert (lo, hi) == (rank * per, (rank + 1) * per)
+    shard = torch.empty(per, dtype=torch.float32, device=device)
+    edges = sorted({min(per, (per * c // chunks) // UNIT * UNIT) for c in range(max(1, chunks))} | {per})
+    q_max = max(b - a for a, b in zip(edges, edges[1:]))
+    bufs = [torch.empty(world * q_max, dtype=torch.float32, device=device) for _ in range(min(2, len(edges) - 1))]
+    pending = [None] * len(bufs)
+    for c, (a, b) in enumerate(zip(edges, edges[1:])):
+        q = b - a
+        i = c % len(bufs)
+        if pending[i] is not None:  # the buffer's previous reduce-scatter must be done before it is refilled
+            pending[i].wait()
+        buf = bufs[i][:world * q]
+        for r in range(world):
+            out = buf[r * q:(r + 1) * q]
+            if clients:
+                o0 = r * per + a
+                reduce([_piece(x, o0, o0 + q, itemsize) for x in clients], weights, q, out=out)
+            else:  # a rank without clients contributes zeros
+                out.zero_()
+        pending[i] = dist.reduce_scatter_tensor(shard[a:b], buf, op=dist.ReduceOp.SUM, async_op=True)
+    for p in pending:
+        if p is not None:
+            p.wait()
     return shard
 
 

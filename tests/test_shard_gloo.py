@@ -37,10 +37,14 @@ def worker(rank, world, port, n, D, seed, q):
         w = O.weights(D)
         dev = torch.device("cpu")
 
-        def reducer(clients, weights, m, init=None):
+        def reducer(clients, weights, m, init=None, out=None):
             xs = [c.numpy() for c in clients]
-            return torch.from_numpy(O.fedavg(xs, np.asarray(weights, np.float32),
-                                             init=None if init is None else init.numpy()))
+            r = torch.from_numpy(O.fedavg(xs, np.asarray(weights, np.float32),
+                                          init=None if init is None else init.numpy()))
+            if out is None:
+                return r
+            out.copy_(r)
+            return out
         res = {}
         # range: this rank's slice of every client bucket
         lo, hi = shard.range_bounds(n, world, rank)
@@ -53,6 +57,7 @@ def worker(rank, world, port, n, D, seed, q):
         npad = -(-n // (world * shard.UNIT)) * world * shard.UNIT
         mine_p = [torch.nn.functional.pad(x, (0, npad - n)) for x in mine]
         res["rs"] = shard.reduce_rs(reducer, dist, mine_p, w[c0:c1], npad, dev).numpy()
+        res["rs_chunked"] = shard.reduce_rs(reducer, dist, mine_p, w[c0:c1], npad, dev, chunks=3).numpy()
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -89,10 +94,11 @@ def test_layouts_match_single_gpu_chain(O, world, n, D):
         assert got.size == n
         assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), layout
     # rs changes the summation order: within 1e-6 of sum_k |w_k x_k|
-    got = np.concatenate([out[r]["rs"] for r in range(world)])[:n]
     absw = sum(abs(np.float64(wk)) * np.abs(x.astype(np.float64)) for wk, x in zip(w, xs))
-    ok, worst = shard.tolerance_ok(got, ref, absw)
-    assert ok, worst
+    for layout in ("rs", "rs_chunked"):  # chunked: reduce of chunk c+1 overlaps the reduce-scatter of chunk c
+        got = np.concatenate([out[r][layout] for r in range(world)])[:n]
+        ok, worst = shard.tolerance_ok(got, ref, absw)
+        assert ok, (layout, worst)
 
 
 def test_bounds_cover_and_align():
