@@ -54,6 +54,11 @@ for s in $STEPS; do
         timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
             --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2 --dist-backend gloo > "$OUT/bench_2ranks.json" 2> "$OUT/bench_2ranks.err"
         rc=$?; cat "$OUT/bench_2ranks.json"; tail -3 "$OUT/bench_2ranks.err"; ok_or_fail $rc ranks ;;
+    vmm)  # physical placement of the client pool via the VMM API (tools/exp_vmm.hip)
+        hipcc --offload-arch=gfx950 -O2 tools/exp_vmm.hip -Iinclude -Lmultihop-federeated-split-learning_amd/lib -lfa \
+            -Wl,-rpath,$PWD/multihop-federeated-split-learning_amd/lib -o "$OUT/exp_vmm" > "$OUT/vmm_build.log" 2>&1 &&
+        timeout -k 10 400 "$OUT/exp_vmm" ${VMM_ARGS:-26 3} > "$OUT/exp_vmm.jsonl" 2> "$OUT/exp_vmm.err"
+        rc=$?; cat "$OUT/exp_vmm.jsonl"; tail -3 "$OUT/exp_vmm.err"; ok_or_fail $rc vmm ;;
     e2e)
         timeout -k 10 900 python tools/e2e_bench.py 4 3 > "$OUT/e2e_bench.json" 2> "$OUT/e2e_bench.err"
         rc=$?; cat "$OUT/e2e_bench.json"; tail -3 "$OUT/e2e_bench.err"; ok_or_fail $rc e2e ;;
