@@ -59,6 +59,11 @@ for s in $STEPS; do
             -Wl,-rpath,$PWD/multihop-federeated-split-learning_amd/lib -o "$OUT/exp_vmm" > "$OUT/vmm_build.log" 2>&1 &&
         timeout -k 10 400 "$OUT/exp_vmm" ${VMM_ARGS:-26 3} > "$OUT/exp_vmm.jsonl" 2> "$OUT/exp_vmm.err"
         rc=$?; cat "$OUT/exp_vmm.jsonl"; tail -3 "$OUT/exp_vmm.err"; ok_or_fail $rc vmm ;;
+    outplace)  # where the output is written (tools/exp_out.hip)
+        hipcc --offload-arch=gfx950 -O2 tools/exp_out.hip -Iinclude -Lmultihop-federeated-split-learning_amd/lib -lfa \
+            -Wl,-rpath,$PWD/multihop-federeated-split-learning_amd/lib -o "$OUT/exp_out" > "$OUT/out_build.log" 2>&1 &&
+        timeout -k 10 400 "$OUT/exp_out" ${OUT_ARGS:-26 4} > "$OUT/exp_out.jsonl" 2> "$OUT/exp_out.err"
+        rc=$?; cat "$OUT/exp_out.jsonl"; tail -3 "$OUT/exp_out.err"; ok_or_fail $rc outplace ;;
     e2e)
         timeout -k 10 900 python tools/e2e_bench.py 4 3 > "$OUT/e2e_bench.json" 2> "$OUT/e2e_bench.err"
         rc=$?; cat "$OUT/e2e_bench.json"; tail -3 "$OUT/e2e_bench.err"; ok_or_fail $rc e2e ;;
