@@ -139,6 +139,8 @@ class Setup:
                 # global client id and element offset: ranks hold disjoint clients or slices of one bucket
                 fa.fill_uniform(ptr, cnt, self.in_dt, seed + s, client0 + k, idx0=elem0)
         self.w = self._weights(D)
+        # pool placement chosen by fa_bucket_define (probe times of the candidates)
+        self.placement = [self.agg.placement(s, 0) for s in range(self.nsets)]
 
     @staticmethod
     def _weights(D):
@@ -331,7 +333,8 @@ def main():
                    "clients": D * (world if args.layout != "range" else 1),
                    "elems_per_client": n * (world if args.layout == "range" else 1), "in_dtype": in_dt,
                    "out_dtype": out_dt, "layout": layout_desc, "parallelism": "%s%d" % (args.layout, world),
-                   "tuning": fa.get_tuning(), "input_sets_rotated": setup.nsets},
+                   "tuning": fa.get_tuning(), "input_sets_rotated": setup.nsets,
+                   "placement": setup.placement},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,

@@ -129,6 +129,9 @@ int fa_reduce_part(fa_ctx* ctx, int part_id, const float* h_weights, void* hip_s
 int fa_bucket_slot(fa_ctx* ctx, int part_id, int gpu, int client_slot, void** d_ptr, size_t* n_elems,
                    size_t* elem_offset);
 int fa_bucket_output(fa_ctx* ctx, int part_id, int gpu, void** d_ptr);
+/* Placement probe record of a bucket pool on GPU `gpu`: how many candidates were timed (0 = not
+ * probed), their probe times in ms (probe_ms: room for 8), and the index of the one kept. */
+int fa_bucket_placement(fa_ctx* ctx, int part_id, int gpu, int* n_probes, float* probe_ms, int* chosen);
 /* D2H of the part's current device output (after fa_reduce_part), waiting for it. */
 int fa_copy_output(fa_ctx* ctx, int part_id, void* host_dst);
 /* Wait for all copy and compute work of the ctx. */
@@ -179,6 +182,8 @@ typedef struct {
     int store_policy; /* output stores: 1 plain, 2 nt, 3 sc1 (write-through), 4 sc0 sc1 */
     int slot_skew;    /* bytes between consecutive client slots beyond 4 KiB alignment (multiple of 16);
                          -1 = none; applies to buckets defined afterwards */
+    int placement_probes; /* FedAvg bucket pools >= 1 GiB: at most this many candidate allocations are
+                             timed and the fastest kept; -1 = 1 (no probing); default 4 */
 } fa_tuning;
 int fa_set_tuning(const fa_tuning* t);
 int fa_get_tuning(fa_tuning* t);

@@ -34,7 +34,8 @@ class FaError(RuntimeError):
 
 class _Tuning(ctypes.Structure):
     _fields_ = [("block", ctypes.c_int), ("max_blocks", ctypes.c_int), ("unroll", ctypes.c_int),
-                ("load_policy", ctypes.c_int), ("store_policy", ctypes.c_int), ("slot_skew", ctypes.c_int)]
+                ("load_policy", ctypes.c_int), ("store_policy", ctypes.c_int), ("slot_skew", ctypes.c_int),
+                ("placement_probes", ctypes.c_int)]
 
 
 def build():
@@ -77,6 +78,7 @@ def lib():
         "fa_host_free": (I, [P]),
         "fa_sync_device": (I, [P, I, P, P, I, S, I, P]),
         "fa_sync_part": (I, [P, I, P, P]),
+        "fa_bucket_placement": (I, [P, I, I, ctypes.POINTER(I), ctypes.POINTER(F), ctypes.POINTER(I)]),
         "fa_reduce_device": (I, [P, I, P, P, I, S, I, P, I, I, P, P]),
         "fa_fill_uniform": (I, [P, S, I, U64, U32, U64, P]),
         "fa_set_tuning": (I, [ctypes.POINTER(_Tuning)]),
@@ -158,16 +160,17 @@ def get_tuning():
     t = _Tuning()
     check(lib().fa_get_tuning(ctypes.byref(t)))
     return {"block": t.block, "max_blocks": t.max_blocks, "unroll": t.unroll, "load_policy": t.load_policy,
-            "store_policy": t.store_policy, "slot_skew": t.slot_skew}
+            "store_policy": t.store_policy, "slot_skew": t.slot_skew, "placement_probes": t.placement_probes}
 
 
 LOAD_DEFAULT, LOAD_NT = 1, 2
 STORE_PLAIN, STORE_NT, STORE_SC1, STORE_SC01 = 1, 2, 3, 4
 
 
-def set_tuning(block=0, max_blocks=0, unroll=0, load_policy=0, store_policy=0, slot_skew=0):
-    """fa_set_tuning; every argument 0 = keep.  max_blocks -1 = one-shot grid, slot_skew -1 = none."""
-    t = _Tuning(block, max_blocks, unroll, load_policy, store_policy, slot_skew)
+def set_tuning(block=0, max_blocks=0, unroll=0, load_policy=0, store_policy=0, slot_skew=0, placement_probes=0):
+    """fa_set_tuning; every argument 0 = keep.  max_blocks -1 = one-shot grid, slot_skew -1 = none,
+    placement_probes -1 = no probing."""
+    t = _Tuning(block, max_blocks, unroll, load_policy, store_policy, slot_skew, placement_probes)
     check(lib().fa_set_tuning(ctypes.byref(t)))
 
 
@@ -283,6 +286,13 @@ class Aggregator:
         check(lib().fa_bucket_slot(self.handle, part_id, gpu, client_slot, ctypes.byref(ptr), ctypes.byref(n),
                                    ctypes.byref(off)))
         return ptr.value, n.value, off.value
+
+    def placement(self, part_id, gpu=0):
+        """fa_bucket_placement: {"probe_ms": [...], "chosen": i} ({"probe_ms": []} when not probed)."""
+        n, ch = ctypes.c_int(), ctypes.c_int()
+        ms = (ctypes.c_float * 8)()
+        check(lib().fa_bucket_placement(self.handle, part_id, gpu, ctypes.byref(n), ms, ctypes.byref(ch)))
+        return {"probe_ms": [round(ms[i], 4) for i in range(n.value)], "chosen": ch.value}
 
     def output(self, part_id, gpu=0):
         ptr = ctypes.c_void_p()

@@ -40,6 +40,11 @@ thread_local std::string g_err;
 fa::Tuning g_tuning{128, 0, 16, 1, 2};
 // Byte skew between consecutive client slots of one bucket (see slot_stride).
 size_t g_slot_skew = 512;
+// Placement probing of large FedAvg bucket pools (see alloc_placed): at most this many candidates.
+int g_placement_probes = 4;
+constexpr size_t kProbeMinBytes = 1ull << 30;  // smaller pools: one allocation, no probe
+constexpr double kFastGBs = 0.83 * 8000.0;     // a candidate at >= 83% of the 8 TB/s spec is kept at once
+constexpr int kMaxProbeRecord = 8;
 
 int fail(int code, const char* fmt, ...) {
     char buf[512];
@@ -97,6 +102,8 @@ struct Part {
     std::vector<char*> slots;      // per GPU: == pool (slot k at pool + k * stride)
     std::vector<void*> dout;       // per GPU: pool + D * stride
     std::vector<float> w;
+    std::vector<std::vector<float>> probe_ms;  // per GPU: probe time of each placement candidate
+    std::vector<int> chosen;                   // per GPU: the candidate kept
     std::vector<char> submitted;
     int n_submitted = 0;
     int last_slot = -1;
@@ -305,6 +312,79 @@ int sync_on(fa_ctx* ctx, int g, void* const* slots, const float* w, int D, size_
         t.w[k] = w[k];
     }
     FA_HIP(fa::launch_sync(t, D, dt, nullptr, head, nvec, (int64_t)n, vec, g_tuning, s));
+    return FA_OK;
+}
+
+// Placement of a bucket pool.  The same reduction over the same layout runs at two speeds depending
+// on which physical HBM a large allocation receives: 1.29-1.30 ms vs 1.41-1.42 ms for 32 x 256 MiB
+// (tools/exp_pick.hip: of 8 pools allocated in sequence, 6 fast and 2 slow, each stable over
+// interleaved rounds; physically contiguous pools and 2 MiB-granule VMM pools in any mapping order
+// were slow, tools/exp_vmm.hip; the output's placement does not matter, tools/exp_out.hip).  So a
+// large FedAvg pool is chosen by measurement: allocate a candidate, time the part's own reduction
+// over it (uninitialized contents: the timing does not depend on the values), keep it if it reaches
+// kFastGBs, else keep it allocated (so the next candidate lands elsewhere) and try another, up to
+// g_placement_probes candidates; the fastest is kept and the others are freed.
+int probe_pool(fa_ctx* ctx, int g, const Part& p, size_t stride, char* pool, float* ms_out) {
+    GpuRes& r = ctx->gpu[(size_t)g];
+    const size_t n = p.cnt[(size_t)g];
+    std::vector<const void*> cl((size_t)p.D);
+    for (int k = 0; k < p.D; ++k) cl[(size_t)k] = pool + (size_t)k * stride;
+    std::vector<float> w((size_t)p.D, 1.0f / (float)p.D);
+    void* out = pool + (size_t)p.D * stride;
+    hipEvent_t a, b;
+    FA_HIP(hipEventCreate(&a));
+    FA_HIP(hipEventCreate(&b));
+    float best = 1e30f;
+    int rc = FA_OK;
+    for (int it = 0; it < 4 && rc == FA_OK; ++it) {
+        FA_HIP(hipEventRecord(a, r.compute));
+        rc = reduce_on(ctx, g, cl.data(), w.data(), p.D, n, p.in, out, p.out, FA_FEDAVG, 1.0f, nullptr, r.compute);
+        FA_HIP(hipEventRecord(b, r.compute));
+        FA_HIP(hipEventSynchronize(b));
+        float t = 0;
+        FA_HIP(hipEventElapsedTime(&t, a, b));
+        if (it > 0) best = std::min(best, t);  // first launch warms up
+    }
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    *ms_out = best;
+    return rc;
+}
+
+int alloc_placed(fa_ctx* ctx, int g, Part& p, size_t stride, size_t bytes, char** out) {
+    const size_t algo = (size_t)p.D * p.cnt[(size_t)g] * dsize(p.in) + p.cnt[(size_t)g] * dsize(p.out);
+    const int probes = (p.mode == FA_FEDAVG && bytes >= kProbeMinBytes && p.cnt[(size_t)g] > 0)
+                           ? std::max(1, g_placement_probes) : 1;
+    std::vector<char*> cand;
+    std::vector<float>& ms = p.probe_ms[(size_t)g];
+    int best = -1, rc = FA_OK;
+    for (int i = 0; i < probes; ++i) {
+        char* c = nullptr;
+        if (hipMalloc((void**)&c, bytes) != hipSuccess) {  // out of memory for another candidate: stop
+            (void)hipGetLastError();
+            break;
+        }
+        cand.push_back(c);
+        if (probes == 1) {
+            best = 0;
+            break;
+        }
+        float t = 0;
+        if ((rc = probe_pool(ctx, g, p, stride, c, &t))) break;
+        if (ms.size() < (size_t)kMaxProbeRecord) ms.push_back(t);
+        if (best < 0 || t < ms[(size_t)best]) best = i;
+        if ((double)algo / (t * 1e-3) / 1e9 >= kFastGBs) break;
+    }
+    if (cand.empty()) return fail(FA_ERR_NOMEM, "device alloc of %zu B failed on GPU %d", bytes, g);
+    if (best < 0) best = 0;
+    for (size_t i = 0; i < cand.size(); ++i)
+        if ((int)i != best) (void)hipFree(cand[i]);
+    if (rc) {
+        (void)hipFree(cand[(size_t)best]);
+        return rc;
+    }
+    p.chosen[(size_t)g] = best;
+    *out = cand[(size_t)best];
     return FA_OK;
 }
 
@@ -571,8 +651,14 @@ int fa_set_tuning(const fa_tuning* t) {
         if (t->slot_skew > 0 && t->slot_skew % 16) return fail(FA_ERR_ARG, "slot_skew must be a multiple of 16");
         skew = t->slot_skew < 0 ? 0 : (size_t)t->slot_skew;
     }
+    int probes = g_placement_probes;
+    if (t->placement_probes) {
+        if (t->placement_probes > 16) return fail(FA_ERR_ARG, "placement_probes must be <= 16");
+        probes = t->placement_probes < 0 ? 1 : t->placement_probes;
+    }
     g_tuning = nt;
     g_slot_skew = skew;
+    g_placement_probes = probes;
     return FA_OK;
 }
 
@@ -585,6 +671,7 @@ int fa_get_tuning(fa_tuning* t) {
     t->load_policy = g_tuning.load_nt ? 2 : 1;
     t->store_policy = g_tuning.store_policy + 1;
     t->slot_skew = (int)g_slot_skew;
+    t->placement_probes = g_placement_probes;
     return FA_OK;
 }
 
@@ -686,13 +773,16 @@ int fa_bucket_define(fa_ctx* ctx, int part_id, size_t n_elems, fa_dtype in, fa_d
     p.slots.assign(G, nullptr);
     p.dout.assign(G, nullptr);
     p.stride.assign(G, 0);
+    p.probe_ms.assign(G, {});
+    p.chosen.assign(G, 0);
     for (size_t g = 0; g < G; ++g) {
         DeviceGuard dg(ctx->gpu[g].dev);
         p.stride[g] = slot_stride(p.cnt[g] * dsize(in));
         const size_t bytes = (size_t)n_clients * p.stride[g] + std::max<size_t>(1, p.cnt[g] * dsize(out));
-        if (hipMalloc((void**)&p.pool[g], bytes) != hipSuccess) {
+        int rc = alloc_placed(ctx, (int)g, p, p.stride[g], bytes, &p.pool[g]);
+        if (rc) {
             free_part(ctx, p);
-            return fail(FA_ERR_NOMEM, "device alloc of %zu B for part %d failed on GPU %zu", bytes, part_id, g);
+            return rc;
         }
         p.slots[g] = p.pool[g];
         p.dout[g] = p.pool[g] + (size_t)n_clients * p.stride[g];
@@ -796,6 +886,20 @@ int fa_bucket_slot(fa_ctx* ctx, int part_id, int gpu, int client_slot, void** d_
     if (d_ptr) *d_ptr = slot_ptr(*p, gpu, client_slot);
     if (n_elems) *n_elems = p->cnt[gpu];
     if (elem_offset) *elem_offset = p->off[gpu];
+    return FA_OK;
+}
+
+int fa_bucket_placement(fa_ctx* ctx, int part_id, int gpu, int* n_probes, float* probe_ms, int* chosen) {
+    g_err.clear();
+    Part* p;
+    int rc = check_part(ctx, part_id, &p);
+    if (rc) return rc;
+    if (gpu < 0 || gpu >= ctx->G) return fail(FA_ERR_ARG, "gpu %d out of range", gpu);
+    const auto& ms = p->probe_ms[(size_t)gpu];
+    if (n_probes) *n_probes = (int)ms.size();
+    if (probe_ms)
+        for (size_t i = 0; i < ms.size(); ++i) probe_ms[i] = ms[i];
+    if (chosen) *chosen = p->chosen[(size_t)gpu];
     return FA_OK;
 }
 

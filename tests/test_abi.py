@@ -73,12 +73,17 @@ def test_tuning_roundtrip(fa):
     before = fa.get_tuning()
     fa.set_tuning(block=128, unroll=16, load_policy=1, store_policy=4)
     assert fa.get_tuning() == {"block": 128, "max_blocks": before["max_blocks"], "unroll": 16, "load_policy": 1,
-                               "store_policy": 4, "slot_skew": before["slot_skew"]}
+                               "store_policy": 4, "slot_skew": before["slot_skew"],
+                               "placement_probes": before["placement_probes"]}
     with pytest.raises(fa.FaError):
         fa.set_tuning(store_policy=5)
     assert fa.get_tuning()["store_policy"] == 4  # a rejected call changes nothing
     fa.set_tuning(slot_skew=-1)
     assert fa.get_tuning()["slot_skew"] == 0
+    fa.set_tuning(placement_probes=-1)
+    assert fa.get_tuning()["placement_probes"] == 1
+    with pytest.raises(fa.FaError):
+        fa.set_tuning(placement_probes=17)
     with pytest.raises(fa.FaError):
         fa.set_tuning(slot_skew=100)
     fa.set_tuning(**{k: (v or -1) if k in ("max_blocks", "slot_skew") else v for k, v in before.items()})
