@@ -4,7 +4,13 @@
 //   fa_archive_tool patch <archive> <in.f32> <out>  archive with new parameters + fixed CRCs
 //   fa_archive_tool frame <archive> <out>           a Message.h aggregation frame carrying it
 //   fa_archive_tool unframe <frame> <out>           the archive inside a frame (round trip)
+//   fa_archive_tool encode out=<file> key=value ...  any Message.h frame (values=@file, data_owners=0,2,3,
+//                                                    rooting_table=0:10.0.0.1,4:10.0.0.5)
+//   fa_archive_tool decode <frame>                  JSON of every field (values as length + CRC-32)
+// encode/decode take the same arguments as oracle/ref_wire (the reference's own Message.h), so the
+// wire tests compare the two byte for byte (tests/golden/frames).
 #include <cstdio>
+#include <cstring>
 #include <fstream>
 #include <iostream>
 #include <sstream>
@@ -39,7 +45,86 @@ static void dump_list(const char* key, const std::vector<TensorView>& v) {
     printf("]");
 }
 
+static int wire_encode(int argc, char** argv) {
+    Message m;
+    std::string out;
+    for (int i = 2; i < argc; ++i) {
+        const std::string a = argv[i];
+        const size_t eq = a.find('=');
+        if (eq == std::string::npos) return std::cerr << "expected key=value: " << a << "\n", 2;
+        const std::string k = a.substr(0, eq), v = a.substr(eq + 1);
+        auto list = [&](char sep) {
+            std::vector<std::string> r;
+            std::stringstream ss(v);
+            std::string t;
+            while (std::getline(ss, t, sep)) r.push_back(t);
+            return r;
+        };
+        if (k == "out") out = v;
+        else if (k == "save_connection") m.save_connection = std::stoi(v);
+        else if (k == "type") m.type = std::stoi(v);
+        else if (k == "client_id") m.client_id = std::stoi(v);
+        else if (k == "prev_node") m.prev_node = std::stoi(v);
+        else if (k == "size_") m.size_ = std::stoi(v);
+        else if (k == "type_op") m.type_op = std::stoi(v);
+        else if (k == "model_part") m.model_part = std::stoi(v);
+        else if (k == "t_start") m.t_start = std::stol(v);
+        else if (k == "batch0") m.batch0 = std::stoi(v);
+        else if (k == "values") m.values = !v.empty() && v[0] == '@' ? slurp(v.c_str() + 1) : v;
+        else if (k == "start") m.start = std::stoi(v);
+        else if (k == "end") m.end = std::stoi(v);
+        else if (k == "prev") m.prev = std::stoi(v);
+        else if (k == "next") m.next = std::stoi(v);
+        else if (k == "dataset") m.dataset = std::stoi(v);
+        else if (k == "num_classes") m.num_classes = std::stoi(v);
+        else if (k == "model_name") m.model_name = std::stoi(v);
+        else if (k == "model_type") m.model_type = std::stoi(v);
+        else if (k == "read_table") m.read_table = std::stoi(v);
+        else if (k == "data_owners")
+            for (auto& t : list(',')) m.data_owners.push_back(std::stoi(t));
+        else if (k == "rooting_table")
+            for (auto& t : list(',')) {
+                const size_t c = t.find(':');
+                m.rooting_table.push_back({std::stoi(t.substr(0, c)), t.substr(c + 1)});
+            }
+        else return std::cerr << "unknown key " << k << "\n", 2;
+    }
+    const std::string f = frame(m);
+    spit(out.c_str(), f.data(), f.size());
+    return 0;
+}
+
+static int wire_decode(const std::string& raw) {
+    int32_t len = 0;
+    if (raw.size() < 4) return std::cerr << "short frame\n", 1;
+    std::memcpy(&len, raw.data(), 4);
+    if (len < 0 || (size_t)len + 4 != raw.size()) return std::cerr << "length prefix does not match\n", 1;
+    Message m;
+    std::string err;
+    if (!decode(raw.substr(4), &m, &err)) return std::cerr << err << "\n", 1;
+    printf("{\"save_connection\": %d, \"type\": %d", m.save_connection, m.type);
+    if (m.type == OPERATION) {
+        printf(", \"client_id\": %d, \"prev_node\": %d, \"size_\": %d, \"type_op\": %d, \"model_part\": %d, "
+               "\"t_start\": %ld, \"batch0\": %d, \"values_len\": %zu, \"values_crc32\": %u",
+               m.client_id, m.prev_node, m.size_, m.type_op, m.model_part, m.t_start, m.batch0, m.values.size(),
+               crc32((const uint8_t*)m.values.data(), m.values.size()));
+    } else {
+        printf(", \"start\": %d, \"end\": %d, \"prev\": %d, \"next\": %d, \"dataset\": %d, \"num_classes\": %d, "
+               "\"model_name\": %d, \"model_type\": %d, \"read_table\": %d, \"data_owners\": [",
+               m.start, m.end, m.prev, m.next, m.dataset, m.num_classes, m.model_name, m.model_type, m.read_table);
+        for (size_t i = 0; i < m.data_owners.size(); ++i) printf("%s%d", i ? ", " : "", m.data_owners[i]);
+        printf("], \"rooting_table\": [");
+        for (size_t i = 0; i < m.rooting_table.size(); ++i)
+            printf("%s[%d, \"%s\"]", i ? ", " : "", m.rooting_table[i].first, m.rooting_table[i].second.c_str());
+        printf("]");
+    }
+    printf("}\n");
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc >= 2 && std::string(argv[1]) == "encode") return wire_encode(argc, argv);
+    if (argc >= 3 && std::string(argv[1]) == "decode") return wire_decode(slurp(argv[2]));
     if (argc < 3) {
         std::cerr << "usage: fa_archive_tool dump|gather|patch|frame|unframe ...\n";
         return 2;

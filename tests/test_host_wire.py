@@ -114,3 +114,28 @@ def test_net_layer_and_buffer_pool_selftest(cfg):
     assert r.returncode == 0, r.stderr[-2000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["ok"] and res["archive_bytes"] > 0
+
+
+FRAMES = os.path.join(GOLDEN, "frames")
+
+
+def _frame_cases():
+    with open(os.path.join(FRAMES, "manifest.json")) as f:
+        return json.load(f)["cases"]
+
+
+@pytest.mark.parametrize("case", _frame_cases(), ids=lambda c: c["name"])
+def test_wire_matches_reference_encoder_and_parser(case, tmp_path):
+    """host/wire.cpp against the reference's own Message.h (tests/golden/frames, tools/gen_wire_golden.py):
+    the same arguments give the reference's bytes, and our parser reads the reference's bytes into the
+    fields the reference's parser found."""
+    tool = os.path.join(PKG_DIR, "bin", "fa_archive_tool")
+    args = [a.replace("GOLDEN", GOLDEN).replace("FRAMES", FRAMES) for a in case["args"]]
+    ours = str(tmp_path / "ours.bin")
+    subprocess.run([tool, "encode", "out=" + ours] + args, check=True)
+    ref_path = os.path.join(FRAMES, case["name"] + ".bin")
+    with open(ours, "rb") as a, open(ref_path, "rb") as b:
+        mine, ref = a.read(), b.read()
+    assert len(mine) == case["bytes"] and mine == ref
+    got = json.loads(subprocess.run([tool, "decode", ref_path], check=True, capture_output=True, text=True).stdout)
+    assert got == case["fields"]
