@@ -289,7 +289,9 @@ void NetLayer::reader_loop(Conn* c) {
         }
         bytes_rx_ += text->size() + 4;
         bool keep = false;
-        publish(seq, parse_frame(text, &keep));
+        // hand the frame over: once published, the consumer holds the only reference, so the buffer
+        // returns to the pool as soon as the receipt is dropped (not when this thread gets to run again)
+        publish(seq, parse_frame(std::move(text), &keep));
         if (!keep) break;
         bool ready = false;
         while (running_ && !ready) {

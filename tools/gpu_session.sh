@@ -21,7 +21,7 @@ for s in $STEPS; do
     echo "== $s $(date +%T)" | tee -a "$OUT/session.log"
     case $s in
     test)
-        timeout -k 10 900 python -m pytest tests -m gpu -q -rf > "$OUT/pytest_gpu.log" 2>&1
+        timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rf --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
         rc=$?; tail -5 "$OUT/pytest_gpu.log"; ok_or_fail $rc test ;;
     smoke)
         timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
