@@ -183,7 +183,7 @@ typedef struct {
     int slot_skew;    /* bytes between consecutive client slots beyond 4 KiB alignment (multiple of 16);
                          -1 = none; applies to buckets defined afterwards */
     int placement_probes; /* FedAvg bucket pools >= 1 GiB: at most this many candidate allocations are
-                             timed and the fastest kept; -1 = 1 (no probing); default 4 */
+                             timed and the fastest kept; -1 = 1 (no probing); default 8 */
 } fa_tuning;
 int fa_set_tuning(const fa_tuning* t);
 int fa_get_tuning(fa_tuning* t);

@@ -41,7 +41,7 @@ fa::Tuning g_tuning{128, 0, 16, 1, 2};
 // Byte skew between consecutive client slots of one bucket (see slot_stride).
 size_t g_slot_skew = 512;
 // Placement probing of large FedAvg bucket pools (see alloc_placed): at most this many candidates.
-int g_placement_probes = 4;
+int g_placement_probes = 8;
 constexpr size_t kProbeMinBytes = 1ull << 30;  // smaller pools: one allocation, no probe
 constexpr double kFastGBs = 0.83 * 8000.0;     // a candidate at >= 83% of the 8 TB/s spec is kept at once
 constexpr int kMaxProbeRecord = 8;

@@ -139,6 +139,32 @@ __device__ __forceinline__ void chain_scalar_edges(const ClientTable& t, int nc,
     }
 }
 
+// The last r < U clients of the chain (k .. k+r-1) in groups of up to G: a group's loads are all
+// issued before its first FMA (r is uniform, so the guards are scalar branches), instead of a runtime
+// loop that the compiler emits as load / wait / fma per client -- one HBM round trip per client, which
+// a bucket with D < U (e.g. C2, D = 8 under U = 16) would otherwise pay for every vector.  G = 8 keeps
+// the f32 kernel at 64 VGPRs (8 waves per SIMD); a 15-wide group would take 72.
+template <typename IN, int U, bool LNT, int V>
+__device__ __forceinline__ void chain_tail(const ClientTable& t, int k, int r, int64_t e, float* acc) {
+    constexpr int G = U < 8 ? U : 8;
+    for (; r > 0; k += G, r -= G) {
+        u32x4 raw[G];
+#pragma unroll
+        for (int u = 0; u < G; ++u)
+            if (u < r) raw[u] = ld16<LNT>(reinterpret_cast<const IN*>(t.src[k + u]) + e);
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+            if (u < r) {
+                float x[V];
+                In<IN>::widen(raw[u], x);
+                const float w = t.w[k + u];
+#pragma unroll
+                for (int j = 0; j < V; ++j) acc[j] = __builtin_fmaf(x[j], w, acc[j]);
+            }
+        }
+    }
+}
+
 // Vector body over nvec lane-vectors starting at element `head`; lane-vector v
 // covers elements head + v*V .. head + v*V + V-1 of every bucket.  LNT: nt
 // loads; SP: store policy (st16).
@@ -176,13 +202,7 @@ __global__ __launch_bounds__(256) void fedavg_chain_kernel(const ClientTable t, 
                 for (int j = 0; j < V; ++j) acc[j] = __builtin_fmaf(x[j], w, acc[j]);
             }
         }
-        for (; k < nc; ++k) {
-            float x[V];
-            In<IN>::widen(ld16<LNT>(reinterpret_cast<const IN*>(t.src[k]) + e), x);
-            const float w = t.w[k];
-#pragma unroll
-            for (int j = 0; j < V; ++j) acc[j] = __builtin_fmaf(x[j], w, acc[j]);
-        }
+        chain_tail<IN, U, LNT, V>(t, k, nc - k, e, acc);
         Out<OUT>::template store<V, SP>(out, e, acc);
     }
 }
@@ -255,13 +275,7 @@ __global__ __launch_bounds__(256) void fedavg_sync_kernel(const ClientTable t, i
                 for (int j = 0; j < V; ++j) acc[j] = __builtin_fmaf(x[j], w, acc[j]);
             }
         }
-        for (; k < nc; ++k) {
-            float x[V];
-            In<T>::widen(ld16<true>(reinterpret_cast<const T*>(t.src[k]) + e), x);
-            const float w = t.w[k];
-#pragma unroll
-            for (int j = 0; j < V; ++j) acc[j] = __builtin_fmaf(x[j], w, acc[j]);
-        }
+        chain_tail<T, U, true, V>(t, k, nc - k, e, acc);
         for (int k2 = 0; k2 < nc; ++k2) Out<T>::template store<V, SP>(const_cast<void*>(t.src[k2]), e, acc);
     }
 }

@@ -75,6 +75,25 @@ def test_fedavg_f32_bitexact(fa, O, torch_gpu, D):
         assert_bits(run_fedavg(fa, torch, clients, w, n, False, False), O.fedavg(xs, w))
 
 
+@pytest.mark.parametrize("unroll", [4, 8, 16])
+def test_fedavg_every_tail_width(fa, O, torch_gpu, unroll):
+    """Every remainder of D modulo the unroll (the grouped chain tail: 0..U-1 clients after the full
+    groups, in groups of up to 8), f32 and bf16, bit-exact."""
+    torch = torch_gpu
+    before = fa.get_tuning()
+    try:
+        fa.set_tuning(unroll=unroll)
+        n = 4099
+        for D in list(range(1, 2 * unroll + 2)) + [47]:
+            w = O.weights(D)
+            for bf16 in (False, True):
+                xs = host_clients(O, 300 + D, D, n, bf16)
+                clients = [filled(fa, torch, n, bf16, 300 + D, k) for k in range(D)]
+                assert_bits(run_fedavg(fa, torch, clients, w, n, bf16, False), O.fedavg(xs, w))
+    finally:
+        fa.set_tuning(unroll=before["unroll"])
+
+
 def test_fedavg_zero_elements_is_noop(fa, O, torch_gpu):
     torch = torch_gpu
     c = [dev_buf(torch, 4, False)]

@@ -82,6 +82,17 @@ for s in $STEPS; do
         rc=$?; head -5 "$OUT/sweep_northstar.jsonl"; ok_or_fail $rc sweep
         timeout -k 10 600 python tools/sweep.py c2 > "$OUT/sweep_c2.jsonl" 2>> "$OUT/sweep.err"
         rc=$?; head -5 "$OUT/sweep_c2.jsonl"; ok_or_fail $rc sweep_c2 ;;
+    unroll)  # unroll sweep per workload (block 128, sc1 stores), 3 pools each, interleaved in one process
+        for W in c2 c3 northstar; do
+            SWEEP_BLOCKS=128 SWEEP_STORES=3 SWEEP_UNROLLS=4,8,16 timeout -k 10 300 python tools/sweep.py $W \
+                > "$OUT/sweep_unroll_$W.jsonl" 2>> "$OUT/sweep.err"
+            rc=$?; cat "$OUT/sweep_unroll_$W.jsonl"; ok_or_fail $rc unroll_$W
+        done ;;
+    bench3)  # three bench runs (fresh process each): the spread of pool placement
+        for i in 1 2 3; do
+            timeout -k 10 300 python bench.py --no-cpu-baseline --no-secondary > "$OUT/bench3_$i.json" 2> "$OUT/bench3_$i.err"
+            rc=$?; cat "$OUT/bench3_$i.json"; ok_or_fail $rc bench3_$i
+        done ;;
     layout)
         timeout -k 10 600 python tools/exp_layout.py > "$OUT/exp_layout.jsonl" 2> "$OUT/exp_layout.err"
         rc=$?; head -8 "$OUT/exp_layout.jsonl"; tail -3 "$OUT/exp_layout.err"; ok_or_fail $rc layout ;;

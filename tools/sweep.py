@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
-"""Tuning sweep of the FedAvg kernel on the north-star workload (GPU box tool).
+"""Tuning sweep of the FedAvg kernel on a bench workload (GPU box tool).
+
+  python tools/sweep.py [workload]   SWEEP_BLOCKS / SWEEP_UNROLLS / SWEEP_STORES / SWEEP_POOLS: comma lists
 
 Interleaves every configuration in rounds inside one process (rule: A/B deltas
 come from one process), prints one JSON line per configuration with the median
@@ -25,7 +27,11 @@ def main():
     setups = [bench.Setup(fa, torch, D, n, i, o, 0, 0) for _ in range(pools)]  # placement varies per pool
     setup = setups[0]
     stream = torch.cuda.Stream()
-    grid = list(itertools.product([128, 256], [0], [8, 16], [2], [1, 2, 3, 4]))
+    def env_list(name, default):
+        v = os.environ.get(name)
+        return [int(x) for x in v.split(",")] if v else default
+    grid = list(itertools.product(env_list("SWEEP_BLOCKS", [128, 256]), [0], env_list("SWEEP_UNROLLS", [8, 16]), [2],
+                                  env_list("SWEEP_STORES", [1, 2, 3, 4])))
     times = {(g, p): [] for g in grid for p in range(pools)}
     for rnd in range(3):
         for g in grid:
