@@ -384,7 +384,10 @@ hipError_t launch_chain_u(const ClientTable& t, int nc, const float* init, void*
 template <typename IN, typename OUT, bool LNT, int SP>
 hipError_t launch_chain_sp(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
                            int64_t n, const Tuning& tu, hipStream_t s) {
-    switch (tu.unroll) {
+    // D <= 8 never fills a 16-wide group: the 8-wide body (loads and FMAs interleaved by the
+    // compiler) is ~2% faster there than the guarded tail group (tools/sweep.py c2, profiles/).
+    const int unroll = (nc <= 8 && tu.unroll == 16) ? 8 : tu.unroll;
+    switch (unroll) {
         case 4: return launch_chain_u<IN, OUT, 4, LNT, SP>(t, nc, init, out, head, nvec, n, tu, s);
         case 16: return launch_chain_u<IN, OUT, 16, LNT, SP>(t, nc, init, out, head, nvec, n, tu, s);
         default: return launch_chain_u<IN, OUT, 8, LNT, SP>(t, nc, init, out, head, nvec, n, tu, s);

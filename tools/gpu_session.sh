@@ -93,6 +93,9 @@ for s in $STEPS; do
             timeout -k 10 300 python bench.py --no-cpu-baseline --no-secondary > "$OUT/bench3_$i.json" 2> "$OUT/bench3_$i.err"
             rc=$?; cat "$OUT/bench3_$i.json"; ok_or_fail $rc bench3_$i
         done ;;
+    data)  # value dependence of the reduction time (tools/exp_data.py)
+        timeout -k 10 300 python tools/exp_data.py 3 10 > "$OUT/exp_data.jsonl" 2> "$OUT/exp_data.err"
+        rc=$?; cat "$OUT/exp_data.jsonl"; tail -2 "$OUT/exp_data.err"; ok_or_fail $rc data ;;
     layout)
         timeout -k 10 600 python tools/exp_layout.py > "$OUT/exp_layout.jsonl" 2> "$OUT/exp_layout.err"
         rc=$?; head -8 "$OUT/exp_layout.jsonl"; tail -3 "$OUT/exp_layout.err"; ok_or_fail $rc layout ;;
