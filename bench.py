@@ -40,7 +40,8 @@ WORKLOADS = {
     "c2": (8, 12_557_962, "f32", "f32", "ResNet-18 full model buckets (reference build), 8 data owners, fp32"),
     "c3": (32, 42_737_546, "bf16", "bf16", "ResNet-101 full model buckets (basic-block build), 32 owners, bf16"),
     "c4": (64, 139_611_210, "f32", "f32", "VGG-19 full model buckets (reference build), 64 owners, fp32, on one GPU"),
-    "c5": (128, 1 << 28, "f32", "f32", "synthetic 1 GiB fp32 bucket x 128 clients (two 64-client passes), one GPU"),
+    "c5": (128, 1 << 28, "f32", "f32", "synthetic 1 GiB fp32 bucket x 128 clients, all on one GPU (129 GiB resident)"),
+    "c5r": (128, 1 << 25, "f32", "f32", "C5 one rank's share on 8 GPUs (range layout): 128 clients x 128 MiB slice"),
 }
 ROTATE_MIN_BYTES = 1 << 30  # rotate input sets until a step's working set no longer fits the 256 MiB MALL
 

@@ -144,7 +144,7 @@ int fa_sync(fa_ctx* ctx);
  * starts at d_init[i] instead of +0 (used to split clients across launches or
  * GPUs bit-exactly).  Enqueued on hip_stream (a hipStream_t; NULL = the
  * ctx's compute stream of `gpu`); returns without synchronizing.  ctx may be
- * NULL except for bf16 output with D > 64 (needs ctx scratch). */
+ * NULL except for bf16 output with D > 128 (needs ctx scratch). */
 int fa_reduce_device(fa_ctx* ctx, int gpu, const void* const* d_clients, const float* h_weights, int D, size_t n,
                      fa_dtype in, void* d_out, fa_dtype out, fa_mode mode, const float* d_init, void* hip_stream);
 
@@ -156,7 +156,7 @@ int fa_reduce_device(fa_ctx* ctx, int gpu, const void* const* d_clients, const f
  * rounded once to the slot dtype and written back to all D slots, so each
  * client continues training from the FedAvg model.  HBM traffic is D*s read +
  * D*s written per element.
- * fa_sync_device: raw device pointers, any D >= 1 (ctx needed only for D > 64).
+ * fa_sync_device: raw device pointers, any D >= 1 (ctx needed only for D > 128).
  * fa_sync_part: the part's own slots on every GPU of the ctx (range shards sync
  * their ranges); h_weights NULL = the weights given to fa_submit.  Both are
  * async on hip_stream (NULL = ctx compute stream). */

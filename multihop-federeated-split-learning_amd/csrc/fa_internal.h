@@ -8,8 +8,9 @@
 namespace fa {
 
 // Clients per launch.  Pointers + weights travel in the kernel-argument segment
-// (768 B), read with scalar loads; more clients continue the chain in another pass.
-constexpr int kMaxClients = 64;
+// (1.5 KiB of the 4 KiB kernarg segment), read with scalar loads; more clients continue the chain in
+// another pass.  128 covers C5 (D = 128) in one pass.
+constexpr int kMaxClients = 128;
 
 struct ClientTable {
     const void* src[kMaxClients];

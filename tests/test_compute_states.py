@@ -73,7 +73,7 @@ def test_states_reject_mixed_architectures():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("D,bf16", [(1, False), (5, False), (3, True), (13, False), (13, True), (64, False), (70, False), (70, True)])
+@pytest.mark.parametrize("D,bf16", [(1, False), (5, False), (3, True), (13, False), (13, True), (64, False), (70, False), (70, True), (130, False), (130, True)])
 def test_sync_device_bitexact(fa, O, torch_gpu, D, bf16):
     torch = torch_gpu
     n = 100_003
@@ -83,7 +83,7 @@ def test_sync_device_bitexact(fa, O, torch_gpu, D, bf16):
         xs = [O.f32_to_bf16(x) for x in xs]
     want = O.fedavg(xs, w, out_dtype="bf16" if bf16 else "f32")
     dev = [torch.from_numpy(x.view(np.int16) if bf16 else x).cuda() for x in xs]
-    ctx = fa.Aggregator(1) if D > 64 else None
+    ctx = fa.Aggregator(1) if D > 128 else None
     fa.sync_device(dev, w, n, fa.BF16 if bf16 else fa.F32, ctx=ctx)
     torch.cuda.synchronize()
     for d in dev:

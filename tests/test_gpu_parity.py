@@ -126,7 +126,7 @@ def test_fedavg_init_continues_the_chain(fa, O, torch_gpu):
 
 
 @pytest.mark.parametrize("out_bf16", [False, True])
-@pytest.mark.parametrize("D", [1, 7, 32, 70])
+@pytest.mark.parametrize("D", [1, 7, 32, 70, 130])
 def test_fedavg_bf16_inputs(fa, O, torch_gpu, D, out_bf16):
     torch = torch_gpu
     n = 100_003
@@ -134,7 +134,7 @@ def test_fedavg_bf16_inputs(fa, O, torch_gpu, D, out_bf16):
     xs = host_clients(O, 9, D, n, True)
     clients = [filled(fa, torch, n, True, 9, k) for k in range(D)]
     ref = O.fedavg(xs, w, out_dtype="bf16" if out_bf16 else "f32")
-    if out_bf16 and D > 64:
+    if out_bf16 and D > 128:
         ctx = fa.Aggregator(1)  # bf16 output across passes needs ctx scratch
         out = dev_buf(torch, n, True)
         fa.reduce_device(clients, w, n, fa.BF16, out, fa.BF16, ctx=ctx)
