@@ -360,7 +360,7 @@ def main():
                          "kernel_ms_avg": round(ka, 4),
                          "achieved_GBs": round(s.algo_bytes() / (ka * 1e-3) / 1e9, 1),
                          "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                         "input_sets_rotated": s.nsets}
+                         "input_sets_rotated": s.nsets, "placement": s.placement}
             s.close()
         # compute-node aggregation on the C2 shape: 8 client copies synced in place
         sD, sn, si, so, _ = WORKLOADS["c2"]
