@@ -75,6 +75,11 @@ for s in $STEPS; do
             -Wl,-rpath,$PWD/multihop-federeated-split-learning_amd/lib -o "$OUT/exp_slow" > "$OUT/slow_build.log" 2>&1 &&
         timeout -k 10 400 "$OUT/exp_slow" ${SLOW_ARGS:-26 6 3} > "$OUT/exp_slow.jsonl" 2> "$OUT/exp_slow.err"
         rc=$?; cat "$OUT/exp_slow.jsonl"; tail -3 "$OUT/exp_slow.err"; ok_or_fail $rc slow ;;
+    skew)  # per-slot skew inside the same pool (tools/exp_skew.hip)
+        hipcc --offload-arch=gfx950 -O2 tools/exp_skew.hip -Iinclude -Lmultihop-federeated-split-learning_amd/lib -lfa \
+            -Wl,-rpath,$PWD/multihop-federeated-split-learning_amd/lib -o "$OUT/exp_skew" > "$OUT/skew_build.log" 2>&1 &&
+        timeout -k 10 400 "$OUT/exp_skew" ${SKEW_ARGS:-26 6 3} > "$OUT/exp_skew.jsonl" 2> "$OUT/exp_skew.err"
+        rc=$?; cat "$OUT/exp_skew.jsonl"; tail -3 "$OUT/exp_skew.err"; ok_or_fail $rc skew ;;
     e2e)
         timeout -k 10 900 python tools/e2e_bench.py 4 3 > "$OUT/e2e_bench.json" 2> "$OUT/e2e_bench.err"
         rc=$?; cat "$OUT/e2e_bench.json"; tail -3 "$OUT/e2e_bench.err"; ok_or_fail $rc e2e ;;
