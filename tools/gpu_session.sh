@@ -80,6 +80,11 @@ for s in $STEPS; do
             -Wl,-rpath,$PWD/multihop-federeated-split-learning_amd/lib -o "$OUT/exp_skew" > "$OUT/skew_build.log" 2>&1 &&
         timeout -k 10 400 "$OUT/exp_skew" ${SKEW_ARGS:-26 6 3} > "$OUT/exp_skew.jsonl" 2> "$OUT/exp_skew.err"
         rc=$?; cat "$OUT/exp_skew.jsonl"; tail -3 "$OUT/exp_skew.err"; ok_or_fail $rc skew ;;
+    cross)  # inputs of pool p into the output of pool q (tools/exp_cross.hip)
+        hipcc --offload-arch=gfx950 -O2 tools/exp_cross.hip -Iinclude -Lmultihop-federeated-split-learning_amd/lib -lfa \
+            -Wl,-rpath,$PWD/multihop-federeated-split-learning_amd/lib -o "$OUT/exp_cross" > "$OUT/cross_build.log" 2>&1 &&
+        timeout -k 10 400 "$OUT/exp_cross" ${CROSS_ARGS:-26 5 3} > "$OUT/exp_cross.jsonl" 2> "$OUT/exp_cross.err"
+        rc=$?; cat "$OUT/exp_cross.jsonl"; tail -3 "$OUT/exp_cross.err"; ok_or_fail $rc cross ;;
     e2e)
         timeout -k 10 900 python tools/e2e_bench.py 4 3 > "$OUT/e2e_bench.json" 2> "$OUT/e2e_bench.err"
         rc=$?; cat "$OUT/e2e_bench.json"; tail -3 "$OUT/e2e_bench.err"; ok_or_fail $rc e2e ;;
