@@ -85,6 +85,11 @@ for s in $STEPS; do
             -Wl,-rpath,$PWD/multihop-federeated-split-learning_amd/lib -o "$OUT/exp_cross" > "$OUT/cross_build.log" 2>&1 &&
         timeout -k 10 400 "$OUT/exp_cross" ${CROSS_ARGS:-26 5 3} > "$OUT/exp_cross.jsonl" 2> "$OUT/exp_cross.err"
         rc=$?; cat "$OUT/exp_cross.jsonl"; tail -3 "$OUT/exp_cross.err"; ok_or_fail $rc cross ;;
+    order)  # walk order of the grid over the buckets vs the slow-pool penalty (tools/exp_order.hip)
+        hipcc --offload-arch=gfx950 -O2 tools/exp_order.hip -Iinclude -Lmultihop-federeated-split-learning_amd/lib -lfa \
+            -Wl,-rpath,$PWD/multihop-federeated-split-learning_amd/lib -o "$OUT/exp_order" > "$OUT/order_build.log" 2>&1 &&
+        timeout -k 10 400 "$OUT/exp_order" ${ORDER_ARGS:-26 5 3} > "$OUT/exp_order.jsonl" 2> "$OUT/exp_order.err"
+        rc=$?; cat "$OUT/exp_order.jsonl"; tail -3 "$OUT/exp_order.err"; ok_or_fail $rc order ;;
     e2e)
         timeout -k 10 900 python tools/e2e_bench.py 4 3 > "$OUT/e2e_bench.json" 2> "$OUT/e2e_bench.err"
         rc=$?; cat "$OUT/e2e_bench.json"; tail -3 "$OUT/e2e_bench.err"; ok_or_fail $rc e2e ;;
