@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 2
+#define FA_ABI_VERSION 3
 
 typedef struct fa_ctx fa_ctx; /* opaque: device slots, streams, pinned staging */
 
@@ -184,6 +184,8 @@ typedef struct {
                          -1 = none; applies to buckets defined afterwards */
     int placement_probes; /* FedAvg bucket pools >= 1 GiB: at most this many candidate allocations are
                              timed and the fastest kept; -1 = 1 (no probing); default 8 */
+    int walk;         /* FedAvg grid walk over a bucket: 1 linear, 2 each XCD's workgroups own one contiguous
+                         eighth, 3 the same with the odd eighths walked backwards (one-shot grid only) */
 } fa_tuning;
 int fa_set_tuning(const fa_tuning* t);
 int fa_get_tuning(fa_tuning* t);

@@ -35,7 +35,7 @@ class FaError(RuntimeError):
 class _Tuning(ctypes.Structure):
     _fields_ = [("block", ctypes.c_int), ("max_blocks", ctypes.c_int), ("unroll", ctypes.c_int),
                 ("load_policy", ctypes.c_int), ("store_policy", ctypes.c_int), ("slot_skew", ctypes.c_int),
-                ("placement_probes", ctypes.c_int)]
+                ("placement_probes", ctypes.c_int), ("walk", ctypes.c_int)]
 
 
 def build():
@@ -160,17 +160,19 @@ def get_tuning():
     t = _Tuning()
     check(lib().fa_get_tuning(ctypes.byref(t)))
     return {"block": t.block, "max_blocks": t.max_blocks, "unroll": t.unroll, "load_policy": t.load_policy,
-            "store_policy": t.store_policy, "slot_skew": t.slot_skew, "placement_probes": t.placement_probes}
+            "store_policy": t.store_policy, "slot_skew": t.slot_skew, "placement_probes": t.placement_probes,
+            "walk": t.walk}
 
 
 LOAD_DEFAULT, LOAD_NT = 1, 2
 STORE_PLAIN, STORE_NT, STORE_SC1, STORE_SC01 = 1, 2, 3, 4
 
 
-def set_tuning(block=0, max_blocks=0, unroll=0, load_policy=0, store_policy=0, slot_skew=0, placement_probes=0):
+def set_tuning(block=0, max_blocks=0, unroll=0, load_policy=0, store_policy=0, slot_skew=0, placement_probes=0,
+               walk=0):
     """fa_set_tuning; every argument 0 = keep.  max_blocks -1 = one-shot grid, slot_skew -1 = none,
     placement_probes -1 = no probing."""
-    t = _Tuning(block, max_blocks, unroll, load_policy, store_policy, slot_skew, placement_probes)
+    t = _Tuning(block, max_blocks, unroll, load_policy, store_policy, slot_skew, placement_probes, walk)
     check(lib().fa_set_tuning(ctypes.byref(t)))
 
 

@@ -37,9 +37,9 @@ thread_local std::string g_err;
 // block 128, one-shot grid, 16 clients per load group, nt loads, write-through (sc1) stores:
 // tools/sweep.py over 3 pools (profiles/r01_summary.json): sc1 stores 2.7% faster than nt,
 // unroll 16 ~1% faster than 8, block 128 2-3% faster than 256.
-fa::Tuning g_tuning{128, 0, 16, 1, 2};
+fa::Tuning g_tuning{128, 0, 16, 1, 2, 0};
 // Byte skew between consecutive client slots of one bucket (see slot_stride).
-size_t g_slot_skew = 512;
+size_t g_slot_skew = 2048;
 // Placement probing of large FedAvg bucket pools (see alloc_placed): at most this many candidates.
 int g_placement_probes = 8;
 constexpr size_t kProbeMinBytes = 1ull << 30;  // smaller pools: one allocation, no probe
@@ -651,6 +651,10 @@ int fa_set_tuning(const fa_tuning* t) {
         if (t->slot_skew > 0 && t->slot_skew % 16) return fail(FA_ERR_ARG, "slot_skew must be a multiple of 16");
         skew = t->slot_skew < 0 ? 0 : (size_t)t->slot_skew;
     }
+    if (t->walk) {
+        if (t->walk < 1 || t->walk > 3) return fail(FA_ERR_ARG, "walk must be 1..3");
+        nt.walk = t->walk - 1;
+    }
     int probes = g_placement_probes;
     if (t->placement_probes) {
         if (t->placement_probes > 16) return fail(FA_ERR_ARG, "placement_probes must be <= 16");
@@ -672,6 +676,7 @@ int fa_get_tuning(fa_tuning* t) {
     t->store_policy = g_tuning.store_policy + 1;
     t->slot_skew = (int)g_slot_skew;
     t->placement_probes = g_placement_probes;
+    t->walk = g_tuning.walk + 1;
     return FA_OK;
 }
 

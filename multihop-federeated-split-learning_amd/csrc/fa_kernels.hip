@@ -168,13 +168,26 @@ __device__ __forceinline__ void chain_tail(const ClientTable& t, int k, int r, i
 // Vector body over nvec lane-vectors starting at element `head`; lane-vector v
 // covers elements head + v*V .. head + v*V + V-1 of every bucket.  LNT: nt
 // loads; SP: store policy (st16).
+// walk (fa_tuning.walk - 1): 0 = linear grid-stride; 1 = XCD eighths: on a one-shot grid of 8*nb8
+// workgroups, workgroup b takes block slot (b % 8) * nb8 + b / 8, so the workgroups of one XCD (blocks
+// are dealt round-robin over the 8 XCDs; speed only, never correctness) walk one contiguous eighth of
+// the bucket; 2 = the same with the odd eighths walked backwards.
 template <typename IN, typename OUT, int U, bool LNT, int SP, bool INIT>
 __global__ __launch_bounds__(256) void fedavg_chain_kernel(const ClientTable t, int nc, const float* init, void* out,
-                                                           int64_t head, int64_t nvec, int64_t n) {
+                                                           int64_t head, int64_t nvec, int64_t n, int walk) {
     constexpr int V = In<IN>::kVec;
     chain_scalar_edges<IN, OUT, INIT>(t, nc, init, out, head, head + nvec * V, n);
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t v0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (walk) {
+        const int64_t nb8 = gridDim.x >> 3;
+        const int x = blockIdx.x & 7;
+        int64_t j = blockIdx.x >> 3;
+        if (walk == 2 && (x & 1)) j = nb8 - 1 - j;
+        v0 = (x * nb8 + j) * blockDim.x + threadIdx.x;
+        stride = nvec;  // one vector per lane
+    }
+    for (int64_t v = v0; v < nvec; v += stride) {
         const int64_t e = head + v * V;  // first element owned by this lane
         float acc[V];
         if constexpr (INIT) {
@@ -371,13 +384,16 @@ inline int64_t grid_for(int64_t work, const Tuning& tu) {
 template <typename IN, typename OUT, int U, bool LNT, int SP>
 hipError_t launch_chain_u(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
                           int64_t n, const Tuning& tu, hipStream_t s) {
-    const int64_t g = grid_for(nvec > 0 ? nvec : 1, tu);
+    int64_t g = grid_for(nvec > 0 ? nvec : 1, tu);
+    // the XCD walks need the one-shot grid (one vector per lane), rounded up to whole eighths
+    const int walk = (tu.walk && tu.max_blocks <= 0 && nvec >= 8 * (int64_t)tu.block) ? tu.walk : 0;
+    if (walk) g = (g + 7) / 8 * 8;
     if (init)
         hipLaunchKernelGGL((fedavg_chain_kernel<IN, OUT, U, LNT, SP, true>), dim3((unsigned)g), dim3(tu.block), 0, s,
-                           t, nc, init, out, head, nvec, n);
+                           t, nc, init, out, head, nvec, n, walk);
     else
         hipLaunchKernelGGL((fedavg_chain_kernel<IN, OUT, U, LNT, SP, false>), dim3((unsigned)g), dim3(tu.block), 0,
-                           s, t, nc, init, out, head, nvec, n);
+                           s, t, nc, init, out, head, nvec, n, walk);
     return hipGetLastError();
 }
 

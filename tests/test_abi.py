@@ -52,7 +52,7 @@ def test_library_is_gfx950_code(fa, tmp_path):
 
 def test_version_and_errors_without_gpu(fa):
     L = fa.lib()
-    assert L.fa_version() == 2
+    assert L.fa_version() == 3
     # argument errors are reported before any device work
     rc = L.fa_reduce_device(None, 0, None, None, 0, 16, 0, None, 0, 0, None, None)
     assert rc == fa.ERR_ARG and "null" in fa.last_error()
@@ -74,7 +74,7 @@ def test_tuning_roundtrip(fa):
     fa.set_tuning(block=128, unroll=16, load_policy=1, store_policy=4)
     assert fa.get_tuning() == {"block": 128, "max_blocks": before["max_blocks"], "unroll": 16, "load_policy": 1,
                                "store_policy": 4, "slot_skew": before["slot_skew"],
-                               "placement_probes": before["placement_probes"]}
+                               "placement_probes": before["placement_probes"], "walk": before["walk"]}
     with pytest.raises(fa.FaError):
         fa.set_tuning(store_policy=5)
     assert fa.get_tuning()["store_policy"] == 4  # a rejected call changes nothing
@@ -86,6 +86,8 @@ def test_tuning_roundtrip(fa):
         fa.set_tuning(placement_probes=17)
     with pytest.raises(fa.FaError):
         fa.set_tuning(slot_skew=100)
+    with pytest.raises(fa.FaError):
+        fa.set_tuning(walk=4)
     fa.set_tuning(**{k: (v or -1) if k in ("max_blocks", "slot_skew") else v for k, v in before.items()})
     assert fa.get_tuning() == before
 

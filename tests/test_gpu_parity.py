@@ -175,7 +175,10 @@ def test_literal_mode(fa, O, torch_gpu, bf16):
                                     dict(block=256, unroll=8, load_policy=1, store_policy=3, max_blocks=7),
                                     dict(block=256, unroll=16, load_policy=2, store_policy=4, max_blocks=1),
                                     dict(block=128, unroll=8, load_policy=2, store_policy=3, max_blocks=-1),
-                                    dict(block=64, unroll=16, load_policy=1, store_policy=4, max_blocks=5)])
+                                    dict(block=64, unroll=16, load_policy=1, store_policy=4, max_blocks=5),
+                                    dict(block=128, unroll=16, load_policy=2, store_policy=3, max_blocks=-1, walk=2),
+                                    dict(block=256, unroll=8, load_policy=2, store_policy=3, max_blocks=-1, walk=3),
+                                    dict(block=64, unroll=4, load_policy=1, store_policy=2, max_blocks=9, walk=3)])
 def test_tuning_variants_same_bits(fa, O, torch_gpu, tuning):
     torch = torch_gpu
     before = fa.get_tuning()

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Tuning sweep of the FedAvg kernel on a bench workload (GPU box tool).
 
-  python tools/sweep.py [workload]   SWEEP_BLOCKS / SWEEP_UNROLLS / SWEEP_STORES / SWEEP_POOLS: comma lists
+  python tools/sweep.py [workload]   SWEEP_BLOCKS / SWEEP_UNROLLS / SWEEP_STORES / SWEEP_WALKS / SWEEP_POOLS:
+                                     comma lists
 
 Interleaves every configuration in rounds inside one process (rule: A/B deltas
 come from one process), prints one JSON line per configuration with the median
@@ -31,12 +32,12 @@ def main():
         v = os.environ.get(name)
         return [int(x) for x in v.split(",")] if v else default
     grid = list(itertools.product(env_list("SWEEP_BLOCKS", [128, 256]), [0], env_list("SWEEP_UNROLLS", [8, 16]), [2],
-                                  env_list("SWEEP_STORES", [1, 2, 3, 4])))
+                                  env_list("SWEEP_STORES", [1, 2, 3, 4]), env_list("SWEEP_WALKS", [1])))
     times = {(g, p): [] for g in grid for p in range(pools)}
     for rnd in range(3):
         for g in grid:
             fa.set_tuning(block=g[0], max_blocks=g[1] if g[1] else -1, unroll=g[2], load_policy=g[3],
-                          store_policy=g[4])
+                          store_policy=g[4], walk=g[5])
             for p, st in enumerate(setups):
                 ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(4)]
                 for a, b in ev:
@@ -50,6 +51,7 @@ def main():
         meds = [statistics.median(times[(g, p)]) for p in range(pools)]
         med = statistics.mean(meds)
         rows.append({"block": g[0], "max_blocks": g[1], "unroll": g[2], "load_policy": g[3], "store_policy": g[4],
+                     "walk": g[5],
                      "ms_mean_of_pool_medians": round(med, 4), "pool_ms": [round(m, 4) for m in meds],
                      "GBs": round(setup.algo_bytes() / med / 1e6, 1)})
     rows.sort(key=lambda r: r["ms_mean_of_pool_medians"])
