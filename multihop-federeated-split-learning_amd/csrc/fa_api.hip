@@ -36,8 +36,9 @@ namespace {
 thread_local std::string g_err;
 // block 128, one-shot grid, 16 clients per load group, nt loads, write-through (sc1) stores:
 // tools/sweep.py over 3 pools (profiles/r01_summary.json): sc1 stores 2.7% faster than nt,
-// unroll 16 ~1% faster than 8, block 128 2-3% faster than 256.
-fa::Tuning g_tuning{128, 0, 16, 1, 2, 0};
+// unroll 16 ~1% faster than 8, block 128 2-3% faster than 256; XCD-eighths walk 0.5-1.5% faster than
+// linear in 7 of 9 pools over the north star, C3 and C4 (gpurun_out r01s11, profiles/r01_summary.json).
+fa::Tuning g_tuning{128, 0, 16, 1, 2, 1};
 // Byte skew between consecutive client slots of one bucket (see slot_stride).
 size_t g_slot_skew = 2048;
 // Placement probing of large FedAvg bucket pools (see alloc_placed): at most this many candidates.
@@ -410,8 +411,10 @@ void free_part(fa_ctx* ctx, Part& p) {
 // address modulo a large power of two put the U simultaneous loads of a wave
 // (and its store) on the same HBM channels; a small per-slot skew spreads them.
 // Measured on MI355X (profiles/r01_summary.json, tools/exp_layout.py): 256-512 B
-// skew -> 1.30-1.32 ms for 32 x 256 MiB vs 1.47-1.51 ms unskewed; 64 B and
-// >= 1 KiB skews do not help reliably.  Slots stay 16-byte aligned.
+// skew -> 1.30-1.32 ms for 32 x 256 MiB vs 1.47-1.51 ms unskewed.  Re-laid out
+// inside the same six pools (tools/exp_skew.hip), 2048 B beat 512 B in every one
+// (by 0.6-2.9%); 8 KiB + 512 and 2 MiB + 512 are 7-12% slower.  Slots stay
+// 16-byte aligned.
 size_t slot_stride(size_t bytes) { return (bytes + 4095) / 4096 * 4096 + g_slot_skew; }
 
 inline char* slot_ptr(const Part& p, int g, int k) { return p.slots[g] + (size_t)k * p.stride[g]; }
