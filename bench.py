@@ -81,8 +81,21 @@ def cpu_baseline(D, sample_elems, reps):
             out = subprocess.run([harness, "bench-fedavg", str(sample_elems), str(D), str(threads), str(reps)],
                                  capture_output=True, text=True, timeout=600, check=True).stdout
             r = json.loads(out.strip().splitlines()[-1])
-            return {"value": round(r["gib_s"], 3), "unit": "GiB/s", "cores": threads, "kind": "reference",
-                    "sample": sample + "; libtorch at::set_num_threads(%d)" % threads}
+            res = {"value": round(r["gib_s"], 3), "unit": "GiB/s", "cores": threads, "kind": "reference",
+                   "sample": sample + "; libtorch at::set_num_threads(%d)" % threads}
+            # the reference aggregator's own receive loop (aggregator.cpp:59-93: torch::load of each receipt
+            # into the global module + (p+p)/1000 + copy_), on C2's largest bucket, 8 receipts
+            try:
+                out = subprocess.run([harness, "bench-literal", "1", "1", "9", "3", "10", "8", str(threads), "2"],
+                                     capture_output=True, text=True, timeout=300, check=True).stdout
+                lit = json.loads(out.strip().splitlines()[-1])
+                res["reference_receive_loop"] = {
+                    "value": round(lit["gib_s"], 3), "unit": "GiB/s of parameters received",
+                    "sample": "ResNet-18 (C2) model_part 2 (%d fp32 params), 8 receipts: torch::load + (p+p)/1000 "
+                              "+ copy_ per receipt, %d threads" % (lit["numel"], threads)}
+            except Exception as e:  # noqa: BLE001 -- optional second figure
+                print("cpu baseline: reference receive loop not timed (%s)" % e, file=sys.stderr)
+            return res
         except Exception as e:  # noqa: BLE001 -- fall through to the port
             print("cpu baseline: ref_harness failed (%s), timing the oracle port" % e, file=sys.stderr)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
