@@ -100,6 +100,11 @@ for s in $STEPS; do
             -Wl,-rpath,$PWD/multihop-federeated-split-learning_amd/lib -o "$OUT/exp_phase2" > "$OUT/phase2_build.log" 2>&1 &&
         timeout -k 10 300 "$OUT/exp_phase2" ${PHASE_ARGS:-26 4 3} > "$OUT/exp_phase2.jsonl" 2> "$OUT/exp_phase2.err"
         rc=$?; cat "$OUT/exp_phase2.jsonl"; tail -3 "$OUT/exp_phase2.err"; ok_or_fail $rc phase2 ;;
+    phase3)  # register-staged phases and soft barriers (tools/exp_phase3.hip)
+        hipcc --offload-arch=gfx950 -O2 tools/exp_phase3.hip -Iinclude -Lmultihop-federeated-split-learning_amd/lib -lfa \
+            -Wl,-rpath,$PWD/multihop-federeated-split-learning_amd/lib -o "$OUT/exp_phase3" > "$OUT/phase3_build.log" 2>&1 &&
+        timeout -k 10 300 "$OUT/exp_phase3" ${PHASE_ARGS:-26 4 3} > "$OUT/exp_phase3.jsonl" 2> "$OUT/exp_phase3.err"
+        rc=$?; cat "$OUT/exp_phase3.jsonl"; tail -3 "$OUT/exp_phase3.err"; ok_or_fail $rc phase3 ;;
     e2e)
         timeout -k 10 900 python tools/e2e_bench.py 4 3 > "$OUT/e2e_bench.json" 2> "$OUT/e2e_bench.err"
         rc=$?; cat "$OUT/e2e_bench.json"; tail -3 "$OUT/e2e_bench.err"; ok_or_fail $rc e2e ;;
