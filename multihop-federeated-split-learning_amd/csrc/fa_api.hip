@@ -38,7 +38,9 @@ thread_local std::string g_err;
 // tools/sweep.py over 3 pools (profiles/r01_summary.json): sc1 stores 2.7% faster than nt,
 // unroll 16 ~1% faster than 8, block 128 2-3% faster than 256; XCD-eighths walk 0.5-1.5% faster than
 // linear in 7 of 9 pools over the north star, C3 and C4 (gpurun_out r01s11, profiles/r01_summary.json).
-fa::Tuning g_tuning{128, 0, 16, 1, 2, 1};
+// Default walk: phased (fa_kernels.hip, fedavg_phased_kernel) wherever a bucket holds a full phase,
+// the XCD-eighths one-shot grid below that.
+fa::Tuning g_tuning{128, 0, 16, 1, 2, 3};
 // Byte skew between consecutive client slots of one bucket (see slot_stride).
 size_t g_slot_skew = 2048;
 // Placement probing of large FedAvg bucket pools (see alloc_placed): at most this many candidates.
@@ -655,7 +657,7 @@ int fa_set_tuning(const fa_tuning* t) {
         skew = t->slot_skew < 0 ? 0 : (size_t)t->slot_skew;
     }
     if (t->walk) {
-        if (t->walk < 1 || t->walk > 3) return fail(FA_ERR_ARG, "walk must be 1..3");
+        if (t->walk < 1 || t->walk > 4) return fail(FA_ERR_ARG, "walk must be 1..4");
         nt.walk = t->walk - 1;
     }
     int probes = g_placement_probes;

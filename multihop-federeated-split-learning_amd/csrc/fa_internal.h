@@ -23,7 +23,9 @@ struct Tuning {
     int unroll;      // clients per load group: 4, 8, 16
     int load_nt;      // non-temporal client loads
     int store_policy; // 0 plain, 1 nt, 2 sc1 (write-through), 3 sc0 sc1
-    int walk;         // FedAvg grid walk: 0 linear, 1 XCD eighths, 2 XCD eighths, odd ones reversed
+    int walk;         // FedAvg grid walk: 0 linear, 1 XCD eighths, 2 XCD eighths, odd ones reversed,
+                      // 3 phased (persistent grid, reads and writes separated in time; XCD eighths
+                      // for buckets smaller than one phase)
 };
 
 hipError_t launch_chain(const ClientTable& t, int nc, fa_dtype in, fa_dtype out, const float* init, void* dst,

@@ -21,6 +21,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+#include <type_traits>
+
 #include "fa_internal.h"
 
 namespace fa {
@@ -165,6 +168,39 @@ __device__ __forceinline__ void chain_tail(const ClientTable& t, int k, int r, i
     }
 }
 
+// The ordered chain for the V elements of every client bucket starting at element e: groups of U
+// loads in flight before their FMAs, then the grouped tail.  acc starts at +0 or at init[e..].
+template <typename IN, int U, bool LNT, bool INIT>
+__device__ __forceinline__ void chain_vec(const ClientTable& t, int nc, const float* init, int64_t e, float* acc) {
+    constexpr int V = In<IN>::kVec;
+    if constexpr (INIT) {
+#pragma unroll
+        for (int j = 0; j < V; j += 4) {
+            u32x4 r = ld16<LNT>(init + e + j);
+            acc[j] = __uint_as_float(r.x); acc[j + 1] = __uint_as_float(r.y);
+            acc[j + 2] = __uint_as_float(r.z); acc[j + 3] = __uint_as_float(r.w);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < V; ++j) acc[j] = 0.0f;
+    }
+    int k = 0;
+    for (; k + U <= nc; k += U) {
+        u32x4 raw[U];  // U loads in flight before the first FMA of the group
+#pragma unroll
+        for (int u = 0; u < U; ++u) raw[u] = ld16<LNT>(reinterpret_cast<const IN*>(t.src[k + u]) + e);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            float x[V];
+            In<IN>::widen(raw[u], x);
+            const float w = t.w[k + u];
+#pragma unroll
+            for (int j = 0; j < V; ++j) acc[j] = __builtin_fmaf(x[j], w, acc[j]);
+        }
+    }
+    chain_tail<IN, U, LNT, V>(t, k, nc - k, e, acc);
+}
+
 // Vector body over nvec lane-vectors starting at element `head`; lane-vector v
 // covers elements head + v*V .. head + v*V + V-1 of every bucket.  LNT: nt
 // loads; SP: store policy (st16).
@@ -190,33 +226,155 @@ __global__ __launch_bounds__(256) void fedavg_chain_kernel(const ClientTable t, 
     for (int64_t v = v0; v < nvec; v += stride) {
         const int64_t e = head + v * V;  // first element owned by this lane
         float acc[V];
+        chain_vec<IN, U, LNT, INIT>(t, nc, init, e, acc);
+        Out<OUT>::template store<V, SP>(out, e, acc);
+    }
+}
+
+// ---------------------------------------------------------------- phased FedAvg chain
+//
+// The same chain, with the output stream separated from the input streams in TIME.  On MI355X the
+// 32 input streams of the north star read at 7.1 TB/s in every HBM pool, and a write-only stream
+// runs at 6.2 TB/s, but interleaved they lose 0.07 ms (fast pools) to 0.2 ms (slow pools) to
+// read/write turnaround -- which of the two a pool gets depends only on where the allocation of the
+// INPUTS lands physically (tools/exp_slow.hip, exp_cross.hip).  Here a persistent grid
+// (one 256-thread workgroup per CU) works in phases: every lane reduces RL vectors into LDS (160 KiB
+// per CU) and RR more into VGPRs, the workgroups meet at a chip-wide counter, then all of them write
+// the phase's results.  Three phases cover the north star; it runs at the fast pools' speed in every
+// pool (tools/exp_phase3.hip: 1.274-1.279 ms against 1.273-1.276 fast / 1.42 slow for the linear
+// walk).  Results are bit-identical: the phases only reorder stores in time.
+//
+// The counter pair sync[0] (arrivals) / sync[1] (departures) starts at zero; the last workgroup to
+// leave resets both, so the next launch on the stream finds them zero again.  The wait is bounded
+// (every wave reaches the exit even if the grid were not co-resident: then only speed suffers), and
+// starts the write part once all but `slack` workgroups have arrived.
+constexpr int kPhasedThreads = 256;
+
+template <typename IN>
+struct Phased {  // vectors per lane per phase: LDS (160 KiB per workgroup) + registers
+    static constexpr int V = In<IN>::kVec;
+    static constexpr int RL = 160 * 1024 / (kPhasedThreads * V * 4);  // f32 in: 40, bf16 in: 20
+    static constexpr int RR = 128 / V;                                  // 128 VGPRs: 32 / 16
+};
+
+// The register-staged part of a phase: wave w of workgroup b owns a contiguous chunk of RR*64
+// vectors (RR KiB of every bucket for f32), lane l holds vectors c0 + r*64 + l for r < RR in keep[].
+// The loops are swapped -- clients outside (a runtime loop), the RR vectors inside (unrolled, so
+// every index into keep[] is a constant and it stays in VGPRs); each element still sees its clients
+// in order, so the chain is unchanged.  The wave's base address is uniform (SGPRs) and r*1 KiB a
+// constant, so a load needs no per-vector address registers: keep[] (128 VGPRs) and 16 loads in
+// flight fit the 256 architectural VGPRs.  Returns false (nothing staged) for a wave whose chunk
+// runs past the end of the bucket; the caller reduces and stores those vectors directly.
+template <typename IN, bool INIT, int RR>
+__device__ __forceinline__ bool stage_regs(const ClientTable& t, int nc, const float* init, int64_t head, int64_t c0,
+                                           int64_t nvec, float (&keep)[RR][In<IN>::kVec]) {
+    constexpr int V = In<IN>::kVec, G16 = 16;
+    if (c0 + (int64_t)RR * 64 > nvec) return false;
+    const int lane = threadIdx.x & 63;
+    const int64_t ubase = (head + c0 * V) * (int64_t)sizeof(IN);      // wave-uniform
+    const uint32_t loff = (uint32_t)(lane * V * (int)sizeof(IN));     // this lane's 16 B
+    constexpr int64_t kRowBytes = 64 * V * (int64_t)sizeof(IN);        // one vector per lane: 1 KiB
+#pragma unroll
+    for (int r = 0; r < RR; ++r) {
         if constexpr (INIT) {
+            const float* ip = init + head + (c0 + r * 64 + lane) * V;
 #pragma unroll
             for (int j = 0; j < V; j += 4) {
-                u32x4 r = ld16<LNT>(init + e + j);
-                acc[j] = __uint_as_float(r.x); acc[j + 1] = __uint_as_float(r.y);
-                acc[j + 2] = __uint_as_float(r.z); acc[j + 3] = __uint_as_float(r.w);
+                u32x4 q = ld16<true>(ip + j);
+                keep[r][j] = __uint_as_float(q.x); keep[r][j + 1] = __uint_as_float(q.y);
+                keep[r][j + 2] = __uint_as_float(q.z); keep[r][j + 3] = __uint_as_float(q.w);
             }
         } else {
 #pragma unroll
-            for (int j = 0; j < V; ++j) acc[j] = 0.0f;
+            for (int j = 0; j < V; ++j) keep[r][j] = 0.0f;
         }
-        int k = 0;
-        for (; k + U <= nc; k += U) {
-            u32x4 raw[U];  // U loads in flight before the first FMA of the group
+    }
+    for (int k = 0; k < nc; ++k) {
+        const char* src = reinterpret_cast<const char*>(t.src[k]) + ubase;
+        const float w = t.w[k];
 #pragma unroll
-            for (int u = 0; u < U; ++u) raw[u] = ld16<LNT>(reinterpret_cast<const IN*>(t.src[k + u]) + e);
+        for (int r0 = 0; r0 < RR; r0 += G16) {
+            u32x4 raw[G16];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                float x[V];
-                In<IN>::widen(raw[u], x);
-                const float w = t.w[k + u];
+            for (int u = 0; u < G16; ++u)
+                if (r0 + u < RR) raw[u] = ld16<true>(src + (r0 + u) * kRowBytes + loff);
 #pragma unroll
-                for (int j = 0; j < V; ++j) acc[j] = __builtin_fmaf(x[j], w, acc[j]);
+            for (int u = 0; u < G16; ++u) {
+                if (r0 + u < RR) {
+                    float x[V];
+                    In<IN>::widen(raw[u], x);
+#pragma unroll
+                    for (int j = 0; j < V; ++j) keep[r0 + u][j] = __builtin_fmaf(x[j], w, keep[r0 + u][j]);
+                }
             }
         }
-        chain_tail<IN, U, LNT, V>(t, k, nc - k, e, acc);
-        Out<OUT>::template store<V, SP>(out, e, acc);
+    }
+    return true;
+}
+
+template <typename IN, typename OUT, bool INIT>
+__global__ __launch_bounds__(kPhasedThreads) void fedavg_phased_kernel(const ClientTable t, int nc, const float* init,
+                                                                       void* out, int64_t head, int64_t nvec, int64_t n,
+                                                                       unsigned* sync, int slack) {
+    constexpr int V = In<IN>::kVec, T = kPhasedThreads, RL = Phased<IN>::RL, RR = Phased<IN>::RR;
+    constexpr int U = 16;
+    __shared__ float buf[RL * T * V];
+    chain_scalar_edges<IN, OUT, INIT>(t, nc, init, out, head, head + nvec * V, n);
+    const int64_t G = gridDim.x;
+    const int64_t per_phase = G * T * (RL + RR);
+    const int phases = (int)((nvec + per_phase - 1) / per_phase);
+    for (int p = 0; p < phases; ++p) {
+        const int64_t base = (int64_t)p * per_phase + (int64_t)blockIdx.x * T + threadIdx.x;
+#pragma unroll 1
+        for (int i = 0; i < RL; ++i) {
+            const int64_t v = base + (int64_t)i * G * T;
+            if (v < nvec) {
+                float acc[V];
+                chain_vec<IN, U, true, INIT>(t, nc, init, head + v * V, acc);
+#pragma unroll
+                for (int j = 0; j < V; ++j) buf[(i * T + threadIdx.x) * V + j] = acc[j];
+            }
+        }
+        // register part: this wave's contiguous chunk after the phase's LDS part
+        const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+        const int64_t c0 = (int64_t)p * per_phase + G * T * RL + ((int64_t)blockIdx.x * (T / 64) + wave) * RR * 64;
+        float keep[RR][V];
+        const bool staged = stage_regs<IN, INIT, RR>(t, nc, init, head, c0, nvec, keep);
+        if (!staged) {  // the chunk that holds the end of the bucket (or lies past it): no staging
+            for (int r = 0; r < RR; ++r) {
+                const int64_t v = c0 + r * 64 + (threadIdx.x & 63);
+                if (v < nvec) {
+                    float acc[V];
+                    chain_vec<IN, U, true, INIT>(t, nc, init, head + v * V, acc);
+                    Out<OUT>::template store<V, kStSc1>(out, head + v * V, acc);
+                }
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __hip_atomic_fetch_add(&sync[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned target = (unsigned)(G * (p + 1) - slack);
+            for (int spins = 0; __hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
+                                spins < (1 << 16);
+                 ++spins)
+                __builtin_amdgcn_s_sleep(1);
+        }
+        __syncthreads();
+#pragma unroll 1
+        for (int i = 0; i < RL; ++i) {
+            const int64_t v = base + (int64_t)i * G * T;
+            if (v < nvec) Out<OUT>::template store<V, kStSc1>(out, head + v * V, &buf[(i * T + threadIdx.x) * V]);
+        }
+        if (staged) {
+            const int64_t c = c0 + (threadIdx.x & 63);
+#pragma unroll
+            for (int r = 0; r < RR; ++r) Out<OUT>::template store<V, kStSc1>(out, head + (c + r * 64) * V, keep[r]);
+        }
+    }
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(&sync[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)G - 1) {
+        __hip_atomic_store(&sync[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&sync[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -421,9 +579,67 @@ hipError_t launch_chain_lnt(const ClientTable& t, int nc, const float* init, voi
     }
 }
 
+// Per-device state of the phased kernel: the CU count (= its grid) and a small table of zeroed
+// arrival/departure counter pairs, one picked per stream (launches on one stream are serialized, so
+// they never share a pair at the same time; two streams that hash to one pair would only lose speed).
+constexpr int kMaxDevices = 64, kSyncSlots = 64;
+struct PhasedDevice {
+    std::once_flag once;
+    int cus = 0;
+    unsigned* sync = nullptr;  // kSyncSlots pairs
+};
+PhasedDevice g_phased[kMaxDevices];
+
+PhasedDevice* phased_device() {
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
+    PhasedDevice& d = g_phased[dev];
+    std::call_once(d.once, [&] {
+        int cus = 0;
+        unsigned* p = nullptr;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return;
+        if (hipMalloc((void**)&p, sizeof(unsigned) * 2 * kSyncSlots) != hipSuccess) return;
+        if (hipMemset(p, 0, sizeof(unsigned) * 2 * kSyncSlots) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+            (void)hipFree(p);
+            return;
+        }
+        d.cus = cus;
+        d.sync = p;
+    });
+    (void)hipGetLastError();
+    return d.sync ? &d : nullptr;
+}
+
+// The phased kernel when it applies (walk 3 = fa_tuning.walk 4, vector path, at least one full phase
+// of work, one workgroup per CU co-resident); otherwise hipErrorNotSupported and the caller takes the
+// one-shot grid.
+template <typename IN, typename OUT>
+hipError_t launch_phased(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
+                         int64_t n, const Tuning& tu, hipStream_t s) {
+    if (tu.walk != 3) return hipErrorNotSupported;
+    PhasedDevice* d = phased_device();
+    if (!d) return hipErrorNotSupported;
+    const int64_t per_phase = (int64_t)d->cus * kPhasedThreads * (Phased<IN>::RL + Phased<IN>::RR);
+    if (nvec < per_phase) return hipErrorNotSupported;
+    static int occ[2] = {-1, -1};  // per INIT variant; same on every gfx950 device
+    auto kern = init ? fedavg_phased_kernel<IN, OUT, true> : fedavg_phased_kernel<IN, OUT, false>;
+    int& o = occ[init ? 1 : 0];
+    if (o < 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kern, kPhasedThreads, 0) != hipSuccess) o = 0;
+    if (o < 1) return hipErrorNotSupported;
+    unsigned* sync = d->sync + 2 * (((uintptr_t)s >> 4) % kSyncSlots);
+    const int slack = d->cus / 32;  // the write part starts once all but ~3% of the workgroups have arrived
+    hipLaunchKernelGGL(kern, dim3((unsigned)d->cus), dim3(kPhasedThreads), 0, s, t, nc, init, out, head, nvec, n,
+                       sync, slack);
+    return hipGetLastError();
+}
+
 template <typename IN, typename OUT>
 hipError_t launch_chain_t(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
                           int64_t n, bool vector_ok, const Tuning& tu, hipStream_t s) {
+    if (vector_ok) {
+        const hipError_t e = launch_phased<IN, OUT>(t, nc, init, out, head, nvec, n, tu, s);
+        if (e != hipErrorNotSupported) return e;
+    }
     if (!vector_ok) {
         const int64_t g = grid_for(n, tu);
         if (init)

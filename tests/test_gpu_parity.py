@@ -94,6 +94,60 @@ def test_fedavg_every_tail_width(fa, O, torch_gpu, unroll):
         fa.set_tuning(unroll=before["unroll"])
 
 
+PHASE_ELEMS = 256 * 256 * 72 * 4  # one phase of the phased kernel on a 256-CU MI355X (f32 and bf16 alike)
+
+
+@pytest.mark.parametrize("in_bf16,out_bf16,D,phases,offset,use_init", [
+    (False, False, 32, 2.3, 0, False),   # north-star shape, partial last phase
+    (False, False, 3, 1.0, 1, False),    # exactly one phase (+ a misaligned head and a scalar tail)
+    (True, True, 5, 1.6, 0, False),
+    (True, False, 2, 1.2, 3, False),
+    (False, True, 4, 1.1, 0, False),
+    (False, False, 130, 1.05, 0, False),  # two passes: the second continues the chain (INIT)
+    (False, False, 6, 1.4, 0, True),     # d_init given by the caller
+])
+def test_phased_walk_same_bits(fa, O, torch_gpu, in_bf16, out_bf16, D, phases, offset, use_init):
+    """The phased kernel (walk 4: persistent grid, reads and writes separated in time) against the
+    one-shot XCD walk on the same device inputs, full buckets compared bit for bit, at sizes that
+    make whole phases, a partial last phase and a wave chunk that crosses the end of the bucket;
+    plus sampled elements against the oracle."""
+    torch = torch_gpu
+    n = int(PHASE_ELEMS * phases) + 12_345 + offset
+    w = O.weights(D)
+    seed = 900 + D
+    clients = [filled(fa, torch, n, in_bf16, seed, k, offset=offset) for k in range(D)]
+    init = None
+    if use_init:
+        init = dev_buf(torch, n, False, offset)
+        fa.fill_uniform(init, n, fa.F32, seed, 999)
+    before = fa.get_tuning()
+    outs = {}
+    try:
+        for walk in (2, 4):
+            fa.set_tuning(walk=walk)
+            out = dev_buf(torch, n, out_bf16, offset)
+            ctx = fa.Aggregator(1) if (out_bf16 and D > 128) else None
+            fa.reduce_device(clients, w, n, fa.BF16 if in_bf16 else fa.F32, out, fa.BF16 if out_bf16 else fa.F32,
+                             fa.FEDAVG, init=init, ctx=ctx)
+            torch.cuda.synchronize()
+            outs[walk] = out
+    finally:
+        fa.set_tuning(walk=before["walk"])
+    dt = torch.int16 if out_bf16 else torch.int32
+    assert torch.equal(outs[2].view(dt), outs[4].view(dt)), "phased walk differs from the one-shot walk"
+    # sampled elements against the oracle (f32 in, no init: the oracle's closed form)
+    if not in_bf16 and not use_init:
+        rng = np.random.default_rng(D)
+        idx = np.unique(np.concatenate([[0, 1, 2, n - 3, n - 2, n - 1], rng.integers(0, n, 1024)]))
+        got = outs[4][torch.as_tensor(idx, device="cuda")].cpu().numpy()
+        ref = O.fedavg_at(seed, w, idx)
+        if out_bf16:
+            assert_bits(got.view(np.uint16), O.f32_to_bf16(ref))
+        else:
+            assert_bits(got, ref)
+    del clients
+
+
 def test_fedavg_zero_elements_is_noop(fa, O, torch_gpu):
     torch = torch_gpu
     c = [dev_buf(torch, 4, False)]

@@ -124,8 +124,8 @@ for s in $STEPS; do
             rc=$?; cat "$OUT/sweep_unroll_$W.jsonl"; ok_or_fail $rc unroll_$W
         done ;;
     walk)  # grid walk sweep per workload (block 128, unroll 16, sc1 stores), 3 pools, one process
-        for W in northstar c3 c4; do
-            SWEEP_BLOCKS=128 SWEEP_STORES=3 SWEEP_UNROLLS=16 SWEEP_WALKS=1,2,3 timeout -k 10 300 python tools/sweep.py $W \
+        for W in northstar c3 c4 c5r c2; do
+            SWEEP_BLOCKS=128 SWEEP_STORES=3 SWEEP_UNROLLS=16 SWEEP_WALKS=${WALKS:-2,4} timeout -k 10 300 python tools/sweep.py $W \
                 > "$OUT/sweep_walk_$W.jsonl" 2>> "$OUT/sweep.err"
             rc=$?; cat "$OUT/sweep_walk_$W.jsonl"; ok_or_fail $rc walk_$W
         done ;;
