@@ -250,11 +250,11 @@ __global__ __launch_bounds__(256) void fedavg_chain_kernel(const ClientTable t, 
 // starts the write part once all but `slack` workgroups have arrived.
 constexpr int kPhasedThreads = 256;
 
-template <typename IN>
+template <typename IN, int REGS>
 struct Phased {  // vectors per lane per phase: LDS (160 KiB per workgroup) + registers
     static constexpr int V = In<IN>::kVec;
     static constexpr int RL = 160 * 1024 / (kPhasedThreads * V * 4);  // f32 in: 40, bf16 in: 20
-    static constexpr int RR = 128 / V;                                  // 128 VGPRs: 32 / 16
+    static constexpr int RR = REGS / V;  // REGS 128: 32 / 16 vectors (arch VGPRs); 192: 48 / 24 (+ AGPRs)
 };
 
 // The register-staged part of a phase: wave w of workgroup b owns a contiguous chunk of RR*64
@@ -312,11 +312,11 @@ __device__ __forceinline__ bool stage_regs(const ClientTable& t, int nc, const f
     return true;
 }
 
-template <typename IN, typename OUT, bool INIT>
+template <typename IN, typename OUT, bool INIT, int REGS>
 __global__ __launch_bounds__(kPhasedThreads) void fedavg_phased_kernel(const ClientTable t, int nc, const float* init,
                                                                        void* out, int64_t head, int64_t nvec, int64_t n,
                                                                        unsigned* sync, int slack) {
-    constexpr int V = In<IN>::kVec, T = kPhasedThreads, RL = Phased<IN>::RL, RR = Phased<IN>::RR;
+    constexpr int V = In<IN>::kVec, T = kPhasedThreads, RL = Phased<IN, REGS>::RL, RR = Phased<IN, REGS>::RR;
     constexpr int U = 16;
     __shared__ float buf[RL * T * V];
     chain_scalar_edges<IN, OUT, INIT>(t, nc, init, out, head, head + nvec * V, n);
@@ -613,16 +613,15 @@ PhasedDevice* phased_device() {
 // The phased kernel when it applies (walk 3 = fa_tuning.walk 4, vector path, at least one full phase
 // of work, one workgroup per CU co-resident); otherwise hipErrorNotSupported and the caller takes the
 // one-shot grid.
-template <typename IN, typename OUT>
-hipError_t launch_phased(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
-                         int64_t n, const Tuning& tu, hipStream_t s) {
-    if (tu.walk != 3) return hipErrorNotSupported;
+template <typename IN, typename OUT, int REGS>
+hipError_t launch_phased_r(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
+                           int64_t n, hipStream_t s) {
     PhasedDevice* d = phased_device();
     if (!d) return hipErrorNotSupported;
-    const int64_t per_phase = (int64_t)d->cus * kPhasedThreads * (Phased<IN>::RL + Phased<IN>::RR);
+    const int64_t per_phase = (int64_t)d->cus * kPhasedThreads * (Phased<IN, REGS>::RL + Phased<IN, REGS>::RR);
     if (nvec < per_phase) return hipErrorNotSupported;
     static int occ[2] = {-1, -1};  // per INIT variant; same on every gfx950 device
-    auto kern = init ? fedavg_phased_kernel<IN, OUT, true> : fedavg_phased_kernel<IN, OUT, false>;
+    auto kern = init ? fedavg_phased_kernel<IN, OUT, true, REGS> : fedavg_phased_kernel<IN, OUT, false, REGS>;
     int& o = occ[init ? 1 : 0];
     if (o < 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kern, kPhasedThreads, 0) != hipSuccess) o = 0;
     if (o < 1) return hipErrorNotSupported;
@@ -631,6 +630,14 @@ hipError_t launch_phased(const ClientTable& t, int nc, const float* init, void* 
     hipLaunchKernelGGL(kern, dim3((unsigned)d->cus), dim3(kPhasedThreads), 0, s, t, nc, init, out, head, nvec, n,
                        sync, slack);
     return hipGetLastError();
+}
+
+template <typename IN, typename OUT>
+hipError_t launch_phased(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
+                         int64_t n, const Tuning& tu, hipStream_t s) {
+    if (tu.walk == 3) return launch_phased_r<IN, OUT, 128>(t, nc, init, out, head, nvec, n, s);
+    if (tu.walk == 4) return launch_phased_r<IN, OUT, 192>(t, nc, init, out, head, nvec, n, s);
+    return hipErrorNotSupported;
 }
 
 template <typename IN, typename OUT>

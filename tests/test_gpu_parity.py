@@ -94,7 +94,7 @@ def test_fedavg_every_tail_width(fa, O, torch_gpu, unroll):
         fa.set_tuning(unroll=before["unroll"])
 
 
-PHASE_ELEMS = 256 * 256 * 72 * 4  # one phase of the phased kernel on a 256-CU MI355X (f32 and bf16 alike)
+PHASE_ELEMS = 256 * 256 * 72 * 4  # one phase of walk 4 on a 256-CU MI355X (f32 and bf16 alike); walk 5: x 88/72
 
 
 @pytest.mark.parametrize("in_bf16,out_bf16,D,phases,offset,use_init", [
@@ -105,6 +105,7 @@ PHASE_ELEMS = 256 * 256 * 72 * 4  # one phase of the phased kernel on a 256-CU M
     (False, True, 4, 1.1, 0, False),
     (False, False, 130, 1.05, 0, False),  # two passes: the second continues the chain (INIT)
     (False, False, 6, 1.4, 0, True),     # d_init given by the caller
+    (False, False, 7, 1.25, 2, False),   # just over one phase of walk 5
 ])
 def test_phased_walk_same_bits(fa, O, torch_gpu, in_bf16, out_bf16, D, phases, offset, use_init):
     """The phased kernel (walk 4: persistent grid, reads and writes separated in time) against the
@@ -123,7 +124,7 @@ def test_phased_walk_same_bits(fa, O, torch_gpu, in_bf16, out_bf16, D, phases, o
     before = fa.get_tuning()
     outs = {}
     try:
-        for walk in (2, 4):
+        for walk in (2, 4, 5):
             fa.set_tuning(walk=walk)
             out = dev_buf(torch, n, out_bf16, offset)
             ctx = fa.Aggregator(1) if (out_bf16 and D > 128) else None
@@ -134,7 +135,8 @@ def test_phased_walk_same_bits(fa, O, torch_gpu, in_bf16, out_bf16, D, phases, o
     finally:
         fa.set_tuning(walk=before["walk"])
     dt = torch.int16 if out_bf16 else torch.int32
-    assert torch.equal(outs[2].view(dt), outs[4].view(dt)), "phased walk differs from the one-shot walk"
+    for walk in (4, 5):
+        assert torch.equal(outs[2].view(dt), outs[walk].view(dt)), "phased walk %d differs from walk 2" % walk
     # sampled elements against the oracle (f32 in, no init: the oracle's closed form)
     if not in_bf16 and not use_init:
         rng = np.random.default_rng(D)
