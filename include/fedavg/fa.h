@@ -186,10 +186,12 @@ typedef struct {
                              timed and the fastest kept; -1 = 1 (no probing); default 8 */
     int walk;         /* FedAvg grid walk over a bucket: 1 linear, 2 each XCD's workgroups own one contiguous
                          eighth, 3 the same with the odd eighths walked backwards (one-shot grid only),
-                         4 phased (default): a persistent grid reduces a phase into LDS and registers,
-                         then writes it, so the output never streams beside the inputs; buckets smaller
-                         than one phase (~5.8 M f32 / 11.5 M bf16 elements) take walk 2.  The phased
-                         kernel always uses nt loads and sc1 stores */
+                         4 phased: a persistent grid (one workgroup per CU) reduces a phase into LDS and
+                         registers, then writes it, so the output never streams beside the inputs,
+                         5 (default) phased with a larger register stage (fewer phases).  Buckets
+                         smaller than one phase (walk 4: 18.9 M, walk 5: 23.1 M elements per GPU on
+                         256 CUs, f32 or bf16) take walk 2.  The phased kernels always use nt loads
+                         and sc1 stores */
 } fa_tuning;
 int fa_set_tuning(const fa_tuning* t);
 int fa_get_tuning(fa_tuning* t);

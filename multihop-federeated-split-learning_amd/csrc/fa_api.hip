@@ -38,9 +38,11 @@ thread_local std::string g_err;
 // tools/sweep.py over 3 pools (profiles/r01_summary.json): sc1 stores 2.7% faster than nt,
 // unroll 16 ~1% faster than 8, block 128 2-3% faster than 256; XCD-eighths walk 0.5-1.5% faster than
 // linear in 7 of 9 pools over the north star, C3 and C4 (gpurun_out r01s11, profiles/r01_summary.json).
-// Default walk: phased (fa_kernels.hip, fedavg_phased_kernel) wherever a bucket holds a full phase,
-// the XCD-eighths one-shot grid below that.
-fa::Tuning g_tuning{128, 0, 16, 1, 2, 3};
+// Default walk: phased with the larger register stage (fa_kernels.hip, fedavg_phased_kernel) wherever
+// a bucket holds a full phase, the XCD-eighths one-shot grid below that: in one process over 3 pools
+// each (gpurun_out r01s18) 1.269 ms north star in every pool (XCD walk 1.42 there: all slow pools),
+// and ahead of the XCD walk on C3, C4 and C5's per-rank share too.
+fa::Tuning g_tuning{128, 0, 16, 1, 2, 4};
 // Byte skew between consecutive client slots of one bucket (see slot_stride).
 size_t g_slot_skew = 2048;
 // Placement probing of large FedAvg bucket pools (see alloc_placed): at most this many candidates.
@@ -356,7 +358,10 @@ int probe_pool(fa_ctx* ctx, int g, const Part& p, size_t stride, char* pool, flo
 
 int alloc_placed(fa_ctx* ctx, int g, Part& p, size_t stride, size_t bytes, char** out) {
     const size_t algo = (size_t)p.D * p.cnt[(size_t)g] * dsize(p.in) + p.cnt[(size_t)g] * dsize(p.out);
-    const int probes = (p.mode == FA_FEDAVG && bytes >= kProbeMinBytes && p.cnt[(size_t)g] > 0)
+    // The phased walk runs at the same speed in every pool: a part it covers needs no probe.
+    const int64_t phased_from = fa::phased_min_elems(p.in, g_tuning);
+    const bool phased = phased_from > 0 && (int64_t)p.cnt[(size_t)g] >= phased_from;
+    const int probes = (p.mode == FA_FEDAVG && !phased && bytes >= kProbeMinBytes && p.cnt[(size_t)g] > 0)
                            ? std::max(1, g_placement_probes) : 1;
     std::vector<char*> cand;
     std::vector<float>& ms = p.probe_ms[(size_t)g];

@@ -25,11 +25,13 @@ struct Tuning {
     int store_policy; // 0 plain, 1 nt, 2 sc1 (write-through), 3 sc0 sc1
     int walk;         // FedAvg grid walk: 0 linear, 1 XCD eighths, 2 XCD eighths, odd ones reversed,
                       // 3 phased (persistent grid, reads and writes separated in time; XCD eighths
-                      // for buckets smaller than one phase)
+                      // for buckets smaller than one phase), 4 phased with the larger register stage
 };
 
 hipError_t launch_chain(const ClientTable& t, int nc, fa_dtype in, fa_dtype out, const float* init, void* dst,
                         int64_t head, int64_t nvec, int64_t n, bool vector_ok, const Tuning& tu, hipStream_t s);
+// Elements per GPU from which the phased walk applies (0: not in use); see fa_kernels.hip.
+int64_t phased_min_elems(fa_dtype in, const Tuning& tu);
 hipError_t launch_literal(const void* x, fa_dtype in, void* dst, fa_dtype out, float divisor, int64_t head,
                           int64_t nvec, int64_t n, bool vector_ok, const Tuning& tu, hipStream_t s);
 // In-place state sync: every slot t.src[0..nc) := the chain over them (continuing `init` if given).

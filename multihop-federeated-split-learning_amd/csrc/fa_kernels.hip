@@ -239,10 +239,11 @@ __global__ __launch_bounds__(256) void fedavg_chain_kernel(const ClientTable t, 
 // read/write turnaround -- which of the two a pool gets depends only on where the allocation of the
 // INPUTS lands physically (tools/exp_slow.hip, exp_cross.hip).  Here a persistent grid
 // (one 256-thread workgroup per CU) works in phases: every lane reduces RL vectors into LDS (160 KiB
-// per CU) and RR more into VGPRs, the workgroups meet at a chip-wide counter, then all of them write
-// the phase's results.  Three phases cover the north star; it runs at the fast pools' speed in every
-// pool (tools/exp_phase3.hip: 1.274-1.279 ms against 1.273-1.276 fast / 1.42 slow for the linear
-// walk).  Results are bit-identical: the phases only reorder stores in time.
+// per CU) and RR more into registers, the workgroups meet at a chip-wide counter, then all of them
+// write the phase's results.  With the larger register stage (REGS 192, walk 5) three phases cover
+// the north star, and it runs at 1.268-1.270 ms in every pool (gpurun_out r01s18: the one-shot XCD
+// walk took 1.42 ms in the same, slow, pools; 1.27-1.30 in fast ones).  Results are bit-identical:
+// the phases only reorder stores in time.
 //
 // The counter pair sync[0] (arrivals) / sync[1] (departures) starts at zero; the last workgroup to
 // leave resets both, so the next launch on the stream finds them zero again.  The wait is bounded
@@ -632,6 +633,18 @@ hipError_t launch_phased_r(const ClientTable& t, int nc, const float* init, void
     return hipGetLastError();
 }
 
+// Smallest bucket (elements of dtype `in` per GPU) that the phased walk of `tu` takes on the current
+// device, or 0 when the phased kernel is not in use.
+int64_t phased_min_elems_impl(fa_dtype in, const Tuning& tu) {
+    if (tu.walk != 3 && tu.walk != 4) return 0;
+    PhasedDevice* d = phased_device();
+    if (!d) return 0;
+    const int regs = tu.walk == 3 ? 128 : 192;
+    const int V = in == FA_F32 ? 4 : 8;
+    const int rl = 160 * 1024 / (kPhasedThreads * V * 4), rr = regs / V;
+    return (int64_t)d->cus * kPhasedThreads * (rl + rr) * V;
+}
+
 template <typename IN, typename OUT>
 hipError_t launch_phased(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
                          int64_t n, const Tuning& tu, hipStream_t s) {
@@ -662,6 +675,8 @@ hipError_t launch_chain_t(const ClientTable& t, int nc, const float* init, void*
 }
 
 }  // namespace
+
+int64_t phased_min_elems(fa_dtype in, const Tuning& tu) { return phased_min_elems_impl(in, tu); }
 
 hipError_t launch_chain(const ClientTable& t, int nc, fa_dtype in, fa_dtype outdt, const float* init, void* out,
                         int64_t head, int64_t nvec, int64_t n, bool vector_ok, const Tuning& tu, hipStream_t s) {

@@ -501,20 +501,23 @@ def test_context_zero_copy_gather_in_and_out(fa, O, torch_gpu, pinned, gpus):
 
 
 def test_placement_probing_keeps_bits_and_records(fa, O, torch_gpu):
-    """A >= 1 GiB FedAvg pool is placed by probing (fa_bucket_define): the record lists the candidates'
-    probe times and the kept one is the fastest; results stay bit-exact; probing off gives no record."""
+    """A >= 1 GiB FedAvg pool is placed by probing (fa_bucket_define) under a one-shot walk: the record
+    lists the candidates' probe times and the kept one is the fastest; results stay bit-exact; probing
+    off gives no record.  Under the phased walk (same speed in every pool) the pool is not probed."""
     n, D = 80_000_000, 4  # 4 x 320 MB slots + output: 1.6 GB pool
     w = O.weights(D)
     idx = np.unique(np.concatenate([np.arange(0, 4096), np.arange(n - 4096, n),
                                     np.random.default_rng(5).integers(0, n, 4096)]))
     before = fa.get_tuning()
     try:
-        for probes in (3, -1):
-            fa.set_tuning(placement_probes=probes)
+        for probes, walk in ((3, 2), (-1, 2), (3, 5)):
+            fa.set_tuning(placement_probes=probes, walk=walk)
             with fa.Aggregator(1) as agg:
                 agg.define(1, n, fa.F32, fa.F32, D, fa.FEDAVG)
                 rec = agg.placement(1)
-                if probes > 0:
+                if walk == 5:
+                    assert rec["probe_ms"] == []
+                elif probes > 0:
                     assert 1 <= len(rec["probe_ms"]) <= probes
                     assert rec["probe_ms"][rec["chosen"]] == min(rec["probe_ms"])
                 else:
@@ -528,4 +531,4 @@ def test_placement_probing_keeps_bits_and_records(fa, O, torch_gpu):
                 agg.copy_output(1, out)
                 assert_bits(out[idx], O.fedavg_at(71, w, idx))
     finally:
-        fa.set_tuning(placement_probes=before["placement_probes"])
+        fa.set_tuning(placement_probes=before["placement_probes"], walk=before["walk"])

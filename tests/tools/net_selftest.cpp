@@ -1,8 +1,9 @@
 // net_selftest.cpp -- TEST TOOL (CPU): the aggregator's network layer and frame buffers without a GPU.
 //  * D senders push frames at once (one connection each) into one NetLayer; every receipt arrives
 //    once, intact, with its header fields (concurrent per-connection readers);
-//  * frame buffers come from a BufferPool: after the first round no new allocation happens
-//    (recycling), and receipts carry the pool's `pinned` tag;
+//  * frame buffers come from a BufferPool that recycles them: over all rounds it never holds more
+//    buffers than one round can have alive at once (D sender frames + D received frames; without
+//    recycling 3 rounds would allocate 3x that), and receipts carry the pool's `pinned` tag;
 //  * a frame queued for several destinations reaches each of them (serialize-once fan-out), in
 //    order per destination;
 //  * TorchArchive::layout_into + seal_params == with_params_into on a real archive (optional arg).
@@ -61,7 +62,6 @@ int main(int argc, char** argv) {
         std::cerr << "bind failed\n";
         return 1;
     }
-    size_t allocs_after_first = 0;
     for (int r = 0; r < rounds; ++r) {
         std::vector<std::shared_ptr<Bytes>> frames;
         for (int k = 0; k < D; ++k) frames.push_back(make_frame(100 + k, 2 + (k % 2), payload, (uint8_t)(r * 31 + k)));
@@ -103,11 +103,13 @@ int main(int argc, char** argv) {
                     break;
                 }
         }
-        if (r == 0) allocs_after_first = pool->allocations();
     }
+    // How many buffers round 0 needed depends on timing (a receipt dropped early lends its buffer to a
+    // reader still receiving), so the bound is the most a round can hold at once, not round 0's count.
     const size_t allocs = pool->allocations();
-    if (allocs != allocs_after_first) {  // rounds 2.. reuse the first round's buffers
-        std::cerr << "pool allocated " << allocs - allocs_after_first << " buffers after round 1\n";
+    if (allocs > (size_t)(2 * D)) {
+        std::cerr << "pool allocated " << allocs << " buffers over " << rounds << " rounds (at most " << 2 * D
+                  << " can be alive at once)\n";
         ok = false;
     }
 
