@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
 #include <mutex>
 #include <type_traits>
 
@@ -620,7 +621,12 @@ hipError_t launch_phased_r(const ClientTable& t, int nc, const float* init, void
     PhasedDevice* d = phased_device();
     if (!d) return hipErrorNotSupported;
     const int64_t per_phase = (int64_t)d->cus * kPhasedThreads * (Phased<IN, REGS>::RL + Phased<IN, REGS>::RR);
-    if (nvec < per_phase) return hipErrorNotSupported;
+    // experiment knob (tools/): FA_PHASED_MIN_VECS lowers the smallest bucket the phased kernel takes
+    static const int64_t min_env = [] {
+        const char* e = std::getenv("FA_PHASED_MIN_VECS");
+        return e ? (int64_t)std::atoll(e) : (int64_t)-1;
+    }();
+    if (nvec < (min_env >= 0 ? min_env : per_phase)) return hipErrorNotSupported;
     static int occ[2] = {-1, -1};  // per INIT variant; same on every gfx950 device
     auto kern = init ? fedavg_phased_kernel<IN, OUT, true, REGS> : fedavg_phased_kernel<IN, OUT, false, REGS>;
     int& o = occ[init ? 1 : 0];
