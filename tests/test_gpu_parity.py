@@ -532,3 +532,54 @@ def test_placement_probing_keeps_bits_and_records(fa, O, torch_gpu):
                 assert_bits(out[idx], O.fedavg_at(71, w, idx))
     finally:
         fa.set_tuning(placement_probes=before["placement_probes"], walk=before["walk"])
+
+
+# ----------------------------------------------------------------- IEEE special values
+
+def _special_clients(D, n, seed):
+    """Client buckets mixing ordinary values with +-0, +-Inf, NaNs, subnormals and values whose
+    weighted sums land in the subnormal range or overflow (a diverged or a vanishing parameter)."""
+    rng = np.random.default_rng(seed)
+    specials = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e-45, -1e-45, 1.1754942e-38, 1e-39, -3e-39,
+                         1.17549435e-38, 3.4e38, -3.4e38, 1e-30, 1e30], np.float32)
+    xs = []
+    for k in range(D):
+        x = rng.uniform(-1, 1, n).astype(np.float32)
+        pick = rng.random(n) < 0.3
+        x[pick] = specials[rng.integers(0, specials.size, int(pick.sum()))]
+        xs.append(x)
+    return xs
+
+
+def _assert_bits_nan_aware(got, ref):
+    """Bit-exact, except that a NaN only has to be a NaN (x86 and CDNA FMAs may pick different NaN payloads)."""
+    gn, rn = np.isnan(got), np.isnan(ref)
+    assert np.array_equal(gn, rn), "NaN positions differ: %d vs %d" % (gn.sum(), rn.sum())
+    assert_bits(got[~gn], ref[~rn])
+
+
+@pytest.mark.parametrize("D", [3, 17])
+def test_special_values_fedavg_and_literal(fa, O, torch_gpu, D):
+    torch = torch_gpu
+    n = 50_003
+    xs = _special_clients(D, n, 41 + D)
+    for w in (O.weights(D), np.array([1e-30 if k % 2 else 0.75 for k in range(D)], np.float32)):
+        ref = O.fedavg(xs, w)
+        clients = [torch.from_numpy(x).to("cuda") for x in xs]
+        out = torch.empty(n, dtype=torch.float32, device="cuda")
+        fa.reduce_device(clients, w, n, fa.F32, out, fa.F32)
+        torch.cuda.synchronize()
+        _assert_bits_nan_aware(out.cpu().numpy(), ref)
+        # bf16 output of the same chain (one rounding at the end)
+        outb = torch.empty(n, dtype=torch.int16, device="cuda")
+        fa.reduce_device(clients, w, n, fa.F32, outb, fa.BF16)
+        torch.cuda.synchronize()
+        gb = outb.cpu().numpy().view(np.uint16)
+        rb = O.f32_to_bf16(ref)
+        nan_b = ((gb & 0x7FFF) > 0x7F80)
+        assert np.array_equal(nan_b, (rb & 0x7FFF) > 0x7F80)
+        assert np.array_equal(gb[~nan_b], rb[~nan_b])
+    lit = torch.empty(n, dtype=torch.float32, device="cuda")
+    fa.reduce_device(clients, np.zeros(D, np.float32), n, fa.F32, lit, fa.F32, fa.LITERAL)
+    torch.cuda.synchronize()
+    _assert_bits_nan_aware(lit.cpu().numpy(), O.literal(xs[-1]))
