@@ -388,6 +388,18 @@ def main():
                           "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                           "input_sets_rotated": s.nsets}
         s.close()
+        # the same on a large part: 8 copies of VGG-19's FC part (119.6 M parameters, C4's split 3,19)
+        s = SyncSetup(fa, torch, 8, 119_586_826, "f32", "f32", 0, device)
+        torch.cuda.synchronize()
+        w2, km = timed_loop(torch, s, max(10, args.steps), 3, stream, dist, barrier)
+        ka = statistics.mean(km)
+        sec["sync_vgg_fc"] = {"description": "compute-node state sync, 8 client copies of VGG-19's FC part "
+                                             "(119.6 M fp32 parameters), in place",
+                              "kernel_ms_avg": round(ka, 4),
+                              "achieved_GBs": round(s.algo_bytes() / (ka * 1e-3) / 1e9, 1),
+                              "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                              "input_sets_rotated": s.nsets}
+        s.close()
         line["secondary"] = sec
 
     if rank == 0:

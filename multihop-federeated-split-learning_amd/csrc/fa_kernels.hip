@@ -314,14 +314,39 @@ __device__ __forceinline__ bool stage_regs(const ClientTable& t, int nc, const f
     return true;
 }
 
-template <typename IN, typename OUT, bool INIT, int REGS>
+template <typename T, bool INIT>
+__device__ __forceinline__ void sync_scalar_edges(const ClientTable& t, int nc, const float* init, int64_t head,
+                                                  int64_t tail0, int64_t n) {
+    if (blockIdx.x != 0) return;
+    const int64_t n_tail = n - tail0;
+    for (int64_t s = threadIdx.x; s < head + n_tail; s += blockDim.x) {
+        const int64_t i = s < head ? s : tail0 + (s - head);
+        float acc = INIT ? init[i] : 0.0f;
+        for (int k = 0; k < nc; ++k) acc = __builtin_fmaf(In<T>::scalar(t.src[k], i), t.w[k], acc);
+        for (int k = 0; k < nc; ++k) Out<T>::scalar(const_cast<void*>(t.src[k]), i, acc);
+    }
+}
+
+// A reduced vector leaves the phased kernel: to the output, or (SYNC, compute-node state sync) back to
+// every client slot in place.
+template <typename OUT, int V, bool SYNC>
+__device__ __forceinline__ void put(const ClientTable& t, int nc, void* out, int64_t e, const float* acc) {
+    if constexpr (SYNC) {
+        for (int k = 0; k < nc; ++k) Out<OUT>::template store<V, kStSc1>(const_cast<void*>(t.src[k]), e, acc);
+    } else {
+        Out<OUT>::template store<V, kStSc1>(out, e, acc);
+    }
+}
+
+template <typename IN, typename OUT, bool INIT, int REGS, bool SYNC = false>
 __global__ __launch_bounds__(kPhasedThreads) void fedavg_phased_kernel(const ClientTable t, int nc, const float* init,
                                                                        void* out, int64_t head, int64_t nvec, int64_t n,
                                                                        unsigned* sync, int slack) {
     constexpr int V = In<IN>::kVec, T = kPhasedThreads, RL = Phased<IN, REGS>::RL, RR = Phased<IN, REGS>::RR;
     constexpr int U = 16;
     __shared__ float buf[RL * T * V];
-    chain_scalar_edges<IN, OUT, INIT>(t, nc, init, out, head, head + nvec * V, n);
+    if constexpr (SYNC) sync_scalar_edges<IN, INIT>(t, nc, init, head, head + nvec * V, n);
+    else chain_scalar_edges<IN, OUT, INIT>(t, nc, init, out, head, head + nvec * V, n);
     const int64_t G = gridDim.x;
     const int64_t per_phase = G * T * (RL + RR);
     const int phases = (int)((nvec + per_phase - 1) / per_phase);
@@ -348,7 +373,7 @@ __global__ __launch_bounds__(kPhasedThreads) void fedavg_phased_kernel(const Cli
                 if (v < nvec) {
                     float acc[V];
                     chain_vec<IN, U, true, INIT>(t, nc, init, head + v * V, acc);
-                    Out<OUT>::template store<V, kStSc1>(out, head + v * V, acc);
+                    put<OUT, V, SYNC>(t, nc, out, head + v * V, acc);
                 }
             }
         }
@@ -365,12 +390,12 @@ __global__ __launch_bounds__(kPhasedThreads) void fedavg_phased_kernel(const Cli
 #pragma unroll 1
         for (int i = 0; i < RL; ++i) {
             const int64_t v = base + (int64_t)i * G * T;
-            if (v < nvec) Out<OUT>::template store<V, kStSc1>(out, head + v * V, &buf[(i * T + threadIdx.x) * V]);
+            if (v < nvec) put<OUT, V, SYNC>(t, nc, out, head + v * V, &buf[(i * T + threadIdx.x) * V]);
         }
         if (staged) {
             const int64_t c = c0 + (threadIdx.x & 63);
 #pragma unroll
-            for (int r = 0; r < RR; ++r) Out<OUT>::template store<V, kStSc1>(out, head + (c + r * 64) * V, keep[r]);
+            for (int r = 0; r < RR; ++r) put<OUT, V, SYNC>(t, nc, out, head + (c + r * 64) * V, keep[r]);
         }
     }
     if (threadIdx.x == 0 &&
@@ -400,19 +425,6 @@ __global__ __launch_bounds__(256) void fedavg_chain_scalar_kernel(const ClientTa
 // nc client slots, runs the same ordered FMA chain, and writes the rounded result back to every
 // slot (all reads of a vector precede its writes, so aliasing input and output is safe).
 // Per element: nc*s reads + nc*s writes.
-
-template <typename T, bool INIT>
-__device__ __forceinline__ void sync_scalar_edges(const ClientTable& t, int nc, const float* init, int64_t head,
-                                                  int64_t tail0, int64_t n) {
-    if (blockIdx.x != 0) return;
-    const int64_t n_tail = n - tail0;
-    for (int64_t s = threadIdx.x; s < head + n_tail; s += blockDim.x) {
-        const int64_t i = s < head ? s : tail0 + (s - head);
-        float acc = INIT ? init[i] : 0.0f;
-        for (int k = 0; k < nc; ++k) acc = __builtin_fmaf(In<T>::scalar(t.src[k], i), t.w[k], acc);
-        for (int k = 0; k < nc; ++k) Out<T>::scalar(const_cast<void*>(t.src[k]), i, acc);
-    }
-}
 
 template <typename T, int U, int SP, bool INIT>
 __global__ __launch_bounds__(256) void fedavg_sync_kernel(const ClientTable t, int nc, const float* init,
@@ -735,9 +747,32 @@ hipError_t launch_sync_sp(const ClientTable& t, int nc, const float* init, int64
     return hipGetLastError();
 }
 
+// The phased kernel in state-sync form (no init: sync_on chains more than kMaxClients slots into
+// scratch and broadcasts instead).
+template <typename T, int REGS>
+hipError_t launch_sync_phased_r(const ClientTable& t, int nc, int64_t head, int64_t nvec, int64_t n, hipStream_t s) {
+    PhasedDevice* d = phased_device();
+    if (!d) return hipErrorNotSupported;
+    const int64_t per_phase = (int64_t)d->cus * kPhasedThreads * (Phased<T, REGS>::RL + Phased<T, REGS>::RR);
+    if (nvec < per_phase) return hipErrorNotSupported;
+    static int occ = -1;
+    auto kern = fedavg_phased_kernel<T, T, false, REGS, true>;
+    if (occ < 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kPhasedThreads, 0) != hipSuccess) occ = 0;
+    if (occ < 1) return hipErrorNotSupported;
+    unsigned* sync = d->sync + 2 * (((uintptr_t)s >> 4) % kSyncSlots);
+    hipLaunchKernelGGL(kern, dim3((unsigned)d->cus), dim3(kPhasedThreads), 0, s, t, nc, (const float*)nullptr,
+                       (void*)nullptr, head, nvec, n, sync, d->cus / 32);
+    return hipGetLastError();
+}
+
 template <typename T>
 hipError_t launch_sync_t(const ClientTable& t, int nc, const float* init, int64_t head, int64_t nvec, int64_t n,
                          bool vector_ok, const Tuning& tu, hipStream_t s) {
+    if (vector_ok && !init && (tu.walk == 3 || tu.walk == 4)) {
+        const hipError_t e = tu.walk == 3 ? launch_sync_phased_r<T, 128>(t, nc, head, nvec, n, s)
+                                          : launch_sync_phased_r<T, 192>(t, nc, head, nvec, n, s);
+        if (e != hipErrorNotSupported) return e;
+    }
     if (!vector_ok) {
         const int64_t g = grid_for(n, tu);
         if (init)

@@ -164,3 +164,39 @@ def test_client_states_on_gpu(fa, O, torch_gpu):
     for c in ids:
         got = torch.cat([p.detach().reshape(-1) for p in mods[c].parameters()]).cpu().numpy()
         assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D,bf16,phases", [(4, False, 1.3), (3, True, 2.2), (9, False, 1.05)])
+def test_sync_phased_same_bits(fa, O, torch_gpu, D, bf16, phases):
+    """The phased kernel in state-sync form (walk 5) against the one-shot sync (walk 2): every slot of
+    buckets of one to a few phases, bit for bit, plus sampled elements against the oracle."""
+    torch = torch_gpu
+    n = int(256 * 256 * 88 * 4 * phases) + 4_321
+    w = O.weights(D)
+    dt = fa.BF16 if bf16 else fa.F32
+    tdt = torch.int16 if bf16 else torch.float32
+    before = fa.get_tuning()
+    res = {}
+    try:
+        for walk in (2, 5):
+            fa.set_tuning(walk=walk)
+            dev = [torch.empty(n, dtype=tdt, device="cuda") for _ in range(D)]
+            for k, d in enumerate(dev):
+                fa.fill_uniform(d, n, dt, 62, k)
+            fa.sync_device(dev, w, n, dt)
+            torch.cuda.synchronize()
+            res[walk] = dev
+    finally:
+        fa.set_tuning(walk=before["walk"])
+    for k in range(D):
+        assert torch.equal(res[2][k], res[5][k]), "slot %d differs" % k
+        if k:
+            assert torch.equal(res[5][0], res[5][k])
+    idx = np.unique(np.concatenate([[0, 1, n - 2, n - 1], np.random.default_rng(D).integers(0, n, 512)]))
+    got = res[5][0][torch.as_tensor(idx, device="cuda")].cpu().numpy()
+    ref = O.fedavg_at(62, w, idx, bf16=bf16)
+    if bf16:
+        assert np.array_equal(got.view(np.uint16), O.f32_to_bf16(ref))
+    else:
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
