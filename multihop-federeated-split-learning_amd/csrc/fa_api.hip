@@ -662,7 +662,7 @@ int fa_set_tuning(const fa_tuning* t) {
         skew = t->slot_skew < 0 ? 0 : (size_t)t->slot_skew;
     }
     if (t->walk) {
-        if (t->walk < 1 || t->walk > 5) return fail(FA_ERR_ARG, "walk must be 1..5");
+        if (t->walk < 1 || t->walk > 6) return fail(FA_ERR_ARG, "walk must be 1..6");
         nt.walk = t->walk - 1;
     }
     int probes = g_placement_probes;

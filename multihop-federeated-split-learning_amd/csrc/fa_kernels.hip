@@ -252,10 +252,10 @@ __global__ __launch_bounds__(256) void fedavg_chain_kernel(const ClientTable t, 
 // starts the write part once all but `slack` workgroups have arrived.
 constexpr int kPhasedThreads = 256;
 
-template <typename IN, int REGS>
+template <typename IN, int REGS, int TH = kPhasedThreads>
 struct Phased {  // vectors per lane per phase: LDS (160 KiB per workgroup) + registers
     static constexpr int V = In<IN>::kVec;
-    static constexpr int RL = 160 * 1024 / (kPhasedThreads * V * 4);  // f32 in: 40, bf16 in: 20
+    static constexpr int RL = 160 * 1024 / (TH * V * 4);  // 256 threads: f32 in 40, bf16 in 20
     static constexpr int RR = REGS / V;  // REGS 128: 32 / 16 vectors (arch VGPRs); 192: 48 / 24 (+ AGPRs)
 };
 
@@ -267,10 +267,10 @@ struct Phased {  // vectors per lane per phase: LDS (160 KiB per workgroup) + re
 // constant, so a load needs no per-vector address registers: keep[] (128 VGPRs) and 16 loads in
 // flight fit the 256 architectural VGPRs.  Returns false (nothing staged) for a wave whose chunk
 // runs past the end of the bucket; the caller reduces and stores those vectors directly.
-template <typename IN, bool INIT, int RR>
+template <typename IN, bool INIT, int RR, int G16>
 __device__ __forceinline__ bool stage_regs(const ClientTable& t, int nc, const float* init, int64_t head, int64_t c0,
                                            int64_t nvec, float (&keep)[RR][In<IN>::kVec]) {
-    constexpr int V = In<IN>::kVec, G16 = 16;
+    constexpr int V = In<IN>::kVec;
     if (c0 + (int64_t)RR * 64 > nvec) return false;
     const int lane = threadIdx.x & 63;
     const int64_t ubase = (head + c0 * V) * (int64_t)sizeof(IN);      // wave-uniform
@@ -338,12 +338,12 @@ __device__ __forceinline__ void put(const ClientTable& t, int nc, void* out, int
     }
 }
 
-template <typename IN, typename OUT, bool INIT, int REGS, bool SYNC = false>
-__global__ __launch_bounds__(kPhasedThreads) void fedavg_phased_kernel(const ClientTable t, int nc, const float* init,
+template <typename IN, typename OUT, bool INIT, int REGS, bool SYNC, int TH>
+__global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, int nc, const float* init,
                                                                        void* out, int64_t head, int64_t nvec, int64_t n,
                                                                        unsigned* sync, int slack) {
-    constexpr int V = In<IN>::kVec, T = kPhasedThreads, RL = Phased<IN, REGS>::RL, RR = Phased<IN, REGS>::RR;
-    constexpr int U = 16;
+    constexpr int V = In<IN>::kVec, T = TH, RL = Phased<IN, REGS, TH>::RL, RR = Phased<IN, REGS, TH>::RR;
+    constexpr int U = TH > 256 ? 8 : 16;  // loads in flight per wave (2 waves per SIMD at 512 threads)
     __shared__ float buf[RL * T * V];
     if constexpr (SYNC) sync_scalar_edges<IN, INIT>(t, nc, init, head, head + nvec * V, n);
     else chain_scalar_edges<IN, OUT, INIT>(t, nc, init, out, head, head + nvec * V, n);
@@ -366,7 +366,7 @@ __global__ __launch_bounds__(kPhasedThreads) void fedavg_phased_kernel(const Cli
         const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
         const int64_t c0 = (int64_t)p * per_phase + G * T * RL + ((int64_t)blockIdx.x * (T / 64) + wave) * RR * 64;
         float keep[RR][V];
-        const bool staged = stage_regs<IN, INIT, RR>(t, nc, init, head, c0, nvec, keep);
+        const bool staged = stage_regs<IN, INIT, RR, U>(t, nc, init, head, c0, nvec, keep);
         if (!staged) {  // the chunk that holds the end of the bucket (or lies past it): no staging
             for (int r = 0; r < RR; ++r) {
                 const int64_t v = c0 + r * 64 + (threadIdx.x & 63);
@@ -627,12 +627,12 @@ PhasedDevice* phased_device() {
 // The phased kernel when it applies (walk 3 = fa_tuning.walk 4, vector path, at least one full phase
 // of work, one workgroup per CU co-resident); otherwise hipErrorNotSupported and the caller takes the
 // one-shot grid.
-template <typename IN, typename OUT, int REGS>
+template <typename IN, typename OUT, int REGS, int TH>
 hipError_t launch_phased_r(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
                            int64_t n, hipStream_t s) {
     PhasedDevice* d = phased_device();
     if (!d) return hipErrorNotSupported;
-    const int64_t per_phase = (int64_t)d->cus * kPhasedThreads * (Phased<IN, REGS>::RL + Phased<IN, REGS>::RR);
+    const int64_t per_phase = (int64_t)d->cus * TH * (Phased<IN, REGS, TH>::RL + Phased<IN, REGS, TH>::RR);
     // experiment knob (tools/): FA_PHASED_MIN_VECS lowers the smallest bucket the phased kernel takes
     static const int64_t min_env = [] {
         const char* e = std::getenv("FA_PHASED_MIN_VECS");
@@ -640,13 +640,13 @@ hipError_t launch_phased_r(const ClientTable& t, int nc, const float* init, void
     }();
     if (nvec < (min_env >= 0 ? min_env : per_phase)) return hipErrorNotSupported;
     static int occ[2] = {-1, -1};  // per INIT variant; same on every gfx950 device
-    auto kern = init ? fedavg_phased_kernel<IN, OUT, true, REGS> : fedavg_phased_kernel<IN, OUT, false, REGS>;
+    auto kern = init ? fedavg_phased_kernel<IN, OUT, true, REGS, false, TH> : fedavg_phased_kernel<IN, OUT, false, REGS, false, TH>;
     int& o = occ[init ? 1 : 0];
-    if (o < 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kern, kPhasedThreads, 0) != hipSuccess) o = 0;
+    if (o < 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kern, TH, 0) != hipSuccess) o = 0;
     if (o < 1) return hipErrorNotSupported;
     unsigned* sync = d->sync + 2 * (((uintptr_t)s >> 4) % kSyncSlots);
     const int slack = d->cus / 32;  // the write part starts once all but ~3% of the workgroups have arrived
-    hipLaunchKernelGGL(kern, dim3((unsigned)d->cus), dim3(kPhasedThreads), 0, s, t, nc, init, out, head, nvec, n,
+    hipLaunchKernelGGL(kern, dim3((unsigned)d->cus), dim3(TH), 0, s, t, nc, init, out, head, nvec, n,
                        sync, slack);
     return hipGetLastError();
 }
@@ -654,20 +654,21 @@ hipError_t launch_phased_r(const ClientTable& t, int nc, const float* init, void
 // Smallest bucket (elements of dtype `in` per GPU) that the phased walk of `tu` takes on the current
 // device, or 0 when the phased kernel is not in use.
 int64_t phased_min_elems_impl(fa_dtype in, const Tuning& tu) {
-    if (tu.walk != 3 && tu.walk != 4) return 0;
+    if (tu.walk < 3 || tu.walk > 5) return 0;
     PhasedDevice* d = phased_device();
     if (!d) return 0;
-    const int regs = tu.walk == 3 ? 128 : 192;
+    const int regs = tu.walk == 4 ? 192 : tu.walk == 5 ? 96 : 128, th = tu.walk == 5 ? 512 : kPhasedThreads;
     const int V = in == FA_F32 ? 4 : 8;
-    const int rl = 160 * 1024 / (kPhasedThreads * V * 4), rr = regs / V;
-    return (int64_t)d->cus * kPhasedThreads * (rl + rr) * V;
+    const int rl = 160 * 1024 / (th * V * 4), rr = regs / V;
+    return (int64_t)d->cus * th * (rl + rr) * V;
 }
 
 template <typename IN, typename OUT>
 hipError_t launch_phased(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
                          int64_t n, const Tuning& tu, hipStream_t s) {
-    if (tu.walk == 3) return launch_phased_r<IN, OUT, 128>(t, nc, init, out, head, nvec, n, s);
-    if (tu.walk == 4) return launch_phased_r<IN, OUT, 192>(t, nc, init, out, head, nvec, n, s);
+    if (tu.walk == 3) return launch_phased_r<IN, OUT, 128, 256>(t, nc, init, out, head, nvec, n, s);
+    if (tu.walk == 4) return launch_phased_r<IN, OUT, 192, 256>(t, nc, init, out, head, nvec, n, s);
+    if (tu.walk == 5) return launch_phased_r<IN, OUT, 96, 512>(t, nc, init, out, head, nvec, n, s);
     return hipErrorNotSupported;
 }
 
@@ -749,18 +750,18 @@ hipError_t launch_sync_sp(const ClientTable& t, int nc, const float* init, int64
 
 // The phased kernel in state-sync form (no init: sync_on chains more than kMaxClients slots into
 // scratch and broadcasts instead).
-template <typename T, int REGS>
+template <typename T, int REGS, int TH>
 hipError_t launch_sync_phased_r(const ClientTable& t, int nc, int64_t head, int64_t nvec, int64_t n, hipStream_t s) {
     PhasedDevice* d = phased_device();
     if (!d) return hipErrorNotSupported;
-    const int64_t per_phase = (int64_t)d->cus * kPhasedThreads * (Phased<T, REGS>::RL + Phased<T, REGS>::RR);
+    const int64_t per_phase = (int64_t)d->cus * TH * (Phased<T, REGS, TH>::RL + Phased<T, REGS, TH>::RR);
     if (nvec < per_phase) return hipErrorNotSupported;
     static int occ = -1;
-    auto kern = fedavg_phased_kernel<T, T, false, REGS, true>;
-    if (occ < 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kPhasedThreads, 0) != hipSuccess) occ = 0;
+    auto kern = fedavg_phased_kernel<T, T, false, REGS, true, TH>;
+    if (occ < 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, TH, 0) != hipSuccess) occ = 0;
     if (occ < 1) return hipErrorNotSupported;
     unsigned* sync = d->sync + 2 * (((uintptr_t)s >> 4) % kSyncSlots);
-    hipLaunchKernelGGL(kern, dim3((unsigned)d->cus), dim3(kPhasedThreads), 0, s, t, nc, (const float*)nullptr,
+    hipLaunchKernelGGL(kern, dim3((unsigned)d->cus), dim3(TH), 0, s, t, nc, (const float*)nullptr,
                        (void*)nullptr, head, nvec, n, sync, d->cus / 32);
     return hipGetLastError();
 }
@@ -768,9 +769,10 @@ hipError_t launch_sync_phased_r(const ClientTable& t, int nc, int64_t head, int6
 template <typename T>
 hipError_t launch_sync_t(const ClientTable& t, int nc, const float* init, int64_t head, int64_t nvec, int64_t n,
                          bool vector_ok, const Tuning& tu, hipStream_t s) {
-    if (vector_ok && !init && (tu.walk == 3 || tu.walk == 4)) {
-        const hipError_t e = tu.walk == 3 ? launch_sync_phased_r<T, 128>(t, nc, head, nvec, n, s)
-                                          : launch_sync_phased_r<T, 192>(t, nc, head, nvec, n, s);
+    if (vector_ok && !init && tu.walk >= 3 && tu.walk <= 5) {
+        const hipError_t e = tu.walk == 3   ? launch_sync_phased_r<T, 128, 256>(t, nc, head, nvec, n, s)
+                             : tu.walk == 4 ? launch_sync_phased_r<T, 192, 256>(t, nc, head, nvec, n, s)
+                                            : launch_sync_phased_r<T, 96, 512>(t, nc, head, nvec, n, s);
         if (e != hipErrorNotSupported) return e;
     }
     if (!vector_ok) {

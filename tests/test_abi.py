@@ -87,7 +87,7 @@ def test_tuning_roundtrip(fa):
     with pytest.raises(fa.FaError):
         fa.set_tuning(slot_skew=100)
     with pytest.raises(fa.FaError):
-        fa.set_tuning(walk=6)
+        fa.set_tuning(walk=7)
     fa.set_tuning(**{k: (v or -1) if k in ("max_blocks", "slot_skew") else v for k, v in before.items()})
     assert fa.get_tuning() == before
 

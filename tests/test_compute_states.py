@@ -179,7 +179,7 @@ def test_sync_phased_same_bits(fa, O, torch_gpu, D, bf16, phases):
     before = fa.get_tuning()
     res = {}
     try:
-        for walk in (2, 5):
+        for walk in (2, 5, 6):
             fa.set_tuning(walk=walk)
             dev = [torch.empty(n, dtype=tdt, device="cuda") for _ in range(D)]
             for k, d in enumerate(dev):
@@ -191,6 +191,7 @@ def test_sync_phased_same_bits(fa, O, torch_gpu, D, bf16, phases):
         fa.set_tuning(walk=before["walk"])
     for k in range(D):
         assert torch.equal(res[2][k], res[5][k]), "slot %d differs" % k
+        assert torch.equal(res[2][k], res[6][k]), "slot %d differs (walk 6)" % k
         if k:
             assert torch.equal(res[5][0], res[5][k])
     idx = np.unique(np.concatenate([[0, 1, n - 2, n - 1], np.random.default_rng(D).integers(0, n, 512)]))

@@ -124,7 +124,7 @@ def test_phased_walk_same_bits(fa, O, torch_gpu, in_bf16, out_bf16, D, phases, o
     before = fa.get_tuning()
     outs = {}
     try:
-        for walk in (2, 4, 5):
+        for walk in (2, 4, 5, 6):
             fa.set_tuning(walk=walk)
             out = dev_buf(torch, n, out_bf16, offset)
             ctx = fa.Aggregator(1) if (out_bf16 and D > 128) else None
@@ -135,7 +135,7 @@ def test_phased_walk_same_bits(fa, O, torch_gpu, in_bf16, out_bf16, D, phases, o
     finally:
         fa.set_tuning(walk=before["walk"])
     dt = torch.int16 if out_bf16 else torch.int32
-    for walk in (4, 5):
+    for walk in (4, 5, 6):
         assert torch.equal(outs[2].view(dt), outs[walk].view(dt)), "phased walk %d differs from walk 2" % walk
     # sampled elements against the oracle (f32 in, no init: the oracle's closed form)
     if not in_bf16 and not use_init:
