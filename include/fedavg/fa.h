@@ -188,10 +188,11 @@ typedef struct {
                          eighth, 3 the same with the odd eighths walked backwards (one-shot grid only),
                          4 phased: a persistent grid (one workgroup per CU) reduces a phase into LDS and
                          registers, then writes it, so the output never streams beside the inputs,
-                         5 (default) phased with a larger register stage (fewer phases).  Buckets
-                         smaller than one phase (walk 4: 18.9 M, walk 5: 23.1 M elements per GPU on
-                         256 CUs, f32 or bf16) take walk 2.  The phased kernels always use nt loads
-                         and sc1 stores */
+                         5 (default) phased with a larger register stage (fewer phases; bf16 inputs
+                         take the form of walk 6), 6 phased with 512-thread workgroups (2 waves per
+                         SIMD).  Buckets smaller than one phase (walk 4: 18.9 M, walks 5 and 6:
+                         23.1 M elements per GPU on 256 CUs, f32 or bf16) take walk 2.  The phased
+                         kernels always use nt loads and sc1 stores */
 } fa_tuning;
 int fa_set_tuning(const fa_tuning* t);
 int fa_get_tuning(fa_tuning* t);

@@ -657,7 +657,8 @@ int64_t phased_min_elems_impl(fa_dtype in, const Tuning& tu) {
     if (tu.walk < 3 || tu.walk > 5) return 0;
     PhasedDevice* d = phased_device();
     if (!d) return 0;
-    const int regs = tu.walk == 4 ? 192 : tu.walk == 5 ? 96 : 128, th = tu.walk == 5 ? 512 : kPhasedThreads;
+    const bool big = tu.walk == 5 || (tu.walk == 4 && in == FA_BF16);  // the 512-thread form
+    const int regs = big ? 96 : tu.walk == 4 ? 192 : 128, th = big ? 512 : kPhasedThreads;
     const int V = in == FA_F32 ? 4 : 8;
     const int rl = 160 * 1024 / (th * V * 4), rr = regs / V;
     return (int64_t)d->cus * th * (rl + rr) * V;
@@ -667,7 +668,14 @@ template <typename IN, typename OUT>
 hipError_t launch_phased(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
                          int64_t n, const Tuning& tu, hipStream_t s) {
     if (tu.walk == 3) return launch_phased_r<IN, OUT, 128, 256>(t, nc, init, out, head, nvec, n, s);
-    if (tu.walk == 4) return launch_phased_r<IN, OUT, 192, 256>(t, nc, init, out, head, nvec, n, s);
+    if (tu.walk == 4) {  // the default: bf16 inputs take the 512-thread form (2 waves per SIMD hide the
+                         // widening VALU work of 8 elements per load: C3 0.430 vs 0.439 ms), f32 the
+                         // 256-thread one (C4 5.43 vs 5.49 ms, C5's share 2.55 vs 2.56), gpurun_out r01s25
+        if constexpr (std::is_same<IN, uint16_t>::value)
+            return launch_phased_r<IN, OUT, 96, 512>(t, nc, init, out, head, nvec, n, s);
+        else
+            return launch_phased_r<IN, OUT, 192, 256>(t, nc, init, out, head, nvec, n, s);
+    }
     if (tu.walk == 5) return launch_phased_r<IN, OUT, 96, 512>(t, nc, init, out, head, nvec, n, s);
     return hipErrorNotSupported;
 }
