@@ -583,3 +583,57 @@ def test_special_values_fedavg_and_literal(fa, O, torch_gpu, D):
     fa.reduce_device(clients, np.zeros(D, np.float32), n, fa.F32, lit, fa.F32, fa.LITERAL)
     torch.cuda.synchronize()
     _assert_bits_nan_aware(lit.cpu().numpy(), O.literal(xs[-1]))
+
+
+# ----------------------------------------------------------------- beyond 2^31 / 2^32 elements
+
+def _big_idx(n, rng):
+    edges = [0, 1, 2, 3, (1 << 31) - 1, 1 << 31, (1 << 31) + 1, (1 << 32) - 1, 1 << 32, (1 << 32) + 1,
+             n - 5, n - 4, n - 3, n - 2, n - 1]
+    return np.unique(np.array([i for i in edges if 0 <= i < n] + list(rng.integers(0, n, 2048)), np.int64))
+
+
+@pytest.mark.parametrize("in_bf16,n,D,walk", [
+    (False, (1 << 31) + 1027, 3, 5),   # 8 GiB per client, 94 phases of the phased kernel
+    (False, (1 << 31) + 1027, 3, 2),   # the one-shot kernel over the same bucket
+    (True, (1 << 32) + 4099, 2, 5),    # bf16: element offsets past 2^32, byte offsets past 2^33
+])
+def test_buckets_past_32bit_indices(fa, O, torch_gpu, in_bf16, n, D, walk):
+    """Maximum-size buckets: element indices past 2^31 / 2^32 reduce like the small ones (sampled vs the
+    oracle), literal mode at the same size, and the in-place state sync."""
+    torch = torch_gpu
+    before = fa.get_tuning()
+    clients = []
+    try:
+        fa.set_tuning(walk=walk)
+        w = O.weights(D)
+        dt = fa.BF16 if in_bf16 else fa.F32
+        clients = [filled(fa, torch, n, in_bf16, 0x5EED, k) for k in range(D)]
+        idx = _big_idx(n, np.random.default_rng(n))
+        tidx = torch.as_tensor(idx, device="cuda")
+        ref = O.fedavg_at(0x5EED, w, idx, bf16=in_bf16)
+        ref = O.f32_to_bf16(ref) if in_bf16 else ref
+        out = torch.empty(n, dtype=torch.int16 if in_bf16 else torch.float32, device="cuda")
+        fa.reduce_device(clients, w, n, dt, out, dt)
+        torch.cuda.synchronize()
+        got = out[tidx].cpu().numpy()
+        assert_bits(got.view(np.uint16) if in_bf16 else got, ref)
+        # literal mode of the last client, into the same output
+        fa.reduce_device(clients, np.zeros(D, np.float32), n, dt, out, dt, fa.LITERAL)
+        torch.cuda.synchronize()
+        last = O.gen_at(0x5EED, D - 1, idx)
+        if in_bf16:
+            assert_bits(out[tidx].cpu().numpy().view(np.uint16), O.literal(O.f32_to_bf16(last), out_dtype="bf16"))
+        else:
+            assert_bits(out[tidx].cpu().numpy(), O.literal(last))
+        del out
+        # compute-node sync in place: every slot becomes the chain, rounded to the slot dtype
+        fa.sync_device(clients, w, n, dt)
+        torch.cuda.synchronize()
+        for k in (0, D - 1):
+            got = clients[k][tidx].cpu().numpy()
+            assert_bits(got.view(np.uint16) if in_bf16 else got, ref)
+    finally:
+        fa.set_tuning(walk=before["walk"])
+        clients = None
+        torch.cuda.empty_cache()
