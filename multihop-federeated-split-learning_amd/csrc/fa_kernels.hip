@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <cstdlib>
 #include <mutex>
 #include <type_traits>
@@ -246,11 +247,17 @@ __global__ __launch_bounds__(256) void fedavg_chain_kernel(const ClientTable t, 
 // walk took 1.42 ms in the same, slow, pools; 1.27-1.30 in fast ones).  Results are bit-identical:
 // the phases only reorder stores in time.
 //
-// The counter pair sync[0] (arrivals) / sync[1] (departures) starts at zero; the last workgroup to
-// leave resets both, so the next launch on the stream finds them zero again.  The wait is bounded
-// (every wave reaches the exit even if the grid were not co-resident: then only speed suffers), and
-// starts the write part once all but `slack` workgroups have arrived.
+// The meeting point is a counter slot picked per stream: a 64-bit ticket word, then a ring of
+// kSyncRing arrival and kSyncRing departure counters.  Every workgroup takes a ticket when it starts;
+// tickets [jG, (j+1)G) form epoch j, which counts on ring entry j % kSyncRing.  Launches on one stream
+// (or replays of a captured graph) are serialized, so each launch is exactly one epoch; the last
+// workgroup of an epoch to leave zeroes its entry.  Launches on two streams that share a slot may
+// mix their workgroups within an epoch, but every epoch still holds G workgroups, so its entry is
+// zeroed all the same: they lose speed (the wait is bounded), never results or the counters.  The
+// bound also lets every wave reach the exit if the grid were not co-resident.  The write part starts
+// once all but `slack` workgroups have arrived.
 constexpr int kPhasedThreads = 256;
+constexpr int kSyncRing = 8;
 
 template <typename IN, int REGS, int TH = kPhasedThreads>
 struct Phased {  // vectors per lane per phase: LDS (160 KiB per workgroup) + registers
@@ -345,6 +352,12 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
     constexpr int V = In<IN>::kVec, T = TH, RL = Phased<IN, REGS, TH>::RL, RR = Phased<IN, REGS, TH>::RR;
     constexpr int U = TH > 256 ? 8 : 16;  // loads in flight per wave (2 waves per SIMD at 512 threads)
     __shared__ float buf[RL * T * V];
+    // thread 0 takes the ticket; its value is first needed at the phase-0 meeting, so the atomic's
+    // latency hides under the phase's loads
+    unsigned long long ticket = 0;
+    if (threadIdx.x == 0)
+        ticket = __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(sync), 1ull, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
     if constexpr (SYNC) sync_scalar_edges<IN, INIT>(t, nc, init, head, head + nvec * V, n);
     else chain_scalar_edges<IN, OUT, INIT>(t, nc, init, out, head, head + nvec * V, n);
     const int64_t G = gridDim.x;
@@ -379,9 +392,10 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
         }
         __syncthreads();
         if (threadIdx.x == 0) {
-            __hip_atomic_fetch_add(&sync[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            unsigned* arrive = sync + 4 + (unsigned)((ticket / (unsigned long long)G) % kSyncRing);
+            __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const unsigned target = (unsigned)(G * (p + 1) - slack);
-            for (int spins = 0; __hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
+            for (int spins = 0; __hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
                                 spins < (1 << 16);
                  ++spins)
                 __builtin_amdgcn_s_sleep(1);
@@ -398,10 +412,13 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
             for (int r = 0; r < RR; ++r) put<OUT, V, SYNC>(t, nc, out, head + (c + r * 64) * V, keep[r]);
         }
     }
-    if (threadIdx.x == 0 &&
-        __hip_atomic_fetch_add(&sync[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)G - 1) {
-        __hip_atomic_store(&sync[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&sync[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) {
+        const unsigned e = (unsigned)((ticket / (unsigned long long)G) % kSyncRing);
+        if (__hip_atomic_fetch_add(sync + 4 + kSyncRing + e, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            (unsigned)G - 1) {
+            __hip_atomic_store(sync + 4 + e, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(sync + 4 + kSyncRing + e, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -593,14 +610,14 @@ hipError_t launch_chain_lnt(const ClientTable& t, int nc, const float* init, voi
     }
 }
 
-// Per-device state of the phased kernel: the CU count (= its grid) and a small table of zeroed
-// arrival/departure counter pairs, one picked per stream (launches on one stream are serialized, so
-// they never share a pair at the same time; two streams that hash to one pair would only lose speed).
-constexpr int kMaxDevices = 64, kSyncSlots = 64;
+// Per-device state of the phased kernel: the CU count (= its grid) and a table of zeroed counter
+// slots (ticket + ring, fedavg_phased_kernel), one picked per stream, 256 B apart.
+constexpr int kMaxDevices = 64, kSyncSlots = 64, kSyncStride = 64;
+static_assert(4 + 2 * kSyncRing <= kSyncStride, "a counter slot holds the ticket and both rings");
 struct PhasedDevice {
     std::once_flag once;
     int cus = 0;
-    unsigned* sync = nullptr;  // kSyncSlots pairs
+    unsigned* sync = nullptr;  // kSyncSlots slots, kSyncStride words apart
 };
 PhasedDevice g_phased[kMaxDevices];
 
@@ -612,8 +629,9 @@ PhasedDevice* phased_device() {
         int cus = 0;
         unsigned* p = nullptr;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return;
-        if (hipMalloc((void**)&p, sizeof(unsigned) * 2 * kSyncSlots) != hipSuccess) return;
-        if (hipMemset(p, 0, sizeof(unsigned) * 2 * kSyncSlots) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        if (hipMalloc((void**)&p, sizeof(unsigned) * kSyncStride * kSyncSlots) != hipSuccess) return;
+        if (hipMemset(p, 0, sizeof(unsigned) * kSyncStride * kSyncSlots) != hipSuccess ||
+            hipDeviceSynchronize() != hipSuccess) {
             (void)hipFree(p);
             return;
         }
@@ -622,6 +640,28 @@ PhasedDevice* phased_device() {
     });
     (void)hipGetLastError();
     return d.sync ? &d : nullptr;
+}
+
+// Enqueue one phased launch on stream s, on the stream's counter slot.
+template <typename Kern>
+hipError_t phased_enqueue(PhasedDevice* d, Kern kern, int th, hipStream_t s, const ClientTable& t, int nc,
+                          const float* init, void* out, int64_t head, int64_t nvec, int64_t n) {
+    const unsigned slot = (unsigned)(((uintptr_t)s >> 4) % kSyncSlots);
+    const int slack = d->cus / 32;  // the write part starts once all but ~3% of the workgroups have arrived
+    hipLaunchKernelGGL(kern, dim3((unsigned)d->cus), dim3(th), 0, s, t, nc, init, out, head, nvec, n,
+                       d->sync + slot * kSyncStride, slack);
+    return hipGetLastError();
+}
+
+// One occupancy query per kernel instantiation (same on every gfx950 device).
+template <typename Kern>
+bool phased_fits(std::atomic<int>& occ, Kern kern, int th) {
+    int o = occ.load(std::memory_order_relaxed);
+    if (o < 0) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kern, th, 0) != hipSuccess) o = 0;
+        occ.store(o, std::memory_order_relaxed);
+    }
+    return o >= 1;
 }
 
 // The phased kernel when it applies (walk 3 = fa_tuning.walk 4, vector path, at least one full phase
@@ -639,16 +679,10 @@ hipError_t launch_phased_r(const ClientTable& t, int nc, const float* init, void
         return e ? (int64_t)std::atoll(e) : (int64_t)-1;
     }();
     if (nvec < (min_env >= 0 ? min_env : per_phase)) return hipErrorNotSupported;
-    static int occ[2] = {-1, -1};  // per INIT variant; same on every gfx950 device
+    static std::atomic<int> occ[2] = {-1, -1};  // per INIT variant
     auto kern = init ? fedavg_phased_kernel<IN, OUT, true, REGS, false, TH> : fedavg_phased_kernel<IN, OUT, false, REGS, false, TH>;
-    int& o = occ[init ? 1 : 0];
-    if (o < 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kern, TH, 0) != hipSuccess) o = 0;
-    if (o < 1) return hipErrorNotSupported;
-    unsigned* sync = d->sync + 2 * (((uintptr_t)s >> 4) % kSyncSlots);
-    const int slack = d->cus / 32;  // the write part starts once all but ~3% of the workgroups have arrived
-    hipLaunchKernelGGL(kern, dim3((unsigned)d->cus), dim3(TH), 0, s, t, nc, init, out, head, nvec, n,
-                       sync, slack);
-    return hipGetLastError();
+    if (!phased_fits(occ[init ? 1 : 0], kern, TH)) return hipErrorNotSupported;
+    return phased_enqueue(d, kern, TH, s, t, nc, init, out, head, nvec, n);
 }
 
 // Smallest bucket (elements of dtype `in` per GPU) that the phased walk of `tu` takes on the current
@@ -764,14 +798,10 @@ hipError_t launch_sync_phased_r(const ClientTable& t, int nc, int64_t head, int6
     if (!d) return hipErrorNotSupported;
     const int64_t per_phase = (int64_t)d->cus * TH * (Phased<T, REGS, TH>::RL + Phased<T, REGS, TH>::RR);
     if (nvec < per_phase) return hipErrorNotSupported;
-    static int occ = -1;
+    static std::atomic<int> occ{-1};
     auto kern = fedavg_phased_kernel<T, T, false, REGS, true, TH>;
-    if (occ < 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, TH, 0) != hipSuccess) occ = 0;
-    if (occ < 1) return hipErrorNotSupported;
-    unsigned* sync = d->sync + 2 * (((uintptr_t)s >> 4) % kSyncSlots);
-    hipLaunchKernelGGL(kern, dim3((unsigned)d->cus), dim3(TH), 0, s, t, nc, (const float*)nullptr,
-                       (void*)nullptr, head, nvec, n, sync, d->cus / 32);
-    return hipGetLastError();
+    if (!phased_fits(occ, kern, TH)) return hipErrorNotSupported;
+    return phased_enqueue(d, kern, TH, s, t, nc, (const float*)nullptr, (void*)nullptr, head, nvec, n);
 }
 
 template <typename T>

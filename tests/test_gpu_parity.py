@@ -637,3 +637,99 @@ def test_buckets_past_32bit_indices(fa, O, torch_gpu, in_bf16, n, D, walk):
         fa.set_tuning(walk=before["walk"])
         clients = None
         torch.cuda.empty_cache()
+
+
+def test_phased_streams_sharing_a_counter(fa, O, torch_gpu):
+    """Two streams whose phased launches count on the same counter slot (stream handles are hashed onto
+    64 slots), launched so they overlap: every result stays bit-exact, and a later launch on either
+    stream runs as fast as before (no counter is left skewed)."""
+    torch = torch_gpu
+    before = fa.get_tuning()
+    try:
+        fa.set_tuning(walk=5)
+        n, D = 30_000_005, 4  # 1.3 phases of the default f32 form
+        w = O.weights(D)
+        sets = []
+        for s in range(2):
+            clients = [filled(fa, torch, n, False, 0x5EED + s, k) for k in range(D)]
+            sets.append((clients, torch.empty(n, dtype=torch.float32, device="cuda")))
+        ref = []
+        for clients, out in sets:
+            fa.reduce_device(clients, w, n, fa.F32, out, fa.F32)
+            torch.cuda.synchronize()
+            ref.append(out.clone())
+        by_slot = {}
+        streams = []
+        pair = None
+        for _ in range(65):  # pigeonhole: two of 65 streams share one of the 64 slots
+            st = torch.cuda.Stream()
+            streams.append(st)
+            slot = (st.cuda_stream >> 4) % 64
+            if slot in by_slot:
+                pair = (by_slot[slot], st)
+                break
+            by_slot[slot] = st
+        assert pair is not None
+
+        def median_ms(st):
+            evs = []
+            clients, out = sets[0]
+            for _ in range(7):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(st)
+                fa.reduce_device(clients, w, n, fa.F32, out, fa.F32, stream=st)
+                b.record(st)
+                evs.append((a, b))
+            torch.cuda.synchronize()
+            return float(np.median([a.elapsed_time(b) for a, b in evs[2:]]))
+
+        t0 = median_ms(pair[0])
+        for _ in range(6):  # overlapping launches on the two streams
+            for k in range(2):
+                clients, out = sets[k]
+                with torch.cuda.stream(pair[k]):
+                    out.zero_()
+                fa.reduce_device(clients, w, n, fa.F32, out, fa.F32, stream=pair[k])
+        torch.cuda.synchronize()
+        for k in range(2):
+            assert torch.equal(sets[k][1].view(torch.int32), ref[k].view(torch.int32))
+        t1, t2 = median_ms(pair[0]), median_ms(pair[1])
+        assert max(t1, t2) < 1.5 * t0 + 0.05, (t0, t1, t2)
+    finally:
+        fa.set_tuning(walk=before["walk"])
+
+
+def test_phased_graph_replays(fa, O, torch_gpu):
+    """A phased launch captured in a graph and replayed: each replay is one epoch of the counter ring,
+    results stay bit-exact, and an eager launch afterwards runs at its usual speed."""
+    torch = torch_gpu
+    n, D = 30_000_005, 3
+    w = O.weights(D)
+    clients = [filled(fa, torch, n, False, 0x5EED, k) for k in range(D)]
+    out = torch.empty(n, dtype=torch.float32, device="cuda")
+    st = torch.cuda.Stream()
+
+    def eager_ms():
+        evs = []
+        for _ in range(6):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(st)
+            fa.reduce_device(clients, w, n, fa.F32, out, fa.F32, stream=st)
+            b.record(st)
+            evs.append((a, b))
+        torch.cuda.synchronize()
+        return float(np.median([a.elapsed_time(b) for a, b in evs[1:]]))
+
+    t0 = eager_ms()
+    ref = out.clone()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=st):
+        fa.reduce_device(clients, w, n, fa.F32, out, fa.F32, stream=torch.cuda.current_stream())
+    for _ in range(11):  # more replays than ring entries
+        out.zero_()
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out.view(torch.int32), ref.view(torch.int32))
+    t1 = eager_ms()
+    assert t1 < 1.5 * t0 + 0.05, (t0, t1)
