@@ -336,22 +336,23 @@ int probe_pool(fa_ctx* ctx, int g, const Part& p, size_t stride, char* pool, flo
     for (int k = 0; k < p.D; ++k) cl[(size_t)k] = pool + (size_t)k * stride;
     std::vector<float> w((size_t)p.D, 1.0f / (float)p.D);
     void* out = pool + (size_t)p.D * stride;
-    hipEvent_t a, b;
-    FA_HIP(hipEventCreate(&a));
-    FA_HIP(hipEventCreate(&b));
+    struct Ev {  // destroyed on every return path
+        hipEvent_t e = nullptr;
+        ~Ev() { if (e) (void)hipEventDestroy(e); }
+    } a, b;
+    FA_HIP(hipEventCreate(&a.e));
+    FA_HIP(hipEventCreate(&b.e));
     float best = 1e30f;
     int rc = FA_OK;
     for (int it = 0; it < 4 && rc == FA_OK; ++it) {
-        FA_HIP(hipEventRecord(a, r.compute));
+        FA_HIP(hipEventRecord(a.e, r.compute));
         rc = reduce_on(ctx, g, cl.data(), w.data(), p.D, n, p.in, out, p.out, FA_FEDAVG, 1.0f, nullptr, r.compute);
-        FA_HIP(hipEventRecord(b, r.compute));
-        FA_HIP(hipEventSynchronize(b));
+        FA_HIP(hipEventRecord(b.e, r.compute));
+        FA_HIP(hipEventSynchronize(b.e));
         float t = 0;
-        FA_HIP(hipEventElapsedTime(&t, a, b));
+        FA_HIP(hipEventElapsedTime(&t, a.e, b.e));
         if (it > 0) best = std::min(best, t);  // first launch warms up
     }
-    (void)hipEventDestroy(a);
-    (void)hipEventDestroy(b);
     *ms_out = best;
     return rc;
 }
