@@ -22,13 +22,16 @@ bytes per launch ((D+1) * N * sizeof for f32->f32) / average launch duration
 from HIP events on the launch stream.
 """
 import argparse
+import faulthandler
 import importlib.util
 import json
 import os
 import statistics
 import subprocess
 import sys
+import threading
 import time
+import traceback
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG_DIR = os.path.join(ROOT, "multihop-federeated-split-learning_amd")
@@ -219,6 +222,59 @@ def timed_loop(torch, setup, steps, warmup, stream, dist, barrier):
     return wall, kern_ms
 
 
+def time_client_sharded(torch, dist, shard, setup, layout, n, world, device, stream, steps, warmup, chunks, barrier):
+    """Wall time of `steps` rounds of a client-sharded layout: every rank reduces its whole clients (the
+    setup's slots) and the ranks combine them -- "rs": fp32 partials + RCCL reduce-scatter, "chain": the
+    ordered chain handed rank to rank over RCCL p2p (shard.py)."""
+    reducer = shard.fa_reducer(setup.fa, setup.in_dt, stream)
+    cl = setup.clients()
+    dev = torch.device("cuda", device)
+    npad = -(-n // (world * shard.UNIT)) * world * shard.UNIT
+    assert npad == n, "workload size must be a multiple of world * 64"
+
+    def step():
+        with torch.cuda.stream(stream):
+            if world == 1:
+                return reducer(cl, setup.w, n)
+            fn = shard.reduce_rs if layout == "rs" else shard.reduce_chain
+            return fn(reducer, dist, cl, setup.w, n, dev, chunks=chunks, itemsize=setup.s_in)
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0
+
+
+def layout_desc_of(layout, D, chunks):
+    if layout == "rs":
+        return ("client-sharded: each rank reduces its %d whole clients into fp32 partials, RCCL "
+                "reduce-scatter over xGMI in %d chunks overlapped with the reduction" % (D, chunks))
+    return ("client-sharded, bit-exact: the fp32 chain is handed rank to rank over RCCL p2p in %d "
+            "chunks, last rank scatters the ranges" % chunks)
+
+
+class LinePrinter:
+    """Rank 0 prints the one JSON line exactly once (from the main thread or the watchdog)."""
+
+    def __init__(self, rank):
+        self.rank = rank
+        self.lock = threading.Lock()
+        self.done = False
+
+    def emit(self, line):
+        with self.lock:
+            if self.rank == 0 and not self.done:
+                print(json.dumps(line), flush=True)
+            self.done = True
+
+
 def load_shard():
     load_pkg()
     import importlib
@@ -290,36 +346,9 @@ def main():
         layout_desc = "range-sharded: each rank owns %d of %d elements of every bucket, no collective" % (
             n, n * world)
     else:
-        reducer = shard.fa_reducer(fa, setup.in_dt, stream)
-        cl = setup.clients()
-        dev = torch.device("cuda", device)
-        npad = -(-n // (world * shard.UNIT)) * world * shard.UNIT
-        assert npad == n, "workload size must be a multiple of world * 64"
-
-        def step():
-            with torch.cuda.stream(stream):
-                if args.layout == "rs":
-                    return shard.reduce_rs(reducer, dist, cl, setup.w, n, dev, chunks=args.chunks,
-                                           itemsize=setup.s_in) if world > 1 else reducer(cl, setup.w, n)
-                return shard.reduce_chain(reducer, dist, cl, setup.w, n, dev, chunks=args.chunks,
-                                          itemsize=setup.s_in) if world > 1 else reducer(cl, setup.w, n)
-        for _ in range(args.warmup):
-            step()
-        torch.cuda.synchronize()
-        barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        torch.cuda.synchronize()
-        barrier()
-        torch.cuda.synchronize()
-        wall = time.perf_counter() - t0
-        layout_desc = ("client-sharded: each rank reduces its %d whole clients into fp32 partials, RCCL "
-                       "reduce-scatter over xGMI in %d chunks overlapped with the reduction" % (D, args.chunks)
-                       if args.layout == "rs" else
-                       "client-sharded, bit-exact: the fp32 chain is handed rank to rank over RCCL p2p in %d "
-                       "chunks, last rank scatters the ranges" % args.chunks)
+        wall = time_client_sharded(torch, dist, shard, setup, args.layout, n, world, device, stream, args.steps,
+                                   args.warmup, args.chunks, barrier)
+        layout_desc = layout_desc_of(args.layout, D, args.chunks)
     units_bytes = setup.input_bytes() * world
 
     if world > 1:
@@ -402,8 +431,50 @@ def main():
         s.close()
         line["secondary"] = sec
 
-    if rank == 0:
-        print(json.dumps(line), flush=True)
+    printer = LinePrinter(rank)
+    if world > 1 and not args.no_secondary and args.layout == "range":
+        # the client-sharded layouts on the same ranks, as secondaries (the RCCL legs: reduce-scatter and
+        # the p2p chain).  A watchdog bounds them: should a collective stall, rank 0 still prints the
+        # main line (marked) and every rank exits.
+        limit = float(os.environ.get("FA_BENCH_SECONDARY_TIMEOUT", "90"))
+
+        done = threading.Event()
+
+        def watchdog():
+            if not done.wait(limit):
+                print("rank %d: client-sharded layouts still running after %.0f s; stacks:" % (rank, limit),
+                      file=sys.stderr, flush=True)
+                faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+                line["secondary_error"] = "client-sharded layouts did not finish within %.0f s" % limit
+                printer.emit(line)
+                os._exit(0)
+        threading.Thread(target=watchdog, daemon=True).start()
+        setup.close()
+        sec = line["secondary"] = {}  # filled layout by layout, so a watchdog exit keeps what finished
+        steps2 = max(10, args.steps)
+        for L in ("rs", "chain"):
+            try:
+                s2 = Setup(fa, torch, D, n, in_dt, out_dt, 0, device, client0=rank * D)
+                s2.w = Setup._weights(D * world)[rank * D:(rank + 1) * D]
+                torch.cuda.synchronize()
+                w2 = time_client_sharded(torch, dist, shard, s2, L, n, world, device, stream, steps2, 3,
+                                         args.chunks, barrier)
+                t = torch.tensor([w2], dtype=torch.float64, device="cuda")
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                w2 = float(t.item())
+                sec[L] = {"description": layout_desc_of(L, D, args.chunks), "clients": D * world,
+                          "elems_per_client": n, "steps": steps2, "ms_per_step": round(w2 / steps2 * 1e3, 4),
+                          "gib_s": round(s2.input_bytes() * world * steps2 / w2 / 2**30, 1)}
+                s2.close()
+            except Exception as e:  # noqa: BLE001 -- the ranks may now disagree: report and leave
+                traceback.print_exc()
+                print("rank %d: %s layout failed" % (rank, L), file=sys.stderr, flush=True)
+                sec[L] = {"error": repr(e)[:300]}
+                printer.emit(line)
+                os._exit(0)
+        done.set()
+
+    printer.emit(line)
     if world > 1:
         dist.destroy_process_group()
 
