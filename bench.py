@@ -224,7 +224,8 @@ def timed_loop(torch, setup, steps, warmup, stream, dist, barrier):
 
 def time_client_sharded(torch, dist, shard, setup, layout, n, world, device, stream, steps, warmup, chunks, barrier):
     """Wall time of `steps` rounds of a client-sharded layout: every rank reduces its whole clients (the
-    setup's slots) and the ranks combine them -- "rs": fp32 partials + RCCL reduce-scatter, "chain": the
+    setup's slots) and the ranks combine them -- "rs": fp32 partials + RCCL reduce-scatter (block-cyclic
+    ownership, one launch per chunk: shard.reduce_rs_cyclic), "chain": the
     ordered chain handed rank to rank over RCCL p2p (shard.py)."""
     reducer = shard.fa_reducer(setup.fa, setup.in_dt, stream)
     cl = setup.clients()
@@ -236,7 +237,7 @@ def time_client_sharded(torch, dist, shard, setup, layout, n, world, device, str
         with torch.cuda.stream(stream):
             if world == 1:
                 return reducer(cl, setup.w, n)
-            fn = shard.reduce_rs if layout == "rs" else shard.reduce_chain
+            fn = shard.reduce_rs_cyclic if layout == "rs" else shard.reduce_chain
             return fn(reducer, dist, cl, setup.w, n, dev, chunks=chunks, itemsize=setup.s_in)
     for _ in range(warmup):
         step()
@@ -255,7 +256,8 @@ def time_client_sharded(torch, dist, shard, setup, layout, n, world, device, str
 def layout_desc_of(layout, D, chunks):
     if layout == "rs":
         return ("client-sharded: each rank reduces its %d whole clients into fp32 partials, RCCL "
-                "reduce-scatter over xGMI in %d chunks overlapped with the reduction" % (D, chunks))
+                "reduce-scatter over xGMI in %d chunks overlapped with the reduction (block-cyclic "
+                "ownership, one launch per chunk)" % (D, chunks))
     return ("client-sharded, bit-exact: the fp32 chain is handed rank to rank over RCCL p2p in %d "
             "chunks, last rank scatters the ranges" % chunks)
 

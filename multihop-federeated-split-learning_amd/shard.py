@@ -11,7 +11,8 @@ are partitioned instead:
   (``torch.distributed.reduce_scatter_tensor``, backend "nccl" = RCCL over
   xGMI) sums the partials so rank r ends with elements [lo_r, hi_r).  The
   summation order changes: parity is by tolerance (1e-6 relative to
-  sum_k |w_k x_k|).
+  sum_k |w_k x_k|).  ``reduce_rs_cyclic`` is the same exchange with
+  block-cyclic ownership, so every chunk is one launch (what bench.py times).
 * ``chain``  -- client-sharded like ``rs`` but bit-exact: the ordered FMA chain
   is passed rank to rank (rank r continues from rank r-1's fp32 accumulator via
   fa_reduce_device's d_init), pipelined over element chunks with point-to-point
@@ -93,6 +94,63 @@ def reduce_rs(reduce, dist, clients, weights, n, device, chunks=1, itemsize=4):
             else:  # a rank without clients contributes zeros
                 out.zero_()
         pending[i] = dist.reduce_scatter_tensor(shard[a:b], buf, op=dist.ReduceOp.SUM, async_op=True)
+    for p in pending:
+        if p is not None:
+            p.wait()
+    return shard
+
+
+def cyclic_pieces(n, world, chunks):
+    """[A, B) bucket pieces of the block-cyclic rs layout: `chunks` contiguous pieces, each a multiple of
+    world * UNIT elements (n must be a multiple of world * UNIT), so each splits into `world` equal blocks."""
+    g = world * UNIT
+    assert n % g == 0, "pad the bucket to a multiple of world * %d" % UNIT
+    m = n // g
+    edges = sorted({m * c // max(1, chunks) * g for c in range(max(1, chunks))} | {n})
+    return list(zip(edges, edges[1:]))
+
+
+def cyclic_bounds(n, world, rank, chunks):
+    """The [lo, hi) segments rank `rank` owns under reduce_rs_cyclic, in the order of its shard."""
+    out = []
+    for a, b in cyclic_pieces(n, world, chunks):
+        q = (b - a) // world
+        out.append((a + rank * q, a + (rank + 1) * q))
+    return out
+
+
+def reduce_rs_cyclic(reduce, dist, clients, weights, n, device, chunks=16, itemsize=4):
+    """Client-sharded partial + reduce-scatter with block-cyclic ownership: ONE launch per chunk.
+
+    reduce_rs with chunks > 1 reduces every rank's range separately (chunks * world launches per round:
+    128 small ones at 8 ranks x 16 chunks, each a ctypes call).  Here chunk c is one contiguous piece of
+    the bucket (cyclic_pieces), reduced by a single launch into a buffer whose reduce-scatter hands rank
+    r the r-th block of the piece.  The reduce-scatter of piece c overlaps the reduction of piece c+1.
+    Rank r ends with the segments cyclic_bounds(n, world, r, chunks), concatenated.  Same summation as
+    reduce_rs: parity by tolerance (1e-6 relative to sum_k |w_k x_k|).
+    """
+    import torch
+    world = dist.get_world_size()
+    pieces = cyclic_pieces(n, world, chunks)
+    shard = torch.empty(n // world, dtype=torch.float32, device=device)
+    if not pieces:
+        return shard
+    q_max = max(b - a for a, b in pieces)
+    bufs = [torch.empty(q_max, dtype=torch.float32, device=device) for _ in range(min(2, len(pieces)))]
+    pending = [None] * len(bufs)
+    off = 0
+    for c, (a, b) in enumerate(pieces):
+        i = c % len(bufs)
+        if pending[i] is not None:  # the buffer's previous reduce-scatter must be done before it is refilled
+            pending[i].wait()
+        buf = bufs[i][:b - a]
+        if clients:
+            reduce([_piece(x, a, b, itemsize) for x in clients], weights, b - a, out=buf)
+        else:  # a rank without clients contributes zeros
+            buf.zero_()
+        q = (b - a) // world
+        pending[i] = dist.reduce_scatter_tensor(shard[off:off + q], buf, op=dist.ReduceOp.SUM, async_op=True)
+        off += q
     for p in pending:
         if p is not None:
             p.wait()

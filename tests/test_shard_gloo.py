@@ -58,6 +58,9 @@ def worker(rank, world, port, n, D, seed, q):
         mine_p = [torch.nn.functional.pad(x, (0, npad - n)) for x in mine]
         res["rs"] = shard.reduce_rs(reducer, dist, mine_p, w[c0:c1], npad, dev).numpy()
         res["rs_chunked"] = shard.reduce_rs(reducer, dist, mine_p, w[c0:c1], npad, dev, chunks=3).numpy()
+        for ch in (1, 4):
+            res["rs_cyclic%d" % ch] = shard.reduce_rs_cyclic(reducer, dist, mine_p, w[c0:c1], npad, dev,
+                                                              chunks=ch).numpy()
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -99,6 +102,22 @@ def test_layouts_match_single_gpu_chain(O, world, n, D):
         got = np.concatenate([out[r][layout] for r in range(world)])[:n]
         ok, worst = shard.tolerance_ok(got, ref, absw)
         assert ok, (layout, worst)
+    # block-cyclic rs: each rank's shard is its cyclic_bounds segments, concatenated
+    npad = -(-n // (world * shard.UNIT)) * world * shard.UNIT
+    for ch in (1, 4):
+        got = np.full(npad, np.nan, np.float32)
+        for r in range(world):
+            segs = shard.cyclic_bounds(npad, world, r, ch)
+            mine = out[r]["rs_cyclic%d" % ch]
+            assert mine.size == sum(b - a for a, b in segs) == npad // world
+            off = 0
+            for a, b in segs:
+                got[a:b] = mine[off:off + b - a]
+                off += b - a
+        assert not np.isnan(got).any()  # the segments of all ranks cover the bucket
+        ok, worst = shard.tolerance_ok(got[:n], ref, absw)
+        assert ok, ("rs_cyclic", ch, worst)
+        assert np.all(got[n:] == 0)  # padding stays zero
 
 
 def test_bounds_cover_and_align():

@@ -105,6 +105,11 @@ for s in $STEPS; do
             -Wl,-rpath,$PWD/multihop-federeated-split-learning_amd/lib -o "$OUT/exp_phase3" > "$OUT/phase3_build.log" 2>&1 &&
         timeout -k 10 300 "$OUT/exp_phase3" ${PHASE_ARGS:-26 4 3} > "$OUT/exp_phase3.jsonl" 2> "$OUT/exp_phase3.err"
         rc=$?; cat "$OUT/exp_phase3.jsonl"; tail -3 "$OUT/exp_phase3.err"; ok_or_fail $rc phase3 ;;
+    rslaunch)  # local launch pattern of the rs / chain layouts at 4 and 8 ranks (tools/rs_launch.py)
+        for W in 8 4; do
+            timeout -k 10 300 python tools/rs_launch.py $W 16 10 >> "$OUT/rs_launch.jsonl" 2>> "$OUT/rs_launch.err"
+            rc=$?; tail -1 "$OUT/rs_launch.jsonl"; ok_or_fail $rc rslaunch_$W
+        done ;;
     e2e)
         timeout -k 10 900 python tools/e2e_bench.py 4 3 > "$OUT/e2e_bench.json" 2> "$OUT/e2e_bench.err"
         rc=$?; cat "$OUT/e2e_bench.json"; tail -3 "$OUT/e2e_bench.err"; ok_or_fail $rc e2e ;;
