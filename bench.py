@@ -139,7 +139,7 @@ class Setup:
     """
 
     def __init__(self, fa, torch, D, n, in_dt, out_dt, elem0, device, client0=0, seed=0x5EED,
-                 min_rotate_bytes=ROTATE_MIN_BYTES):
+                 min_rotate_bytes=ROTATE_MIN_BYTES, mode=None):
         self.fa, self.torch = fa, torch
         self.D, self.n = D, n
         self.in_dt = fa.F32 if in_dt == "f32" else fa.BF16
@@ -150,7 +150,7 @@ class Setup:
         self.nsets = max(1, -(-min_rotate_bytes // set_bytes))
         self.agg = fa.Aggregator(devices=[device])
         for s in range(self.nsets):
-            self.agg.define(s, n, self.in_dt, self.out_dt, D, fa.FEDAVG)
+            self.agg.define(s, n, self.in_dt, self.out_dt, D, fa.FEDAVG if mode is None else mode)
             for k in range(D):
                 ptr, cnt, _ = self.agg.slot(s, 0, k)
                 # global client id and element offset: ranks hold disjoint clients or slices of one bucket
@@ -430,6 +430,19 @@ def main():
                               "achieved_GBs": round(s.algo_bytes() / (ka * 1e-3) / 1e9, 1),
                               "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                               "input_sets_rotated": s.nsets}
+        s.close()
+        # the reference's own semantics (aggregator.cpp:72-88, literal mode): fl(fl(x+x)/1000) of the last
+        # receipt, on its largest bucket (VGG-19's FC part); per element one read + one write
+        s = Setup(fa, torch, 1, 119_586_826, "f32", "f32", 0, device, mode=fa.LITERAL)
+        torch.cuda.synchronize()
+        w2, km = timed_loop(torch, s, max(10, args.steps), 3, stream, dist, barrier)
+        ka = statistics.mean(km)
+        sec["literal_vgg_fc"] = {"description": "reference-literal mode fl(fl(x+x)/1000) of the last receipt, "
+                                                "VGG-19's FC part (119.6 M fp32 parameters)",
+                                 "kernel_ms_avg": round(ka, 4),
+                                 "achieved_GBs": round(s.algo_bytes() / (ka * 1e-3) / 1e9, 1),
+                                 "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                 "input_sets_rotated": s.nsets}
         s.close()
         line["secondary"] = sec
 
