@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Tuning sweep of the FedAvg kernel on a bench workload (GPU box tool).
 
-  python tools/sweep.py [workload]   SWEEP_BLOCKS / SWEEP_UNROLLS / SWEEP_STORES / SWEEP_WALKS / SWEEP_POOLS:
+  python tools/sweep.py [workload]   SWEEP_BLOCKS / SWEEP_MAXBLOCKS / SWEEP_UNROLLS / SWEEP_STORES / SWEEP_WALKS / SWEEP_POOLS:
                                      comma lists
 
 Interleaves every configuration in rounds inside one process (rule: A/B deltas
@@ -31,7 +31,7 @@ def main():
     def env_list(name, default):
         v = os.environ.get(name)
         return [int(x) for x in v.split(",")] if v else default
-    grid = list(itertools.product(env_list("SWEEP_BLOCKS", [128, 256]), [0], env_list("SWEEP_UNROLLS", [8, 16]), [2],
+    grid = list(itertools.product(env_list("SWEEP_BLOCKS", [128, 256]), env_list("SWEEP_MAXBLOCKS", [0]), env_list("SWEEP_UNROLLS", [8, 16]), [2],
                                   env_list("SWEEP_STORES", [1, 2, 3, 4]), env_list("SWEEP_WALKS", [1])))
     times = {(g, p): [] for g in grid for p in range(pools)}
     for rnd in range(3):
