@@ -178,8 +178,8 @@ def reduce_chain(reduce, dist, clients, weights, n, device, chunks=8, itemsize=4
         if rank > 0:
             dist.recv(acc[a:b], src=rank - 1)
             init = acc[a:b]
-        if clients:
-            acc[a:b] = reduce([_piece(x, a, b, itemsize) for x in clients], weights, b - a, init=init)
+        if clients:  # in place: each lane reads its init elements before it writes them
+            reduce([_piece(x, a, b, itemsize) for x in clients], weights, b - a, init=init, out=acc[a:b])
         elif rank == 0:
             acc[a:b].zero_()  # the chain starts at +0
         if rank < world - 1:

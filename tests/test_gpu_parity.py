@@ -181,6 +181,26 @@ def test_fedavg_init_continues_the_chain(fa, O, torch_gpu):
     assert_bits(out, O.fedavg(xs, w))
 
 
+@pytest.mark.parametrize("n", [300_001, int(PHASE_ELEMS * 1.3) + 7])  # one-shot and phased kernels
+def test_fedavg_init_in_place(fa, O, torch_gpu, n):
+    """d_init and the output may be the same buffer (shard.reduce_chain continues a rank's chain in
+    place): every lane reads its init elements before it writes them.  Same bits as a separate output,
+    and as the oracle on sampled elements."""
+    torch = torch_gpu
+    D = 10
+    w = O.weights(D)
+    clients = [filled(fa, torch, n, False, 6, k) for k in range(D)]
+    acc = dev_buf(torch, n, False)
+    fa.reduce_device(clients[:4], w[:4], n, fa.F32, acc, fa.F32)
+    sep = dev_buf(torch, n, False)
+    fa.reduce_device(clients[4:], w[4:], n, fa.F32, sep, fa.F32, fa.FEDAVG, init=acc)
+    fa.reduce_device(clients[4:], w[4:], n, fa.F32, acc, fa.F32, fa.FEDAVG, init=acc)
+    torch.cuda.synchronize()
+    assert torch.equal(acc.view(torch.int32), sep.view(torch.int32))
+    idx = np.unique(np.concatenate([[0, 1, n - 2, n - 1], np.random.default_rng(n).integers(0, n, 1024)]))
+    assert_bits(acc[torch.as_tensor(idx, device="cuda")].cpu().numpy(), O.fedavg_at(6, w, idx))
+
+
 @pytest.mark.parametrize("out_bf16", [False, True])
 @pytest.mark.parametrize("D", [1, 7, 32, 70, 130])
 def test_fedavg_bf16_inputs(fa, O, torch_gpu, D, out_bf16):
