@@ -162,6 +162,30 @@ def _piece(x, a, b, itemsize):
     return x + a * itemsize if isinstance(x, int) else x[a:b]
 
 
+def _staged(dist, t):
+    """gloo's send/recv take host tensors only (a device tensor's pointer would be read as host memory):
+    device tensors go through a host copy there.  RCCL moves device buffers directly."""
+    return t.is_cuda and dist.get_backend() == "gloo"
+
+
+def _send(dist, t, dst):
+    """Send `t` to `dst`; returns a handle to wait() on (the send is blocking when staged through host)."""
+    if _staged(dist, t):
+        dist.send(t.cpu(), dst=dst)
+        return None
+    return dist.isend(t, dst=dst)
+
+
+def _recv(dist, t, src):
+    if _staged(dist, t):
+        import torch
+        h = torch.empty(t.shape, dtype=t.dtype)
+        dist.recv(h, src=src)
+        t.copy_(h)
+    else:
+        dist.recv(t, src=src)
+
+
 def reduce_chain(reduce, dist, clients, weights, n, device, chunks=8, itemsize=4):
     """Bit-exact client-sharded reduction: the fp32 chain is handed rank r -> r+1 chunk by chunk.
 
@@ -176,16 +200,17 @@ def reduce_chain(reduce, dist, clients, weights, n, device, chunks=8, itemsize=4
     for a, b in zip(edges, edges[1:]):
         init = None
         if rank > 0:
-            dist.recv(acc[a:b], src=rank - 1)
+            _recv(dist, acc[a:b], rank - 1)
             init = acc[a:b]
         if clients:  # in place: each lane reads its init elements before it writes them
             reduce([_piece(x, a, b, itemsize) for x in clients], weights, b - a, init=init, out=acc[a:b])
         elif rank == 0:
             acc[a:b].zero_()  # the chain starts at +0
         if rank < world - 1:
-            sends.append(dist.isend(acc[a:b], dst=rank + 1))
+            sends.append(_send(dist, acc[a:b], rank + 1))
     for r in sends:
-        r.wait()
+        if r is not None:
+            r.wait()
     # the last rank holds the full chain: it sends every rank its range
     lo, hi = range_bounds(n, world, rank)
     mine = torch.empty(hi - lo, dtype=torch.float32, device=device)
@@ -195,12 +220,13 @@ def reduce_chain(reduce, dist, clients, weights, n, device, chunks=8, itemsize=4
         for r in range(world - 1):
             rlo, rhi = range_bounds(n, world, r)
             if rhi > rlo:
-                outs.append(dist.isend(acc[rlo:rhi].contiguous(), dst=r))
+                outs.append(_send(dist, acc[rlo:rhi].contiguous(), r))
         mine.copy_(acc[lo:hi])
         for o in outs:
-            o.wait()
+            if o is not None:
+                o.wait()
     elif hi > lo:
-        dist.recv(mine, src=last)
+        _recv(dist, mine, last)
     return mine
 
 
