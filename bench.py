@@ -403,6 +403,8 @@ def main():
             sec[name] = {"description": sdesc, "gib_s": round(s.input_bytes() * max(10, args.steps) / w2 / 2**30, 1),
                          "kernel_ms_avg": round(ka, 4),
                          "achieved_GBs": round(s.algo_bytes() / (ka * 1e-3) / 1e9, 1),
+                         "algorithmic_bytes_per_launch": s.algo_bytes(),
+                         "traffic": traffic_from_profile(name, 1)[0],
                          "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          "input_sets_rotated": s.nsets, "placement": s.placement}
             s.close()
