@@ -4,22 +4,26 @@
 One step = one pass of the hot path over one round's synthetic client buckets
 already resident in HBM: the ordered weighted-sum reduction of D client buckets
 (pipeline_simulation/aggregator.cpp:59-93 / :112-150, FedAvg semantics) through
-libfa.so's C ABI (fa_reduce_device).
+libfa.so's C ABI (fa_reduce_part on the context's own slots).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload northstar|c2|c3]
-                  [--layout range|rs|chain] [--no-cpu-baseline] [--no-secondary]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload northstar|c2|c3|c4|c5|c5r]
+                  [--scaling strong|weak] [--layout range|rs|chain] [--no-cpu-baseline] [--no-secondary]
 
-N > 1 runs one process per GPU (torch.distributed.run sets RANK/LOCAL_RANK/
-WORLD_SIZE).  Layout "range" (default) shards every bucket by element range:
-each rank reduces its own 256 MiB slice of all D clients, no collective
-(weak scaling).  Layouts "rs" and "chain" give each rank 32 whole clients:
-"rs" combines the fp32 partials with an RCCL reduce-scatter over xGMI, "chain"
-hands the ordered fp32 chain rank to rank (bit-exact) over RCCL p2p.
+One process per GPU.  `--gpus N` with N > 1 starts its own N rank processes
+(RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in their env) unless a launcher such as
+torch.distributed.run already set WORLD_SIZE.  Scaling "strong" (default): the
+north star's 32 x 256 MiB problem is fixed and split over the ranks; layout
+"range" gives rank r the elements [r n/N, (r+1) n/N) of every client bucket
+(no collective, bit-exact).  "rs" / "chain" deal the 32 clients to the ranks
+instead: "rs" combines fp32 partials with an RCCL reduce-scatter over xGMI,
+"chain" hands the ordered fp32 chain rank to rank over RCCL p2p (bit-exact).
+At N > 1 the weak-scaled range layout and the rs / chain layouts are reported
+under "secondary".
 
-value = bytes of client input reduced by all ranks / max-over-ranks wall time,
-in GiB/s (D * N * sizeof(in) / t / 2^30).  roofline.achieved = algorithmic HBM
-bytes per launch ((D+1) * N * sizeof for f32->f32) / average launch duration
-from HIP events on the launch stream.
+value = bytes of client input of the whole problem / max-over-ranks wall time,
+in GiB/s (D * n * sizeof(in) / t / 2^30).  roofline.achieved = algorithmic HBM
+bytes of this rank's launch ((D+1) * n_rank * sizeof for f32->f32) / its
+average duration from HIP events on the launch stream.
 """
 import argparse
 import faulthandler
@@ -45,6 +49,10 @@ WORKLOADS = {
     "c4": (64, 139_611_210, "f32", "f32", "VGG-19 full model buckets (reference build), 64 owners, fp32, on one GPU"),
     "c5": (128, 1 << 28, "f32", "f32", "synthetic 1 GiB fp32 bucket x 128 clients, all on one GPU (129 GiB resident)"),
     "c5r": (128, 1 << 25, "f32", "f32", "C5 one rank's share on 8 GPUs (range layout): 128 clients x 128 MiB slice"),
+    # one rank's share of the strong-scaled north star (bench.py --gpus W): 32 clients x 256/W MiB
+    "ns_w2": (32, 32 << 20, "f32", "f32", "north star, one rank's share at 2 GPUs (strong scaling): 32 x 128 MiB"),
+    "ns_w4": (32, 16 << 20, "f32", "f32", "north star, one rank's share at 4 GPUs (strong scaling): 32 x 64 MiB"),
+    "ns_w8": (32, 8 << 20, "f32", "f32", "north star, one rank's share at 8 GPUs (strong scaling): 32 x 32 MiB"),
 }
 ROTATE_MIN_BYTES = 1 << 30  # rotate input sets until a step's working set no longer fits the 256 MiB MALL
 
@@ -156,8 +164,6 @@ class Setup:
                 # global client id and element offset: ranks hold disjoint clients or slices of one bucket
                 fa.fill_uniform(ptr, cnt, self.in_dt, seed + s, client0 + k, idx0=elem0)
         self.w = self._weights(D)
-        # pool placement chosen by fa_bucket_define (probe times of the candidates)
-        self.placement = [self.agg.placement(s, 0) for s in range(self.nsets)]
 
     @staticmethod
     def _weights(D):
@@ -253,13 +259,13 @@ def time_client_sharded(torch, dist, shard, setup, layout, n, world, device, str
     return time.perf_counter() - t0
 
 
-def layout_desc_of(layout, D, chunks):
+def layout_desc_of(layout, D, world, chunks):
     if layout == "rs":
         return ("client-sharded: each rank reduces its %d whole clients into fp32 partials, RCCL "
                 "reduce-scatter over xGMI in %d chunks overlapped with the reduction (block-cyclic "
                 "ownership, one launch per chunk)" % (D, chunks))
-    return ("client-sharded, bit-exact: the fp32 chain is handed rank to rank over RCCL p2p in %d "
-            "chunks, last rank scatters the ranges" % chunks)
+    return ("client-sharded, bit-exact: each rank chains its %d whole clients and hands the fp32 chain to the "
+            "next rank over RCCL p2p in %d chunks, last rank scatters the ranges" % (D, chunks))
 
 
 class LinePrinter:
@@ -283,27 +289,74 @@ def load_shard():
     return importlib.import_module("mhfsl_amd.shard")
 
 
+def spawn_ranks(n, argv):
+    """`--gpus N` (N > 1) without a launcher: start N rank processes (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_* in their environment, one GPU each) and wait for them.  Runs before this process touches
+    torch or HIP, so nothing is exec'd after GPU init; returns the worst exit code.  Should one rank
+    fail, the others get a grace period and are then terminated (a collective would otherwise wait
+    for the dead rank forever)."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + argv, env=env))
+    grace = float(os.environ.get("FA_BENCH_RANK_GRACE", "60"))
+    failed_at = None
+    while True:
+        rcs = [p.poll() for p in procs]
+        if all(rc is not None for rc in rcs):
+            break
+        if failed_at is None and any(rc not in (None, 0) for rc in rcs):
+            failed_at = time.monotonic()
+            print("bench: a rank exited with %s; waiting %.0f s for the others" % (rcs, grace), file=sys.stderr)
+        if failed_at is not None and time.monotonic() - failed_at > grace:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=20)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            break
+        time.sleep(0.2)
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="northstar", choices=sorted(WORKLOADS))
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong (default): the workload is split over the ranks by element range; weak: every "
+                         "rank reduces a full-size slice of its own")
     ap.add_argument("--layout", default="range", choices=["range", "rs", "chain"])
     ap.add_argument("--chunks", type=int, default=16,
                     help="rs / chain layouts: chunks (reduce of chunk c+1 overlaps the exchange of chunk c)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
-    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL over xGMI) or gloo (rehearsal only)")
+    ap.add_argument("--dist-backend", default="auto",
+                    help="auto (nccl = RCCL over xGMI when every rank has its own GPU, else gloo), nccl or gloo")
     ap.add_argument("--tune", default="", help="block,max_blocks,unroll,load_policy,store_policy (fa_tuning)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world), file=sys.stderr)
     D, n, in_dt, out_dt, desc = WORKLOADS[args.workload]
+    strong = args.scaling == "strong"
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -313,17 +366,21 @@ def main():
     import torch.distributed as dist
     fa = load_pkg()
     shard = load_shard()
-    device = local_rank % max(1, torch.cuda.device_count())  # == local_rank on a node with one GPU per rank
+    n_dev = torch.cuda.device_count()  # counts without initialising the GPU
+    device = local_rank % max(1, n_dev)  # == local_rank on a node with one GPU per rank
+    backend = args.dist_backend
+    if backend == "auto":
+        backend = "nccl" if n_dev >= world else "gloo"
     torch.cuda.set_device(device)
     fa.lib()
     if args.tune:
         b, mb, u, lp, sp = [int(x) for x in args.tune.split(",")]
         fa.set_tuning(block=b, max_blocks=mb, unroll=u, load_policy=lp, store_policy=sp)
     if world > 1:
-        if args.dist_backend == "nccl":
+        if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
-            dist.init_process_group(args.dist_backend)
+            dist.init_process_group(backend)
 
         def barrier():
             dist.barrier()
@@ -331,157 +388,120 @@ def main():
         def barrier():
             pass
 
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
     stream = torch.cuda.Stream()
-    # weak scaling: per-rank work is fixed -- range: a 256 MiB slice of every one of D buckets;
-    # rs / chain: D whole 256 MiB buckets (global clients rank*D .. rank*D+D-1 of D*world).
+    s_in = 4 if in_dt == "f32" else 2
     if args.layout == "range":
-        setup = Setup(fa, torch, D, n, in_dt, out_dt, rank * n, device)
+        # strong: rank r owns elements [lo, hi) of every one of the D buckets (the bucket is split W ways);
+        # weak: rank r owns its own full-size slice [r n, (r+1) n) of D buckets W times as long
+        lo, hi = shard.range_bounds(n, world, rank) if strong else (rank * n, (rank + 1) * n)
+        setup = Setup(fa, torch, D, hi - lo, in_dt, out_dt, lo, device)
+        total_bytes = D * n * s_in * (1 if strong else world)
+        layout_desc = "range-sharded: rank %d owns elements [%d, %d) of every one of %d buckets of %d elements, " \
+                      "no collective" % (rank, lo, hi, D, n if strong else n * world)
     else:
-        setup = Setup(fa, torch, D, n, in_dt, out_dt, 0, device, client0=rank * D)
-        setup.w = Setup._weights(D * world)[rank * D:(rank + 1) * D]
+        # client-sharded: strong: the D clients are dealt to the ranks; weak: every rank holds D clients
+        c0, c1 = shard.client_bounds(D, world, rank) if strong else (rank * D, (rank + 1) * D)
+        setup = Setup(fa, torch, c1 - c0, n, in_dt, out_dt, 0, device, client0=c0)
+        setup.w = Setup._weights(D if strong else D * world)[c0:c1]
+        total_bytes = D * n * s_in * (1 if strong else world)
+        layout_desc = layout_desc_of(args.layout, c1 - c0, world, args.chunks)
     torch.cuda.synchronize()
 
     # the dominant kernel alone (roofline), HIP events on its stream
     wall_k, kern_ms = timed_loop(torch, setup, args.steps, args.warmup, stream, dist, barrier)
     if args.layout == "range":
         wall = wall_k
-        layout_desc = "range-sharded: each rank owns %d of %d elements of every bucket, no collective" % (
-            n, n * world)
     else:
         wall = time_client_sharded(torch, dist, shard, setup, args.layout, n, world, device, stream, args.steps,
                                    args.warmup, args.chunks, barrier)
-        layout_desc = layout_desc_of(args.layout, D, args.chunks)
-    units_bytes = setup.input_bytes() * world
-
-    if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
+    wall = max_over_ranks(wall)
 
     kavg = statistics.mean(kern_ms)
     achieved = setup.algo_bytes() / (kavg * 1e-3) / 1e9
     traffic, traffic_src = traffic_from_profile(args.workload, world)
     line = {
         "metric": "GiB/s aggregated (device-resident), D-client fp32 bucket FedAvg reduce",
-        "value": round(units_bytes * args.steps / wall / 2**30, 3),
+        "value": round(total_bytes * args.steps / wall / 2**30, 3),
         "unit": "GiB/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(wall / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": in_dt,
         "data": "synthetic (counter-based splitmix64 uniform[-1,1), generated in HBM)",
-        "config": {"workload": args.workload, "description": desc,
-                   "clients": D * (world if args.layout != "range" else 1),
-                   "elems_per_client": n * (world if args.layout == "range" else 1), "in_dtype": in_dt,
-                   "out_dtype": out_dt, "layout": layout_desc, "parallelism": "%s%d" % (args.layout, world),
-                   "tuning": fa.get_tuning(), "input_sets_rotated": setup.nsets,
-                   "placement": setup.placement},
+        "config": {"workload": args.workload, "description": desc, "clients": D,
+                   "elems_per_client": n * (1 if strong else world), "in_dtype": in_dt, "out_dtype": out_dt,
+                   "layout": layout_desc, "parallelism": "%s%d" % (args.layout, world),
+                   "world_size": dist.get_world_size() if world > 1 else 1,
+                   "dist_backend": backend if world > 1 else None,
+                   "tuning": setup.agg.get_tuning(), "input_sets_rotated": setup.nsets},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": setup.algo_bytes(),
                      "kernel_ms_avg": round(kavg, 4), "kernel_ms_min": round(min(kern_ms), 4),
-                     "kernel_ms_median": round(statistics.median(kern_ms), 4)},
+                     "kernel_ms_median": round(statistics.median(kern_ms), 4),
+                     "kernel": "rank %d's launch (%s)" % (rank, "its range of every bucket" if args.layout == "range"
+                                                         else "its clients' local reduction")},
         "cpu_baseline": cpu,
     }
+    if world > 1:
+        line["roofline"]["kernel_ms_avg_max_over_ranks"] = round(max_over_ranks(kavg), 4)
 
     if rank == 0 and world == 1 and not args.no_secondary:
-        sec = {}
         setup.close()
-        for name in sorted(WORKLOADS):
-            if name == args.workload:
-                continue
-            sD, sn, si, so, sdesc = WORKLOADS[name]
-            s = Setup(fa, torch, sD, sn, si, so, 0, device)
-            torch.cuda.synchronize()
-            w2, km = timed_loop(torch, s, max(10, args.steps), 3, stream, dist, barrier)
-            ka = statistics.mean(km)
-            sec[name] = {"description": sdesc, "gib_s": round(s.input_bytes() * max(10, args.steps) / w2 / 2**30, 1),
-                         "kernel_ms_avg": round(ka, 4),
-                         "achieved_GBs": round(s.algo_bytes() / (ka * 1e-3) / 1e9, 1),
-                         "algorithmic_bytes_per_launch": s.algo_bytes(),
-                         "traffic": traffic_from_profile(name, 1)[0],
-                         "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                         "input_sets_rotated": s.nsets, "placement": s.placement}
-            s.close()
-        # compute-node aggregation on the C2 shape: 8 client copies synced in place
-        sD, sn, si, so, _ = WORKLOADS["c2"]
-        s = SyncSetup(fa, torch, sD, sn, si, so, 0, device)
-        torch.cuda.synchronize()
-        w2, km = timed_loop(torch, s, max(10, args.steps), 3, stream, dist, barrier)
-        ka = statistics.mean(km)
-        sec["sync_c2"] = {"description": "compute-node state sync, 8 client copies of the ResNet-18 buckets, fp32, "
-                                         "in place (D reads + D writes per element)",
-                          "kernel_ms_avg": round(ka, 4),
-                          "achieved_GBs": round(s.algo_bytes() / (ka * 1e-3) / 1e9, 1),
-                          "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                          "input_sets_rotated": s.nsets}
-        s.close()
-        # the same on a large part: 8 copies of VGG-19's FC part (119.6 M parameters, C4's split 3,19)
-        s = SyncSetup(fa, torch, 8, 119_586_826, "f32", "f32", 0, device)
-        torch.cuda.synchronize()
-        w2, km = timed_loop(torch, s, max(10, args.steps), 3, stream, dist, barrier)
-        ka = statistics.mean(km)
-        sec["sync_vgg_fc"] = {"description": "compute-node state sync, 8 client copies of VGG-19's FC part "
-                                             "(119.6 M fp32 parameters), in place",
-                              "kernel_ms_avg": round(ka, 4),
-                              "achieved_GBs": round(s.algo_bytes() / (ka * 1e-3) / 1e9, 1),
-                              "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                              "input_sets_rotated": s.nsets}
-        s.close()
-        # the reference's own semantics (aggregator.cpp:72-88, literal mode): fl(fl(x+x)/1000) of the last
-        # receipt, on its largest bucket (VGG-19's FC part); per element one read + one write
-        s = Setup(fa, torch, 1, 119_586_826, "f32", "f32", 0, device, mode=fa.LITERAL)
-        torch.cuda.synchronize()
-        w2, km = timed_loop(torch, s, max(10, args.steps), 3, stream, dist, barrier)
-        ka = statistics.mean(km)
-        sec["literal_vgg_fc"] = {"description": "reference-literal mode fl(fl(x+x)/1000) of the last receipt, "
-                                                "VGG-19's FC part (119.6 M fp32 parameters)",
-                                 "kernel_ms_avg": round(ka, 4),
-                                 "achieved_GBs": round(s.algo_bytes() / (ka * 1e-3) / 1e9, 1),
-                                 "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                                 "input_sets_rotated": s.nsets}
-        s.close()
-        line["secondary"] = sec
+        line["secondary"] = single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier)
 
     printer = LinePrinter(rank)
     if world > 1 and not args.no_secondary and args.layout == "range":
-        # the client-sharded layouts on the same ranks, as secondaries (the RCCL legs: reduce-scatter and
-        # the p2p chain).  A watchdog bounds them: should a collective stall, rank 0 still prints the
-        # main line (marked) and every rank exits.
+        # the other layouts on the same ranks, as secondaries: weak-scaled range (every rank a full 256 MiB
+        # slice), and the client-sharded RCCL legs (reduce-scatter, p2p chain) on the same strong problem.
+        # A watchdog bounds them: should a collective stall, rank 0 still prints the main line (marked)
+        # and every rank exits.
         limit = float(os.environ.get("FA_BENCH_SECONDARY_TIMEOUT", "90"))
-
         done = threading.Event()
 
         def watchdog():
             if not done.wait(limit):
-                print("rank %d: client-sharded layouts still running after %.0f s; stacks:" % (rank, limit),
+                print("rank %d: secondary layouts still running after %.0f s; stacks:" % (rank, limit),
                       file=sys.stderr, flush=True)
                 faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
-                line["secondary_error"] = "client-sharded layouts did not finish within %.0f s" % limit
+                line["secondary_error"] = "secondary layouts did not finish within %.0f s" % limit
                 printer.emit(line)
                 os._exit(0)
         threading.Thread(target=watchdog, daemon=True).start()
         setup.close()
         sec = line["secondary"] = {}  # filled layout by layout, so a watchdog exit keeps what finished
         steps2 = max(10, args.steps)
-        for L in ("rs", "chain"):
+        for L in ("weak_range", "rs", "chain"):
             try:
-                s2 = Setup(fa, torch, D, n, in_dt, out_dt, 0, device, client0=rank * D)
-                s2.w = Setup._weights(D * world)[rank * D:(rank + 1) * D]
-                torch.cuda.synchronize()
-                w2 = time_client_sharded(torch, dist, shard, s2, L, n, world, device, stream, steps2, 3,
-                                         args.chunks, barrier)
-                t = torch.tensor([w2], dtype=torch.float64, device="cuda")
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                w2 = float(t.item())
-                sec[L] = {"description": layout_desc_of(L, D, args.chunks), "clients": D * world,
-                          "elems_per_client": n, "steps": steps2, "ms_per_step": round(w2 / steps2 * 1e3, 4),
-                          "gib_s": round(s2.input_bytes() * world * steps2 / w2 / 2**30, 1)}
+                if L == "weak_range":
+                    s2 = Setup(fa, torch, D, n, in_dt, out_dt, rank * n, device)
+                    torch.cuda.synchronize()
+                    w2, _ = timed_loop(torch, s2, steps2, 3, stream, dist, barrier)
+                    tb, desc2 = D * n * s_in * world, "weak scaling: every rank reduces its own %d-element slice " \
+                                                       "of %d buckets, no collective" % (n, D)
+                else:
+                    c0, c1 = shard.client_bounds(D, world, rank)
+                    s2 = Setup(fa, torch, c1 - c0, n, in_dt, out_dt, 0, device, client0=c0)
+                    s2.w = Setup._weights(D)[c0:c1]
+                    torch.cuda.synchronize()
+                    w2 = time_client_sharded(torch, dist, shard, s2, L, n, world, device, stream, steps2, 3,
+                                             args.chunks, barrier)
+                    tb, desc2 = D * n * s_in, layout_desc_of(L, c1 - c0, world, args.chunks)
+                w2 = max_over_ranks(w2)
+                sec[L] = {"description": desc2, "clients": D, "steps": steps2,
+                          "ms_per_step": round(w2 / steps2 * 1e3, 4), "gib_s": round(tb * steps2 / w2 / 2**30, 1)}
                 s2.close()
             except Exception as e:  # noqa: BLE001 -- the ranks may now disagree: report and leave
                 traceback.print_exc()
@@ -494,6 +514,50 @@ def main():
     printer.emit(line)
     if world > 1:
         dist.destroy_process_group()
+
+
+def single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier):
+    """The other BASELINE configs' single-GPU shapes, compute-node sync and literal mode (rank 0, N = 1)."""
+    sec = {}
+    for name in sorted(WORKLOADS):
+        if name == args.workload:
+            continue
+        sD, sn, si, so, sdesc = WORKLOADS[name]
+        s = Setup(fa, torch, sD, sn, si, so, 0, device)
+        torch.cuda.synchronize()
+        w2, km = timed_loop(torch, s, max(10, args.steps), 3, stream, dist, barrier)
+        ka = statistics.mean(km)
+        sec[name] = {"description": sdesc, "gib_s": round(s.input_bytes() * max(10, args.steps) / w2 / 2**30, 1),
+                     "kernel_ms_avg": round(ka, 4),
+                     "achieved_GBs": round(s.algo_bytes() / (ka * 1e-3) / 1e9, 1),
+                     "algorithmic_bytes_per_launch": s.algo_bytes(),
+                     "traffic": traffic_from_profile(name, 1)[0],
+                     "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "input_sets_rotated": s.nsets}
+        s.close()
+
+    def one(key, s, desc):
+        torch.cuda.synchronize()
+        _, km = timed_loop(torch, s, max(10, args.steps), 3, stream, dist, barrier)
+        ka = statistics.mean(km)
+        sec[key] = {"description": desc, "kernel_ms_avg": round(ka, 4),
+                    "achieved_GBs": round(s.algo_bytes() / (ka * 1e-3) / 1e9, 1),
+                    "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                    "input_sets_rotated": s.nsets}
+        s.close()
+    # compute-node aggregation (SURVEY.md 8f row 4) on the C2 shape: 8 client copies synced in place
+    sD, sn, si, so, _ = WORKLOADS["c2"]
+    one("sync_c2", SyncSetup(fa, torch, sD, sn, si, so, 0, device),
+        "compute-node state sync, 8 client copies of the ResNet-18 buckets, fp32, in place "
+        "(D reads + D writes per element)")
+    # the same on a large part: 8 copies of VGG-19's FC part (119.6 M parameters, C4's split 3,19)
+    one("sync_vgg_fc", SyncSetup(fa, torch, 8, 119_586_826, "f32", "f32", 0, device),
+        "compute-node state sync, 8 client copies of VGG-19's FC part (119.6 M fp32 parameters), in place")
+    # the reference's own semantics (aggregator.cpp:72-88, literal mode): fl(fl(x+x)/1000) of the last
+    # receipt, on its largest bucket (VGG-19's FC part); per element one read + one write
+    one("literal_vgg_fc", Setup(fa, torch, 1, 119_586_826, "f32", "f32", 0, device, mode=fa.LITERAL),
+        "reference-literal mode fl(fl(x+x)/1000) of the last receipt, VGG-19's FC part (119.6 M fp32 parameters)")
+    return sec
 
 
 if __name__ == "__main__":

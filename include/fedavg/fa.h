@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 3
+#define FA_ABI_VERSION 4
 
 typedef struct fa_ctx fa_ctx; /* opaque: device slots, streams, pinned staging */
 
@@ -49,11 +49,26 @@ typedef enum {
     FA_ERR_NOMEM = -3,   /* device or pinned allocation failed */
     FA_ERR_STATE = -4,   /* call out of order (e.g. finalize before any submit) */
     FA_ERR_NODEV = -5,   /* no usable gfx950 device */
-    FA_ERR_ALIGN = -6    /* pointer not 4-byte (f32) / 2-byte (bf16) aligned */
+    FA_ERR_ALIGN = -6,   /* pointer not 4-byte (f32) / 2-byte (bf16) aligned */
+    FA_ERR_NCCL = -7     /* an RCCL call failed (FA_SHARD_CLIENT_RS) */
 } fa_status;
 
 /* fa_create flags */
-#define FA_SHARD_RANGE 0x1 /* n_gpus > 1: GPU g owns elements [g*n/G, (g+1)*n/G) of every bucket */
+/* n_gpus > 1: GPU g owns elements [g*n/G, (g+1)*n/G) of every client bucket; bit-exact, no collective. */
+#define FA_SHARD_RANGE 0x1
+/* Client-sharded: GPU g holds whole buckets of clients [c_g, c_{g+1}) (contiguous, balanced), reduces them
+ * into an fp32 partial, and an RCCL reduce-scatter over xGMI (one communicator per GPU, ncclCommInitAll in
+ * this process) sums the partials piece by piece, overlapped with the reduction of the next piece
+ * (fa_tuning.rs_chunks pieces; GPU g ends with block g of every piece, fa_rs_segments).  The summation
+ * order changes: within 1e-6 of sum_k |w_k x_k| (bit-exact at n_gpus = 1).  Out dtype f32 only. */
+#define FA_SHARD_CLIENT_RS 0x2
+/* Accumulate on arrival (range layout, FedAvg): as soon as receipts 0..k-1 of a round are all in, their
+ * ordered chain is enqueued (continued in an fp32 accumulator), so the phase end only reduces the
+ * clients that came late or out of order.  Same bits as one chain. */
+#define FA_ACCUMULATE_ON_ARRIVAL 0x4
+/* Test only: accept a device id more than once (several shards of one context on one GPU), so the
+ * multi-GPU host logic runs on a one-GPU box. */
+#define FA_TEST_SHARED_DEVICE 0x100
 
 int fa_version(void);
 const char* fa_last_error(void); /* thread-local; "" when the last call succeeded */
@@ -63,7 +78,8 @@ int fa_device_count(int* out);   /* visible HIP devices */
  * + refactor() -> init_model_sate (aggregator.cpp:47,53; systemAPI.cpp:17-38).
  * Uses devices 0..n_gpus-1. */
 int fa_create(fa_ctx** out, int n_gpus, int flags);
-/* Same on an explicit device list (e.g. {LOCAL_RANK} for one process per GPU). */
+/* Same on an explicit device list (e.g. {LOCAL_RANK} for one process per GPU).  Every id once
+ * (FA_SHARD_CLIENT_RS needs distinct devices for its RCCL communicators). */
 int fa_create_ex(fa_ctx** out, const int* device_ids, int n_gpus, int flags);
 void fa_destroy(fa_ctx* ctx);
 
@@ -122,16 +138,25 @@ int fa_host_free(void* p);
  * NULL = ctx compute streams; non-NULL only for a single-GPU ctx.  Async. */
 int fa_reduce_part(fa_ctx* ctx, int part_id, const float* h_weights, void* hip_stream);
 /* Device pointer of client slot `client_slot` on GPU `gpu` (n_elems elements of
- * the input dtype, covering bucket elements [elem_offset, elem_offset+n_elems)),
- * and of the part's device output.  Slots of one bucket share one allocation
+ * the input dtype, covering bucket elements [elem_offset, elem_offset+n_elems);
+ * FA_SHARD_CLIENT_RS: only the GPU holding the client, whole bucket).  Slots of one bucket share one allocation
  * with a small per-slot byte skew (fa_tuning.slot_skew) so that the wave's
  * simultaneous loads spread over HBM channels. */
 int fa_bucket_slot(fa_ctx* ctx, int part_id, int gpu, int client_slot, void** d_ptr, size_t* n_elems,
                    size_t* elem_offset);
+/* The part's device output on GPU `gpu` (range: its shard, `out` dtype; rs: its fp32 shard, the blocks
+ * fa_rs_segments lists, concatenated). */
 int fa_bucket_output(fa_ctx* ctx, int part_id, int gpu, void** d_ptr);
-/* Placement probe record of a bucket pool on GPU `gpu`: how many candidates were timed (0 = not
- * probed), their probe times in ms (probe_ms: room for 8), and the index of the one kept. */
-int fa_bucket_placement(fa_ctx* ctx, int part_id, int gpu, int* n_probes, float* probe_ms, int* chosen);
+/* This round's receipts so far and how many leading client slots are already reduced
+ * (FA_ACCUMULATE_ON_ARRIVAL; n_reduced == D once the round's result is ready). */
+int fa_bucket_progress(fa_ctx* ctx, int part_id, int* n_submitted, int* n_reduced);
+/* Batched device-resident reduction of several parts (e.g. all last-part layers of a phase,
+ * aggregator.cpp:108-150): one launch per GPU covers every part that is FedAvg, range-laid-out, has at
+ * most 128 clients and is below the phased kernel's size (a segment table: one bucket per segment,
+ * the same ordered chain, the same bits); larger parts get their own launch.  h_weights: NULL or one
+ * entry per part (NULL entry = the weights given to fa_submit).  A following fa_finalize* of these
+ * parts only copies the result out.  Async on hip_stream (NULL = ctx compute streams). */
+int fa_reduce_parts(fa_ctx* ctx, int n_parts, const int* part_ids, const float* const* h_weights, void* hip_stream);
 /* D2H of the part's current device output (after fa_reduce_part), waiting for it. */
 int fa_copy_output(fa_ctx* ctx, int part_id, void* host_dst);
 /* Wait for all copy and compute work of the ctx. */
@@ -182,8 +207,6 @@ typedef struct {
     int store_policy; /* output stores: 1 plain, 2 nt, 3 sc1 (write-through), 4 sc0 sc1 */
     int slot_skew;    /* bytes between consecutive client slots beyond 4 KiB alignment (multiple of 16);
                          -1 = none; applies to buckets defined afterwards */
-    int placement_probes; /* FedAvg bucket pools >= 1 GiB: at most this many candidate allocations are
-                             timed and the fastest kept; -1 = 1 (no probing); default 8 */
     int walk;         /* FedAvg grid walk over a bucket: 1 linear, 2 each XCD's workgroups own one contiguous
                          eighth, 3 the same with the odd eighths walked backwards (one-shot grid only),
                          4 phased: a persistent grid (one workgroup per CU) reduces a phase into LDS and
@@ -192,10 +215,23 @@ typedef struct {
                          take the form of walk 6), 6 phased with 512-thread workgroups (2 waves per
                          SIMD).  Buckets smaller than one phase (walk 4: 18.9 M, walks 5 and 6:
                          23.1 M elements per GPU on 256 CUs, f32 or bf16) take walk 2.  The phased
-                         kernels always use nt loads and sc1 stores */
+                         kernels always use nt loads and sc1 stores.  With walk 5, a bucket below one
+                         phase with >= 16 clients takes one phase sized to it */
+    int rs_chunks;    /* FA_SHARD_CLIENT_RS: pieces per round (default 8) */
 } fa_tuning;
+/* Process defaults: every fa_ctx created afterwards starts from them, and fa_reduce_device /
+ * fa_sync_device without a ctx use them. */
 int fa_set_tuning(const fa_tuning* t);
 int fa_get_tuning(fa_tuning* t);
+/* One context's own tuning (buckets defined afterwards take its slot_skew). */
+int fa_ctx_set_tuning(fa_ctx* ctx, const fa_tuning* t);
+int fa_ctx_get_tuning(fa_ctx* ctx, fa_tuning* t);
+
+/* The rs layout's block-cyclic ownership (FA_SHARD_CLIENT_RS): bucket elements [lo, hi) that GPU `gpu`
+ * of n_gpus holds after the reduce-scatter of a bucket of n elements in `chunks` pieces, in the order of
+ * its shard (lo_hi: room for 2 * cap values; elements >= n are padding).  Returns the segment count.
+ * Pure host arithmetic (no device needed). */
+int fa_rs_segments(size_t n, int n_gpus, int chunks, int gpu, size_t* lo_hi, int cap);
 
 #ifdef __cplusplus
 }

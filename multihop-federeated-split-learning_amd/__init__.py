@@ -19,8 +19,8 @@ LIB_PATH = os.path.join(PKG_DIR, "lib", "libfa.so")
 
 F32, BF16 = 0, 1
 FEDAVG, LITERAL = 0, 1
-SHARD_RANGE = 0x1
-OK, ERR_ARG, ERR_HIP, ERR_NOMEM, ERR_STATE, ERR_NODEV, ERR_ALIGN = 0, -1, -2, -3, -4, -5, -6
+SHARD_RANGE, SHARD_CLIENT_RS, ACCUMULATE_ON_ARRIVAL, TEST_SHARED_DEVICE = 0x1, 0x2, 0x4, 0x100
+OK, ERR_ARG, ERR_HIP, ERR_NOMEM, ERR_STATE, ERR_NODEV, ERR_ALIGN, ERR_NCCL = 0, -1, -2, -3, -4, -5, -6, -7
 DTYPE_SIZE = {F32: 4, BF16: 2}
 
 _lib = None
@@ -35,7 +35,7 @@ class FaError(RuntimeError):
 class _Tuning(ctypes.Structure):
     _fields_ = [("block", ctypes.c_int), ("max_blocks", ctypes.c_int), ("unroll", ctypes.c_int),
                 ("load_policy", ctypes.c_int), ("store_policy", ctypes.c_int), ("slot_skew", ctypes.c_int),
-                ("placement_probes", ctypes.c_int), ("walk", ctypes.c_int)]
+                ("walk", ctypes.c_int), ("rs_chunks", ctypes.c_int)]
 
 
 def build():
@@ -78,7 +78,11 @@ def lib():
         "fa_host_free": (I, [P]),
         "fa_sync_device": (I, [P, I, P, P, I, S, I, P]),
         "fa_sync_part": (I, [P, I, P, P]),
-        "fa_bucket_placement": (I, [P, I, I, ctypes.POINTER(I), ctypes.POINTER(F), ctypes.POINTER(I)]),
+        "fa_bucket_progress": (I, [P, I, ctypes.POINTER(I), ctypes.POINTER(I)]),
+        "fa_reduce_parts": (I, [P, I, ctypes.POINTER(I), P, P]),
+        "fa_ctx_set_tuning": (I, [P, ctypes.POINTER(_Tuning)]),
+        "fa_ctx_get_tuning": (I, [P, ctypes.POINTER(_Tuning)]),
+        "fa_rs_segments": (I, [S, I, I, I, ctypes.POINTER(S), I]),
         "fa_reduce_device": (I, [P, I, P, P, I, S, I, P, I, I, P, P]),
         "fa_fill_uniform": (I, [P, S, I, U64, U32, U64, P]),
         "fa_set_tuning": (I, [ctypes.POINTER(_Tuning)]),
@@ -156,24 +160,38 @@ def fill_uniform(dst, n, dtype, seed, client, idx0=0, stream=None):
     check(lib().fa_fill_uniform(_addr(dst), n, dtype, seed, client, idx0, _stream(stream)))
 
 
+def _tuning_dict(t):
+    return {"block": t.block, "max_blocks": t.max_blocks, "unroll": t.unroll, "load_policy": t.load_policy,
+            "store_policy": t.store_policy, "slot_skew": t.slot_skew, "walk": t.walk, "rs_chunks": t.rs_chunks}
+
+
 def get_tuning():
+    """fa_get_tuning: the process defaults (new contexts and context-less calls start from them)."""
     t = _Tuning()
     check(lib().fa_get_tuning(ctypes.byref(t)))
-    return {"block": t.block, "max_blocks": t.max_blocks, "unroll": t.unroll, "load_policy": t.load_policy,
-            "store_policy": t.store_policy, "slot_skew": t.slot_skew, "placement_probes": t.placement_probes,
-            "walk": t.walk}
+    return _tuning_dict(t)
 
 
 LOAD_DEFAULT, LOAD_NT = 1, 2
 STORE_PLAIN, STORE_NT, STORE_SC1, STORE_SC01 = 1, 2, 3, 4
 
 
-def set_tuning(block=0, max_blocks=0, unroll=0, load_policy=0, store_policy=0, slot_skew=0, placement_probes=0,
-               walk=0):
-    """fa_set_tuning; every argument 0 = keep.  max_blocks -1 = one-shot grid, slot_skew -1 = none,
-    placement_probes -1 = no probing."""
-    t = _Tuning(block, max_blocks, unroll, load_policy, store_policy, slot_skew, placement_probes, walk)
+def set_tuning(block=0, max_blocks=0, unroll=0, load_policy=0, store_policy=0, slot_skew=0, walk=0, rs_chunks=0):
+    """fa_set_tuning (process defaults); every argument 0 = keep.  max_blocks -1 = one-shot grid,
+    slot_skew -1 = none."""
+    t = _Tuning(block, max_blocks, unroll, load_policy, store_policy, slot_skew, walk, rs_chunks)
     check(lib().fa_set_tuning(ctypes.byref(t)))
+
+
+def rs_segments(n, n_gpus, chunks, gpu):
+    """fa_rs_segments: [(lo, hi), ...] of bucket elements GPU `gpu` holds after the rs layout's
+    reduce-scatter (block-cyclic over `chunks` pieces), in the order of its shard."""
+    cnt = lib().fa_rs_segments(n, n_gpus, chunks, gpu, None, 0)
+    if cnt < 0:
+        check(cnt)
+    buf = (ctypes.c_size_t * (2 * max(1, cnt)))()
+    lib().fa_rs_segments(n, n_gpus, chunks, gpu, buf, cnt)
+    return [(buf[2 * i], buf[2 * i + 1]) for i in range(cnt)]
 
 
 HOST_PINNED = 0x1
@@ -219,12 +237,13 @@ class Aggregator:
     once (refactor), submit every receipt, finalize to obtain the reduced part.
     """
 
-    def __init__(self, n_gpus=1, flags=None, devices=None):
+    def __init__(self, n_gpus=1, flags=None, devices=None, rs=False, eager=False, shared_device=False):
         if devices is None:
             devices = list(range(n_gpus))
         n_gpus = len(devices)
         if flags is None:
-            flags = SHARD_RANGE if n_gpus > 1 else 0
+            flags = SHARD_CLIENT_RS if rs else SHARD_RANGE if n_gpus > 1 else 0
+            flags |= (ACCUMULATE_ON_ARRIVAL if eager else 0) | (TEST_SHARED_DEVICE if shared_device else 0)
         h = ctypes.c_void_p()
         ids = (ctypes.c_int * n_gpus)(*devices)
         check(lib().fa_create_ex(ctypes.byref(h), ids, n_gpus, flags))
@@ -289,12 +308,32 @@ class Aggregator:
                                    ctypes.byref(off)))
         return ptr.value, n.value, off.value
 
-    def placement(self, part_id, gpu=0):
-        """fa_bucket_placement: {"probe_ms": [...], "chosen": i} ({"probe_ms": []} when not probed)."""
-        n, ch = ctypes.c_int(), ctypes.c_int()
-        ms = (ctypes.c_float * 8)()
-        check(lib().fa_bucket_placement(self.handle, part_id, gpu, ctypes.byref(n), ms, ctypes.byref(ch)))
-        return {"probe_ms": [round(ms[i], 4) for i in range(n.value)], "chosen": ch.value}
+    def progress(self, part_id):
+        """fa_bucket_progress: (receipts submitted this round, leading slots already reduced)."""
+        a, b = ctypes.c_int(), ctypes.c_int()
+        check(lib().fa_bucket_progress(self.handle, part_id, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+    def reduce_parts(self, part_ids, weights=None, stream=None):
+        """fa_reduce_parts: one batched reduction of several parts (async); weights: None or one array per
+        part (None entries = the submitted weights)."""
+        ids = (ctypes.c_int * len(part_ids))(*part_ids)
+        wp = None
+        if weights is not None:
+            keep = [None if w is None else np.ascontiguousarray(np.asarray(w, np.float32)) for w in weights]
+            self._w_keep = keep
+            wp = (ctypes.c_void_p * len(part_ids))(*[None if w is None else w.ctypes.data for w in keep])
+        check(lib().fa_reduce_parts(self.handle, len(part_ids), ids, wp, _stream(stream)))
+
+    def set_tuning(self, **kw):
+        """fa_ctx_set_tuning: this context's tuning (same keys as set_tuning; 0 = keep)."""
+        t = _Tuning(*[kw.get(k, 0) for k, _ in _Tuning._fields_])
+        check(lib().fa_ctx_set_tuning(self.handle, ctypes.byref(t)))
+
+    def get_tuning(self):
+        t = _Tuning()
+        check(lib().fa_ctx_get_tuning(self.handle, ctypes.byref(t)))
+        return _tuning_dict(t)
 
     def output(self, part_id, gpu=0):
         ptr = ctypes.c_void_p()

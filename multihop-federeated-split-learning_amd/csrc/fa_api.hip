@@ -1,5 +1,7 @@
 // fa_api.hip -- the C ABI (include/fedavg/fa.h): aggregation context, device
-// slots, pinned staging, multi-GPU range sharding, and the raw device entry.
+// slots, pinned staging, multi-GPU layouts (range shards; client shards + an
+// RCCL reduce-scatter), batched and accumulate-on-arrival reductions, and the
+// raw device entry.
 //
 // What it replaces in the reference (paths relative to the reference root):
 //   fa_create / fa_bucket_define  <- systemAPI(true,-1,..) + refactor() ->
@@ -7,26 +9,28 @@
 //       model parts the aggregator owns.
 //   fa_submit                     <- one receipt: torch::load of Task.model_parts
 //       into parts_[..] and the per-parameter update (aggregator.cpp:60-92,
-//       :113-149).  Here the bytes are staged to HBM; the arithmetic is deferred
-//       to finalize so that it runs as one ordered chain over all clients.
+//       :113-149).  Here the bytes are staged to HBM; the arithmetic runs as one
+//       ordered chain over all clients, at the phase end or (FA_ACCUMULATE_ON_ARRIVAL)
+//       continued as the in-order prefix of receipts grows.
 //   fa_finalize                   <- the reduced module handed to new_message()
 //       (aggregator.cpp:96-106, :153-166).
 // No CPU fallback exists: without a gfx950 device every entry that needs one
 // returns FA_ERR_NODEV.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <condition_variable>
 #include <cstdarg>
+#include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
-#include <thread>
-#include <cstdio>
-#include <cstring>
-#include <map>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "fa_internal.h"
@@ -34,22 +38,27 @@
 namespace {
 
 thread_local std::string g_err;
-// block 128, one-shot grid, 16 clients per load group, nt loads, write-through (sc1) stores:
-// tools/sweep.py over 3 pools (profiles/r01_summary.json): sc1 stores 2.7% faster than nt,
-// unroll 16 ~1% faster than 8, block 128 2-3% faster than 256; XCD-eighths walk 0.5-1.5% faster than
-// linear in 7 of 9 pools over the north star, C3 and C4 (gpurun_out r01s11, profiles/r01_summary.json).
-// Default walk: phased with the larger register stage (fa_kernels.hip, fedavg_phased_kernel) wherever
-// a bucket holds a full phase, the XCD-eighths one-shot grid below that: in one process over 3 pools
-// each (gpurun_out r01s18) 1.269 ms north star in every pool (XCD walk 1.42 there: all slow pools),
-// and ahead of the XCD walk on C3, C4 and C5's per-rank share too.
-fa::Tuning g_tuning{128, 0, 16, 1, 2, 4};
-// Byte skew between consecutive client slots of one bucket (see slot_stride).
-size_t g_slot_skew = 2048;
-// Placement probing of large FedAvg bucket pools (see alloc_placed): at most this many candidates.
-int g_placement_probes = 8;
-constexpr size_t kProbeMinBytes = 1ull << 30;  // smaller pools: one allocation, no probe
-constexpr double kFastGBs = 0.83 * 8000.0;     // a candidate at >= 83% of the 8 TB/s spec is kept at once
-constexpr int kMaxProbeRecord = 8;
+
+// Per-context tuning (fa_ctx_set_tuning); fa_set_tuning sets the process defaults that new contexts and
+// context-less fa_reduce_device calls start from.
+struct CtxTuning {
+    // block 128, one-shot grid, 16 clients per load group, nt loads, write-through (sc1) stores, phased
+    // walk with the larger register stage where a bucket holds a phase (tools/sweep.py over 3
+    // pools, profiles/r01_summary.json: sc1 stores 2.7% faster than nt, unroll 16 ~1% faster than 8,
+    // block 128 2-3% faster than 256; the phased walk 1.269 ms on the north star in every pool).
+    fa::Tuning tu{128, 0, 16, 1, 2, 4};
+    // Byte skew between consecutive client slots of one bucket (see slot_stride).
+    size_t slot_skew = 2048;
+    // FA_SHARD_CLIENT_RS: pieces per round (the reduce-scatter of piece c overlaps the reduce of c+1).
+    int rs_chunks = 8;
+};
+std::mutex g_defaults_mu;
+CtxTuning g_defaults;
+
+CtxTuning defaults() {
+    std::lock_guard<std::mutex> g(g_defaults_mu);
+    return g_defaults;
+}
 
 int fail(int code, const char* fmt, ...) {
     char buf[512];
@@ -68,6 +77,13 @@ int fail(int code, const char* fmt, ...) {
                                           __FILE__, __LINE__);                                     \
     } while (0)
 
+#define FA_NCCL(call)                                                                                   \
+    do {                                                                                                \
+        ncclResult_t r_ = (call);                                                                       \
+        if (r_ != ncclSuccess) return fail(FA_ERR_NCCL, "%s: %s (%s:%d)", #call, ncclGetErrorString(r_), \
+                                           __FILE__, __LINE__);                                         \
+    } while (0)
+
 inline size_t dsize(fa_dtype t) { return t == FA_F32 ? 4 : 2; }
 inline bool dvalid(int t) { return t == FA_F32 || t == FA_BF16; }
 
@@ -84,41 +100,12 @@ struct DeviceGuard {
 };
 
 constexpr size_t kStageBytes = 32u << 20;  // pinned staging chunk per buffer
+constexpr size_t kShardUnit = 64;          // range shards / rs pieces: multiples of 64 elements (16-B phase kept)
+constexpr int kMaxSegments = 256;          // buckets per batched launch
 
-struct GpuRes {
-    int dev = 0;
-    hipStream_t compute = nullptr, copy = nullptr;
-    char* stage[2] = {nullptr, nullptr};
-    hipEvent_t stage_ev[2] = {nullptr, nullptr};
-    int stage_i = 0;
-    void* scratch = nullptr;  // fp32 chain accumulator for bf16-out, D > kMaxClients
-    size_t scratch_bytes = 0;
-};
-
-struct Part {
-    size_t n = 0;
-    fa_dtype in = FA_F32, out = FA_F32;
-    int D = 0;
-    fa_mode mode = FA_FEDAVG;
-    float divisor = FA_DEFAULT_DIVISOR;
-    std::vector<size_t> off, cnt;  // per-GPU element range
-    std::vector<char*> pool;       // per GPU: D client slots + the output, one allocation
-    std::vector<size_t> stride;    // per GPU: bytes between consecutive slots
-    std::vector<char*> slots;      // per GPU: == pool (slot k at pool + k * stride)
-    std::vector<void*> dout;       // per GPU: pool + D * stride
-    std::vector<float> w;
-    std::vector<std::vector<float>> probe_ms;  // per GPU: probe time of each placement candidate
-    std::vector<int> chosen;                   // per GPU: the candidate kept
-    std::vector<char> submitted;
-    int n_submitted = 0;
-    int last_slot = -1;
-};
-
-}  // namespace
-
-namespace {
 // Host memcpy into / out of the pinned staging chunks, split over worker threads:
-// one thread copies ~8-10 GB/s, a PCIe Gen5 x16 link takes ~50 GB/s.
+// one thread copies ~8-10 GB/s, a PCIe Gen5 x16 link takes ~50 GB/s.  One pool per GPU, so the GPUs of a
+// range-sharded context stage their pieces concurrently.
 class CopyPool {
 public:
     explicit CopyPool(int n) : n_(std::max(1, n)) {
@@ -190,15 +177,91 @@ int default_copy_threads() {
     const unsigned hw = std::thread::hardware_concurrency();
     return (int)std::max(1u, std::min(8u, hw / 2));
 }
+
+// Runs fn(g) for g in [0, G): G > 1 on one thread per GPU (the host-side staging of each GPU is
+// independent), returning the first non-zero status.
+int for_each_gpu(int G, const std::function<int(int)>& fn) {
+    if (G == 1) return fn(0);
+    std::vector<int> rc((size_t)G, FA_OK);
+    std::vector<std::string> err((size_t)G);
+    std::vector<std::thread> th;
+    for (int g = 1; g < G; ++g)
+        th.emplace_back([&, g] {
+            rc[(size_t)g] = fn(g);
+            if (rc[(size_t)g]) err[(size_t)g] = g_err;  // g_err is thread-local
+        });
+    rc[0] = fn(0);
+    if (rc[0]) err[0] = g_err;
+    for (auto& t : th) t.join();
+    for (int g = 0; g < G; ++g)
+        if (rc[(size_t)g]) {
+            g_err = err[(size_t)g];
+            return rc[(size_t)g];
+        }
+    return FA_OK;
+}
+
+struct GpuRes {
+    int dev = 0;
+    hipStream_t compute = nullptr, copy = nullptr, comm = nullptr;
+    char* stage[2] = {nullptr, nullptr};
+    hipEvent_t stage_ev[2] = {nullptr, nullptr};
+    int stage_i = 0;
+    hipEvent_t copy_ev = nullptr;  // orders a reduction after the H2D copies queued on `copy`
+    uint64_t copy_gen = 0;         // H2D batches queued on `copy` so far (a submit adds one)
+    uint64_t copy_ev_gen = 0;      // the batch copy_ev was last recorded after
+    std::map<hipStream_t, uint64_t> waited;  // per stream: the copy batch it last waited for
+    hipEvent_t step_ev = nullptr;  // orders the rs exchange of a piece after its reduction
+    void* scratch = nullptr;       // fp32 chain accumulator for bf16-out, D > kMaxClients
+    size_t scratch_bytes = 0;
+    fa::SegDesc* seg_host = nullptr;  // pinned segment table of the batched launch
+    fa::SegDesc* seg_dev = nullptr;
+    hipEvent_t seg_ev = nullptr;      // the table's last upload (the host copy is rewritten after it)
+    std::unique_ptr<CopyPool> pool;
+    ncclComm_t nccl = nullptr;
+};
+
+// One copy-out run: elements [src, src + cnt) of a GPU's output buffer are bucket elements [dst, dst + cnt).
+struct Run {
+    size_t src, dst, cnt;
+};
+
+struct Part {
+    size_t n = 0;
+    fa_dtype in = FA_F32, out = FA_F32;
+    int D = 0;
+    fa_mode mode = FA_FEDAVG;
+    float divisor = FA_DEFAULT_DIVISOR;
+    bool rs = false;               // FA_SHARD_CLIENT_RS layout
+    size_t npad = 0;               // rs: slot length (n padded to a multiple of G * 64)
+    std::vector<size_t> off, cnt;  // per GPU: bucket elements held by its slots (range: its shard; rs: [0, n))
+    std::vector<int> c0, c1;       // per GPU: the client slots it holds, [c0, c1)
+    std::vector<char*> pool;       // per GPU: its client slots + the output (+ rs partial, eager acc)
+    std::vector<size_t> stride;    // per GPU: bytes between consecutive slots
+    std::vector<void*> dout;       // per GPU: the output (range: cnt elements of `out`; rs: its fp32 shard)
+    std::vector<float*> partial;   // rs: per GPU, fp32 partial over its clients, npad elements
+    std::vector<float*> acc;       // FA_ACCUMULATE_ON_ARRIVAL: per GPU, fp32 chain of the reduced prefix
+    std::vector<hipEvent_t> done;  // per GPU: orders the copy-out after the reduction (see mark_done)
+    std::vector<hipStream_t> done_stream;  // per GPU: the stream the last reduction ran on
+    std::vector<float> w;
+    std::vector<char> submitted;
+    int n_submitted = 0;
+    int last_slot = -1;
+    int reduced = 0;    // accumulate on arrival: slots [0, reduced) are chained into acc (or dout)
+    bool ready = false; // this round's output is reduced already (eager prefix reached D, fa_reduce_parts)
+    std::vector<std::vector<Run>> runs;  // per GPU: where its output goes (set by the last reduction)
+    std::vector<void*> run_src;          // per GPU: the buffer the runs read
+};
+
 }  // namespace
 
 struct fa_ctx {
     int G = 1;
     int flags = 0;
     float divisor = FA_DEFAULT_DIVISOR;
+    CtxTuning tuning;
     std::vector<GpuRes> gpu;
     std::map<int, Part> parts;
-    std::unique_ptr<CopyPool> pool{new CopyPool(default_copy_threads())};
 };
 
 namespace {
@@ -218,9 +281,10 @@ int ensure_scratch(fa_ctx* ctx, int g, size_t bytes) {
 
 bool aligned(const void* p, size_t a) { return ((uintptr_t)p % a) == 0; }
 
-// The device reduction for one GPU, shared by fa_reduce_device and fa_finalize.
-int reduce_on(fa_ctx* ctx, int g, const void* const* clients, const float* w, int D, size_t n, fa_dtype in,
-              void* dst, fa_dtype out, fa_mode mode, float divisor, const float* init, hipStream_t s) {
+// The device reduction for one GPU, shared by every entry: D clients (any D >= 1; more than kMaxClients
+// continue the chain from an fp32 accumulator in further passes) -> dst.
+int reduce_on(fa_ctx* ctx, int g, const fa::Tuning& tu, const void* const* clients, const float* w, int D, size_t n,
+              fa_dtype in, void* dst, fa_dtype out, fa_mode mode, float divisor, const float* init, hipStream_t s) {
     if (n == 0) return FA_OK;
     const size_t si = dsize(in), so = dsize(out);
     const int V = (int)(16 / si);
@@ -245,7 +309,7 @@ int reduce_on(fa_ctx* ctx, int g, const void* const* clients, const float* w, in
     if (init) vec = vec && ((uintptr_t)init + (size_t)head * 4) % 16 == 0;
 
     if (mode == FA_LITERAL) {
-        FA_HIP(fa::launch_literal(clients[D - 1], in, dst, out, divisor, head, nvec, (int64_t)n, vec, g_tuning, s));
+        FA_HIP(fa::launch_literal(clients[D - 1], in, dst, out, divisor, head, nvec, (int64_t)n, vec, tu, s));
         return FA_OK;
     }
 
@@ -272,14 +336,15 @@ int reduce_on(fa_ctx* ctx, int g, const void* const* clients, const float* w, in
         const float* pin = p == 0 ? init : acc;
         const bool last = p == passes - 1;
         void* pdst = last ? dst : acc;
-        FA_HIP(fa::launch_chain(t, nc, in, last ? out : FA_F32, pin, pdst, head, nvec, (int64_t)n, vec, g_tuning, s));
+        FA_HIP(fa::launch_chain(t, nc, in, last ? out : FA_F32, pin, pdst, head, nvec, (int64_t)n, vec, tu, s));
     }
     return FA_OK;
 }
 
 // In-place state sync on GPU g: every slot := sum_k w_k slot_k (rounded to dt).  D <= kMaxClients:
 // one fused launch; more: the chain into fp32 scratch, then broadcast launches of kMaxClients slots.
-int sync_on(fa_ctx* ctx, int g, void* const* slots, const float* w, int D, size_t n, fa_dtype dt, hipStream_t s) {
+int sync_on(fa_ctx* ctx, int g, const fa::Tuning& tu, void* const* slots, const float* w, int D, size_t n,
+            fa_dtype dt, hipStream_t s) {
     if (n == 0) return FA_OK;
     const size_t si = dsize(dt);
     const int V = (int)(16 / si);
@@ -292,7 +357,7 @@ int sync_on(fa_ctx* ctx, int g, void* const* slots, const float* w, int D, size_
         int rc = ensure_scratch(ctx, g, n * 4);
         if (rc) return rc;
         float* acc = static_cast<float*>(ctx->gpu[g].scratch);
-        rc = reduce_on(ctx, g, (const void* const*)slots, w, D, n, dt, acc, FA_F32, FA_FEDAVG, 0.0f, nullptr, s);
+        rc = reduce_on(ctx, g, tu, (const void* const*)slots, w, D, n, dt, acc, FA_F32, FA_FEDAVG, 0.0f, nullptr, s);
         if (rc) return rc;
         for (int k0 = 0; k0 < D; k0 += fa::kMaxClients) {
             fa::ClientTable t;
@@ -301,7 +366,7 @@ int sync_on(fa_ctx* ctx, int g, void* const* slots, const float* w, int D, size_
                 t.src[k] = slots[k0 + k];
                 t.w[k] = 0.0f;
             }
-            FA_HIP(fa::launch_broadcast(t, nc, dt, acc, (int64_t)n, g_tuning, s));
+            FA_HIP(fa::launch_broadcast(t, nc, dt, acc, (int64_t)n, tu, s));
         }
         return FA_OK;
     }
@@ -316,85 +381,47 @@ int sync_on(fa_ctx* ctx, int g, void* const* slots, const float* w, int D, size_
         t.src[k] = slots[k];
         t.w[k] = w[k];
     }
-    FA_HIP(fa::launch_sync(t, D, dt, nullptr, head, nvec, (int64_t)n, vec, g_tuning, s));
+    FA_HIP(fa::launch_sync(t, D, dt, nullptr, head, nvec, (int64_t)n, vec, tu, s));
     return FA_OK;
 }
 
-// Placement of a bucket pool.  The same reduction over the same layout runs at two speeds depending
-// on which physical HBM a large allocation receives: 1.29-1.30 ms vs 1.41-1.42 ms for 32 x 256 MiB
-// (tools/exp_pick.hip: of 8 pools allocated in sequence, 6 fast and 2 slow, each stable over
-// interleaved rounds; physically contiguous pools and 2 MiB-granule VMM pools in any mapping order
-// were slow, tools/exp_vmm.hip; the output's placement does not matter, tools/exp_out.hip).  So a
-// large FedAvg pool is chosen by measurement: allocate a candidate, time the part's own reduction
-// over it (uninitialized contents: the timing does not depend on the values), keep it if it reaches
-// kFastGBs, else keep it allocated (so the next candidate lands elsewhere) and try another, up to
-// g_placement_probes candidates; the fastest is kept and the others are freed.
-int probe_pool(fa_ctx* ctx, int g, const Part& p, size_t stride, char* pool, float* ms_out) {
-    GpuRes& r = ctx->gpu[(size_t)g];
-    const size_t n = p.cnt[(size_t)g];
-    std::vector<const void*> cl((size_t)p.D);
-    for (int k = 0; k < p.D; ++k) cl[(size_t)k] = pool + (size_t)k * stride;
-    std::vector<float> w((size_t)p.D, 1.0f / (float)p.D);
-    void* out = pool + (size_t)p.D * stride;
-    struct Ev {  // destroyed on every return path
-        hipEvent_t e = nullptr;
-        ~Ev() { if (e) (void)hipEventDestroy(e); }
-    } a, b;
-    FA_HIP(hipEventCreate(&a.e));
-    FA_HIP(hipEventCreate(&b.e));
-    float best = 1e30f;
-    int rc = FA_OK;
-    for (int it = 0; it < 4 && rc == FA_OK; ++it) {
-        FA_HIP(hipEventRecord(a.e, r.compute));
-        rc = reduce_on(ctx, g, cl.data(), w.data(), p.D, n, p.in, out, p.out, FA_FEDAVG, 1.0f, nullptr, r.compute);
-        FA_HIP(hipEventRecord(b.e, r.compute));
-        FA_HIP(hipEventSynchronize(b.e));
-        float t = 0;
-        FA_HIP(hipEventElapsedTime(&t, a.e, b.e));
-        if (it > 0) best = std::min(best, t);  // first launch warms up
-    }
-    *ms_out = best;
-    return rc;
+// ------------------------------------------------------------------ layouts
+
+// [c0, c1) of the D client slots held by GPU g of G under the rs layout (contiguous, balanced; chain
+// order kept within a GPU).  Same rule as shard.client_bounds.
+void client_bounds(int D, int G, int g, int* c0, int* c1) {
+    const int base = D / G, extra = D % G;
+    *c0 = g * base + std::min(g, extra);
+    *c1 = *c0 + base + (g < extra ? 1 : 0);
 }
 
-int alloc_placed(fa_ctx* ctx, int g, Part& p, size_t stride, size_t bytes, char** out) {
-    const size_t algo = (size_t)p.D * p.cnt[(size_t)g] * dsize(p.in) + p.cnt[(size_t)g] * dsize(p.out);
-    // The phased walk runs at the same speed in every pool: a part it covers needs no probe.
-    const int64_t phased_from = fa::phased_min_elems(p.in, g_tuning);
-    const bool phased = phased_from > 0 && (int64_t)p.cnt[(size_t)g] >= phased_from;
-    const int probes = (p.mode == FA_FEDAVG && !phased && bytes >= kProbeMinBytes && p.cnt[(size_t)g] > 0)
-                           ? std::max(1, g_placement_probes) : 1;
-    std::vector<char*> cand;
-    std::vector<float>& ms = p.probe_ms[(size_t)g];
-    int best = -1, rc = FA_OK;
-    for (int i = 0; i < probes; ++i) {
-        char* c = nullptr;
-        if (hipMalloc((void**)&c, bytes) != hipSuccess) {  // out of memory for another candidate: stop
-            (void)hipGetLastError();
-            break;
-        }
-        cand.push_back(c);
-        if (probes == 1) {
-            best = 0;
-            break;
-        }
-        float t = 0;
-        if ((rc = probe_pool(ctx, g, p, stride, c, &t))) break;
-        if (ms.size() < (size_t)kMaxProbeRecord) ms.push_back(t);
-        if (best < 0 || t < ms[(size_t)best]) best = i;
-        if ((double)algo / (t * 1e-3) / 1e9 >= kFastGBs) break;
-    }
-    if (cand.empty()) return fail(FA_ERR_NOMEM, "device alloc of %zu B failed on GPU %d", bytes, g);
-    if (best < 0) best = 0;
-    for (size_t i = 0; i < cand.size(); ++i)
-        if ((int)i != best) (void)hipFree(cand[i]);
-    if (rc) {
-        (void)hipFree(cand[(size_t)best]);
-        return rc;
-    }
-    p.chosen[(size_t)g] = best;
-    *out = cand[(size_t)best];
-    return FA_OK;
+// The rs pieces of a bucket padded to npad (a multiple of G * 64): `chunks` contiguous pieces, each a
+// multiple of G * 64 elements, so each splits into G equal blocks; GPU g owns block g of every piece
+// (block-cyclic, the same rule as shard.cyclic_pieces / cyclic_bounds).
+std::vector<std::pair<size_t, size_t>> rs_pieces(size_t npad, int G, int chunks) {
+    const size_t unit = (size_t)G * kShardUnit, m = npad / unit;
+    chunks = std::max(1, chunks);
+    std::vector<size_t> edges;
+    for (int c = 0; c < chunks; ++c) edges.push_back(m * (size_t)c / (size_t)chunks * unit);
+    edges.push_back(npad);
+    std::sort(edges.begin(), edges.end());
+    edges.erase(std::unique(edges.begin(), edges.end()), edges.end());
+    std::vector<std::pair<size_t, size_t>> out;
+    for (size_t i = 0; i + 1 < edges.size(); ++i) out.emplace_back(edges[i], edges[i + 1]);
+    return out;
+}
+
+// HBM placement of a bucket's slots.  Client buckets that start at the same address modulo a large
+// power of two put the U simultaneous loads of a wave (and its store) on the same HBM channels; a small
+// per-slot skew spreads them.  Measured on MI355X (profiles/r01_summary.json, tools/exp_layout.py):
+// 256-512 B skew -> 1.30-1.32 ms for 32 x 256 MiB vs 1.47-1.51 ms unskewed; re-laid out inside the
+// same six pools (tools/exp_skew.hip), 2048 B beat 512 B in every one (by 0.6-2.9%); 8 KiB + 512 and
+// 2 MiB + 512 are 7-12% slower.  Slots stay 16-byte aligned.
+size_t slot_stride(size_t bytes, size_t skew) { return (bytes + 4095) / 4096 * 4096 + skew; }
+
+inline bool holds(const Part& p, int g, int k) { return k >= p.c0[(size_t)g] && k < p.c1[(size_t)g]; }
+inline char* slot_ptr(const Part& p, int g, int k) {
+    return p.pool[(size_t)g] + (size_t)(k - p.c0[(size_t)g]) * p.stride[(size_t)g];
 }
 
 int check_part(fa_ctx* ctx, int part_id, Part** out) {
@@ -409,42 +436,166 @@ void free_part(fa_ctx* ctx, Part& p) {
     for (size_t g = 0; g < p.pool.size(); ++g) {
         DeviceGuard dg(ctx->gpu[g].dev);
         if (p.pool[g]) (void)hipFree(p.pool[g]);
+        if (g < p.done.size() && p.done[g]) (void)hipEventDestroy(p.done[g]);
     }
     p.pool.clear();
-    p.slots.clear();
     p.dout.clear();
+    p.done.clear();
 }
 
-// HBM placement of a bucket's slots.  Client buckets that start at the same
-// address modulo a large power of two put the U simultaneous loads of a wave
-// (and its store) on the same HBM channels; a small per-slot skew spreads them.
-// Measured on MI355X (profiles/r01_summary.json, tools/exp_layout.py): 256-512 B
-// skew -> 1.30-1.32 ms for 32 x 256 MiB vs 1.47-1.51 ms unskewed.  Re-laid out
-// inside the same six pools (tools/exp_skew.hip), 2048 B beat 512 B in every one
-// (by 0.6-2.9%); 8 KiB + 512 and 2 MiB + 512 are 7-12% slower.  Slots stay
-// 16-byte aligned.
-size_t slot_stride(size_t bytes) { return (bytes + 4095) / 4096 * 4096 + g_slot_skew; }
+// Makes stream s of GPU g wait for the H2D copies queued so far on its copy stream (the submits) -- only
+// if copies were queued since s last waited: a cross-stream wait costs the launch ~7-10 us on the device
+// (fa_reduce_part rounds, gpurun_out r02s05), which a device-resident round (slots written in place, no
+// submits) must not pay.
+int wait_copies(fa_ctx* ctx, int g, hipStream_t s) {
+    GpuRes& r = ctx->gpu[g];
+    auto it = r.waited.find(s);
+    if (it != r.waited.end() ? it->second == r.copy_gen : r.copy_gen == 0) return FA_OK;
+    if (r.copy_ev_gen != r.copy_gen) {
+        FA_HIP(hipEventRecord(r.copy_ev, r.copy));
+        r.copy_ev_gen = r.copy_gen;
+    }
+    FA_HIP(hipStreamWaitEvent(s, r.copy_ev, 0));
+    r.waited[s] = r.copy_gen;
+    return FA_OK;
+}
 
-inline char* slot_ptr(const Part& p, int g, int k) { return p.slots[g] + (size_t)k * p.stride[g]; }
+// Copy-out runs of a range part: GPU g's output holds its shard.
+void set_range_runs(Part& p, int G) {
+    for (int g = 0; g < G; ++g) {
+        p.runs[(size_t)g] = {Run{0, p.off[(size_t)g], p.cnt[(size_t)g]}};
+        p.run_src[(size_t)g] = p.dout[(size_t)g];
+    }
+}
 
-// Enqueue the reduction of part p on every GPU's compute stream (or `s` for a single GPU).
+// The rs exchange state of a part: GPU g's shard holds block g of every piece, clipped to n.
+void set_rs_runs(Part& p, int G, int chunks) {
+    const auto pieces = rs_pieces(p.npad, G, chunks);
+    for (int g = 0; g < G; ++g) {
+        auto& rr = p.runs[(size_t)g];
+        rr.clear();
+        size_t off = 0;
+        for (auto& pc : pieces) {
+            const size_t q = (pc.second - pc.first) / (size_t)G;
+            const size_t lo = pc.first + (size_t)g * q, hi = std::min(p.n, lo + q);
+            if (hi > lo) rr.push_back(Run{off, lo, hi - lo});
+            off += q;
+        }
+        p.run_src[(size_t)g] = p.dout[(size_t)g];
+    }
+}
+
+// Notes the stream the part's reduction on GPU g ran on; the copy-out orders itself after it
+// (copy_output records p.done there at copy time, which covers everything enqueued so far, and waits
+// only when that stream is not its own).  Nothing is recorded in the reduction's path.
+int mark_done(fa_ctx*, Part& p, int g, hipStream_t s) {
+    p.done_stream[(size_t)g] = s;
+    return FA_OK;
+}
+
+// Range layout: enqueue the ordered chain over clients [k0, k1) of part p on GPU g, continuing the
+// fp32 accumulator when k0 > 0 (accumulate on arrival) and writing the output dtype when k1 == D.
+int chain_range(fa_ctx* ctx, Part& p, int g, int k0, int k1, const float* w, hipStream_t st) {
+    std::vector<const void*> ptrs;
+    for (int k = k0; k < k1; ++k) ptrs.push_back(slot_ptr(p, g, k));
+    const bool last = k1 == p.D;
+    const float* init = k0 > 0 ? p.acc[(size_t)g] : nullptr;
+    void* dst = last ? p.dout[(size_t)g] : (void*)p.acc[(size_t)g];
+    return reduce_on(ctx, g, ctx->tuning.tu, ptrs.data(), w + k0, k1 - k0, p.cnt[(size_t)g], p.in, dst,
+                     last ? p.out : FA_F32, FA_FEDAVG, p.divisor, init, st);
+}
+
+// Enqueue the full reduction of part p on every GPU (the ctx's streams, or `s` for a one-GPU ctx):
+// range -> each GPU's shard; rs -> the clients' fp32 partials, piece by piece, each piece's RCCL
+// reduce-scatter (ring over xGMI) overlapping the reduction of the next.
 int reduce_part(fa_ctx* ctx, Part& p, const float* w, hipStream_t s) {
-    std::vector<const void*> ptrs(p.D);
-    for (int g = 0; g < ctx->G; ++g) {
-        GpuRes& r = ctx->gpu[g];
+    const int G = ctx->G;
+    if (!p.rs) {
+        for (int g = 0; g < G; ++g) {
+            GpuRes& r = ctx->gpu[(size_t)g];
+            DeviceGuard dg(r.dev);
+            hipStream_t st = s ? s : r.compute;
+            int rc = wait_copies(ctx, g, st);
+            if (rc) return rc;
+            if (p.mode == FA_LITERAL) {
+                const void* last = slot_ptr(p, g, p.last_slot >= 0 ? p.last_slot : p.D - 1);
+                rc = reduce_on(ctx, g, ctx->tuning.tu, &last, w, 1, p.cnt[(size_t)g], p.in, p.dout[(size_t)g], p.out,
+                               FA_LITERAL, p.divisor, nullptr, st);
+            } else {
+                std::vector<const void*> ptrs;
+                for (int k = 0; k < p.D; ++k) ptrs.push_back(slot_ptr(p, g, k));
+                rc = reduce_on(ctx, g, ctx->tuning.tu, ptrs.data(), w, p.D, p.cnt[(size_t)g], p.in, p.dout[(size_t)g],
+                               p.out, FA_FEDAVG, p.divisor, nullptr, st);
+            }
+            if (rc || (rc = mark_done(ctx, p, g, st))) return rc;
+        }
+        set_range_runs(p, G);
+        return FA_OK;
+    }
+    if (p.mode == FA_LITERAL) {  // the last client's GPU computes the whole bucket; nothing to exchange
+        const int k = p.last_slot >= 0 ? p.last_slot : p.D - 1;
+        int o = 0;
+        while (!holds(p, o, k)) ++o;
+        GpuRes& r = ctx->gpu[(size_t)o];
         DeviceGuard dg(r.dev);
         hipStream_t st = s ? s : r.compute;
-        for (int k = 0; k < p.D; ++k) ptrs[k] = slot_ptr(p, g, k);
-        int rc;
-        if (p.mode == FA_LITERAL) {
-            const void* last = ptrs[p.last_slot >= 0 ? p.last_slot : p.D - 1];
-            rc = reduce_on(ctx, g, &last, w, 1, p.cnt[g], p.in, p.dout[g], p.out, p.mode, p.divisor, nullptr, st);
-        } else {
-            rc = reduce_on(ctx, g, ptrs.data(), w, p.D, p.cnt[g], p.in, p.dout[g], p.out, p.mode, p.divisor, nullptr,
-                           st);
+        int rc = wait_copies(ctx, o, st);
+        const void* last = slot_ptr(p, o, k);
+        if (rc || (rc = reduce_on(ctx, o, ctx->tuning.tu, &last, w, 1, p.n, p.in, p.partial[(size_t)o], FA_F32,
+                                  FA_LITERAL, p.divisor, nullptr, st)))
+            return rc;
+        if ((rc = mark_done(ctx, p, o, st))) return rc;
+        for (int g = 0; g < G; ++g) p.runs[(size_t)g].clear();
+        p.runs[(size_t)o] = {Run{0, 0, p.n}};
+        p.run_src[(size_t)o] = p.partial[(size_t)o];
+        return FA_OK;
+    }
+    const auto pieces = rs_pieces(p.npad, G, ctx->tuning.rs_chunks);
+    for (int g = 0; g < G; ++g) {
+        GpuRes& r = ctx->gpu[(size_t)g];
+        DeviceGuard dg(r.dev);
+        hipStream_t st = s ? s : r.compute;
+        int rc = wait_copies(ctx, g, st);
+        if (rc) return rc;
+        if (p.c1[(size_t)g] == p.c0[(size_t)g])  // a GPU without clients contributes zeros
+            FA_HIP(hipMemsetAsync(p.partial[(size_t)g], 0, p.npad * 4, st));
+    }
+    size_t off = 0;
+    for (auto& pc : pieces) {
+        const size_t a = pc.first, len = pc.second - pc.first, q = len / (size_t)G;
+        for (int g = 0; g < G; ++g) {
+            GpuRes& r = ctx->gpu[(size_t)g];
+            DeviceGuard dg(r.dev);
+            hipStream_t st = s ? s : r.compute;
+            const int k0 = p.c0[(size_t)g], k1 = p.c1[(size_t)g];
+            if (k1 > k0) {
+                std::vector<const void*> ptrs;
+                for (int k = k0; k < k1; ++k) ptrs.push_back(slot_ptr(p, g, k) + a * dsize(p.in));
+                int rc = reduce_on(ctx, g, ctx->tuning.tu, ptrs.data(), w + k0, k1 - k0, len, p.in,
+                                   p.partial[(size_t)g] + a, FA_F32, FA_FEDAVG, p.divisor, nullptr, st);
+                if (rc) return rc;
+            }
+            FA_HIP(hipEventRecord(r.step_ev, st));
+            FA_HIP(hipStreamWaitEvent(r.comm, r.step_ev, 0));
         }
+        FA_NCCL(ncclGroupStart());
+        for (int g = 0; g < G; ++g) {
+            GpuRes& r = ctx->gpu[(size_t)g];
+            ncclResult_t e = ncclReduceScatter(p.partial[(size_t)g] + a, static_cast<float*>(p.dout[(size_t)g]) + off,
+                                               q, ncclFloat32, ncclSum, r.nccl, r.comm);
+            if (e != ncclSuccess) {
+                (void)ncclGroupEnd();
+                return fail(FA_ERR_NCCL, "ncclReduceScatter: %s", ncclGetErrorString(e));
+            }
+        }
+        FA_NCCL(ncclGroupEnd());
+        off += q;
+    }
+    for (int g = 0; g < G; ++g) {
+        int rc = mark_done(ctx, p, g, ctx->gpu[(size_t)g].comm);
         if (rc) return rc;
     }
+    set_rs_runs(p, G, ctx->tuning.rs_chunks);
     return FA_OK;
 }
 
@@ -491,6 +642,29 @@ struct Gather {
     }
 };
 
+// Accumulate on arrival: extend the chain over the in-order prefix of submitted slots.  Slots
+// [p.reduced, j) are all submitted: one launch continues the fp32 accumulator over them (or, when j == D,
+// finishes the chain into the output), after their H2D copies.  Same bits as one chain over all D.
+int advance_prefix(fa_ctx* ctx, Part& p) {
+    if (!(ctx->flags & FA_ACCUMULATE_ON_ARRIVAL) || p.rs || p.mode != FA_FEDAVG || p.ready) return FA_OK;
+    int j = p.reduced;
+    while (j < p.D && p.submitted[(size_t)j]) ++j;
+    if (j == p.reduced) return FA_OK;
+    for (int g = 0; g < ctx->G; ++g) {
+        GpuRes& r = ctx->gpu[(size_t)g];
+        DeviceGuard dg(r.dev);
+        int rc = wait_copies(ctx, g, r.compute);
+        if (rc || (rc = chain_range(ctx, p, g, p.reduced, j, p.w.data(), r.compute))) return rc;
+        if (j == p.D && (rc = mark_done(ctx, p, g, r.compute))) return rc;
+    }
+    p.reduced = j;
+    if (j == p.D) {
+        p.ready = true;
+        set_range_runs(p, ctx->G);
+    }
+    return FA_OK;
+}
+
 int submit_impl(fa_ctx* ctx, int part_id, int slot, const Gather& src, float weight, bool pinned) {
     Part* p;
     int rc = check_part(ctx, part_id, &p);
@@ -500,98 +674,132 @@ int submit_impl(fa_ctx* ctx, int part_id, int slot, const Gather& src, float wei
     const size_t si = dsize(p->in), total = src.total();
     if (total != p->n * si)
         return fail(FA_ERR_ARG, "part %d expects %zu bytes per receipt, got %zu", part_id, p->n * si, total);
-    for (int g = 0; g < ctx->G; ++g) {
-        GpuRes& r = ctx->gpu[g];
+    rc = for_each_gpu(ctx->G, [&](int g) -> int {
+        if (!holds(*p, g, slot)) return FA_OK;  // rs: only the slot's GPU receives it
+        GpuRes& r = ctx->gpu[(size_t)g];
         DeviceGuard dg(r.dev);
-        const size_t base = p->off[g] * si;
+        const size_t base = p->off[(size_t)g] * si;
         char* ds = slot_ptr(*p, g, slot);
-        const size_t bytes = p->cnt[g] * si;
+        const size_t bytes = p->cnt[(size_t)g] * si;
         if (pinned) {  // pinned segments: DMA straight from them, one copy per piece of this GPU's range
             hipError_t e = hipSuccess;
             src.pieces(base, bytes, [&](char* piece, size_t rel, size_t take) {
                 if (e == hipSuccess) e = hipMemcpyAsync(ds + rel, piece, take, hipMemcpyHostToDevice, r.copy);
             });
+            ++r.copy_gen;
             FA_HIP(e);
-            continue;
+            return FA_OK;
         }
+        ++r.copy_gen;
         // Double-buffered staging: fill one pinned chunk while the other is in flight.
         for (size_t o = 0; o < bytes; o += kStageBytes) {
             const size_t b = std::min(kStageBytes, bytes - o);
             const int i = r.stage_i;
             r.stage_i ^= 1;
             FA_HIP(hipEventSynchronize(r.stage_ev[i]));
-            ctx->pool->copy(r.stage[i], b, [&](size_t lo, size_t len, char* d) { src.copy_out(base + o + lo, len, d); });
+            r.pool->copy(r.stage[i], b, [&](size_t lo, size_t len, char* d) { src.copy_out(base + o + lo, len, d); });
             FA_HIP(hipMemcpyAsync(ds + o, r.stage[i], b, hipMemcpyHostToDevice, r.copy));
             FA_HIP(hipEventRecord(r.stage_ev[i], r.copy));
         }
-    }
-    if (!p->submitted[slot]) {
-        p->submitted[slot] = 1;
+        return FA_OK;
+    });
+    if (rc) return rc;
+    p->ready = false;  // a new receipt invalidates a finished reduction (fa_reduce_parts, a full prefix)
+    if (!p->submitted[(size_t)slot]) {
+        p->submitted[(size_t)slot] = 1;
         ++p->n_submitted;
+    } else if (slot < p->reduced) {  // a receipt already chained was replaced: restart the chain
+        p->reduced = 0;
+        p->ready = false;
     }
-    p->w[slot] = weight;
+    p->w[(size_t)slot] = weight;
     p->last_slot = slot;
-    return FA_OK;
+    return advance_prefix(ctx, *p);
 }
 
-// D2H of the part's device output (the result leaves for new_message()) into `dst`: straight into
-// pinned segments, else through the pinned chunks, double-buffered.  Waits for all work on the
-// device first (the reduction may have run on a caller's stream).
+// D2H of the part's output (the result leaves for new_message()) into `dst`, following the runs of its
+// last reduction: straight into pinned segments, else through the pinned chunks, double-buffered.  Every
+// GPU's copies wait on that GPU's done event (no device-wide synchronization); pinned copies of all GPUs
+// are issued before any is waited for, staged ones run on one host thread per GPU.
 int copy_output(fa_ctx* ctx, Part& p, const Gather& dst, bool pinned) {
-    const size_t so = dsize(p.out);
-    if (dst.total() != p.n * so)
-        return fail(FA_ERR_ARG, "output of %zu bytes expected, destination holds %zu", p.n * so, dst.total());
-    for (int g = 0; g < ctx->G; ++g) {
-        GpuRes& r = ctx->gpu[g];
+    const size_t so = p.rs ? 4 : dsize(p.out);
+    if (dst.total() != p.n * dsize(p.out))
+        return fail(FA_ERR_ARG, "output of %zu bytes expected, destination holds %zu", p.n * dsize(p.out),
+                    dst.total());
+    const int G = ctx->G;
+    for (int g = 0; g < G; ++g) {
+        GpuRes& r = ctx->gpu[(size_t)g];
+        hipStream_t ds = p.done_stream[(size_t)g];
+        if (p.runs[(size_t)g].empty() || !ds || ds == r.compute) continue;
         DeviceGuard dg(r.dev);
-        FA_HIP(hipDeviceSynchronize());
-        const char* src = static_cast<const char*>(p.dout[g]);
-        const size_t base = p.off[g] * so;
-        const size_t bytes = p.cnt[g] * so;
-        if (pinned) {
+        FA_HIP(hipEventRecord(p.done[(size_t)g], ds));
+        FA_HIP(hipStreamWaitEvent(r.compute, p.done[(size_t)g], 0));
+    }
+    if (pinned) {
+        for (int g = 0; g < G; ++g) {
+            GpuRes& r = ctx->gpu[(size_t)g];
+            DeviceGuard dg(r.dev);
+            const char* src = static_cast<const char*>(p.run_src[(size_t)g]);
             hipError_t e = hipSuccess;
-            dst.pieces(base, bytes, [&](char* piece, size_t rel, size_t take) {
-                if (e == hipSuccess) e = hipMemcpyAsync(piece, src + rel, take, hipMemcpyDeviceToHost, r.compute);
-            });
+            for (const Run& run : p.runs[(size_t)g])
+                dst.pieces(run.dst * so, run.cnt * so, [&](char* piece, size_t rel, size_t take) {
+                    if (e == hipSuccess)
+                        e = hipMemcpyAsync(piece, src + run.src * so + rel, take, hipMemcpyDeviceToHost, r.compute);
+                });
             FA_HIP(e);
-            FA_HIP(hipStreamSynchronize(r.compute));
-            continue;
         }
-        const size_t chunks = (bytes + kStageBytes - 1) / kStageBytes;
-        // double-buffered: the D2H of chunk c+1 overlaps the host copy-out of chunk c
-        auto issue = [&](size_t c) -> int {
-            const size_t o = c * kStageBytes, b = std::min(kStageBytes, bytes - o);
-            FA_HIP(hipMemcpyAsync(r.stage[c & 1], src + o, b, hipMemcpyDeviceToHost, r.compute));
-            FA_HIP(hipEventRecord(r.stage_ev[c & 1], r.compute));
-            return FA_OK;
-        };
-        if (chunks > 0) {
-            int rc = issue(0);
-            if (rc) return rc;
+        for (int g = 0; g < G; ++g) {
+            DeviceGuard dg(ctx->gpu[(size_t)g].dev);
+            FA_HIP(hipStreamSynchronize(ctx->gpu[(size_t)g].compute));
         }
-        for (size_t c = 0; c < chunks; ++c) {
-            FA_HIP(hipEventSynchronize(r.stage_ev[c & 1]));
-            if (c + 1 < chunks) {
-                int rc = issue(c + 1);
+        return FA_OK;
+    }
+    return for_each_gpu(G, [&](int g) -> int {
+        GpuRes& r = ctx->gpu[(size_t)g];
+        DeviceGuard dg(r.dev);
+        const char* src = static_cast<const char*>(p.run_src[(size_t)g]);
+        for (const Run& run : p.runs[(size_t)g]) {
+            const size_t bytes = run.cnt * so, base = run.dst * so;
+            const char* rsrc = src + run.src * so;
+            const size_t chunks = (bytes + kStageBytes - 1) / kStageBytes;
+            // double-buffered: the D2H of chunk c+1 overlaps the host copy-out of chunk c
+            auto issue = [&](size_t c) -> int {
+                const size_t o = c * kStageBytes, b = std::min(kStageBytes, bytes - o);
+                FA_HIP(hipMemcpyAsync(r.stage[c & 1], rsrc + o, b, hipMemcpyDeviceToHost, r.compute));
+                FA_HIP(hipEventRecord(r.stage_ev[c & 1], r.compute));
+                return FA_OK;
+            };
+            if (chunks > 0) {
+                int rc = issue(0);
                 if (rc) return rc;
             }
-            const size_t o = c * kStageBytes, b = std::min(kStageBytes, bytes - o);
-            char* st = r.stage[c & 1];
-            // the pool partitions [0, b); each worker scatters its share of the chunk
-            ctx->pool->copy(st, b, [&](size_t lo, size_t len, char*) { dst.copy_in(base + o + lo, len, st + lo); });
+            for (size_t c = 0; c < chunks; ++c) {
+                FA_HIP(hipEventSynchronize(r.stage_ev[c & 1]));
+                if (c + 1 < chunks) {
+                    int rc = issue(c + 1);
+                    if (rc) return rc;
+                }
+                const size_t o = c * kStageBytes, b = std::min(kStageBytes, bytes - o);
+                char* st = r.stage[c & 1];
+                // the pool partitions [0, b); each worker scatters its share of the chunk
+                r.pool->copy(st, b, [&](size_t lo, size_t len, char*) { dst.copy_in(base + o + lo, len, st + lo); });
+            }
         }
         FA_HIP(hipStreamSynchronize(r.compute));
-    }
-    return FA_OK;
+        return FA_OK;
+    });
 }
 
-int copy_output_flat(fa_ctx* ctx, Part& p, void* host_dst) {
-    const size_t bytes = p.n * dsize(p.out);
-    const void* segs[1] = {host_dst};
-    return copy_output(ctx, p, Gather{1, segs, &bytes}, false);
+void reset_round(Part& p) {
+    std::fill(p.submitted.begin(), p.submitted.end(), 0);
+    p.n_submitted = 0;
+    p.last_slot = -1;
+    p.reduced = 0;
+    p.ready = false;
 }
 
-// The end of a phase: wait for the submits, reduce on every GPU, copy the result out, reset the round.
+// The end of a phase: wait for the submits, reduce on every GPU (unless the round's reduction is done
+// already: accumulate on arrival reached D, or fa_reduce_parts), copy the result out, reset the round.
 int finalize_impl(fa_ctx* ctx, int part_id, const Gather& dst, bool pinned) {
     Part* p;
     int rc = check_part(ctx, part_id, &p);
@@ -600,23 +808,157 @@ int finalize_impl(fa_ctx* ctx, int part_id, const Gather& dst, bool pinned) {
         return fail(FA_ERR_STATE, "part %d: %d of %d clients submitted", part_id, p->n_submitted, p->D);
     if (p->n_submitted == 0) return fail(FA_ERR_STATE, "part %d: nothing submitted", part_id);
     if ((rc = dst.check("host destination"))) return rc;
-    for (int g = 0; g < ctx->G; ++g) {  // the reduction waits for this round's H2D copies
-        GpuRes& r = ctx->gpu[g];
-        DeviceGuard dg(r.dev);
-        hipEvent_t ev;
-        FA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        FA_HIP(hipEventRecord(ev, r.copy));
-        FA_HIP(hipStreamWaitEvent(r.compute, ev, 0));
-        FA_HIP(hipEventDestroy(ev));
+    if (!p->ready) {
+        if (p->reduced > 0) {  // accumulate on arrival: finish the chain after the reduced prefix
+            for (int g = 0; g < ctx->G; ++g) {
+                GpuRes& r = ctx->gpu[(size_t)g];
+                DeviceGuard dg(r.dev);
+                if ((rc = wait_copies(ctx, g, r.compute))) return rc;
+                if ((rc = chain_range(ctx, *p, g, p->reduced, p->D, p->w.data(), r.compute))) return rc;
+                if ((rc = mark_done(ctx, *p, g, r.compute))) return rc;
+            }
+            set_range_runs(*p, ctx->G);
+        } else if ((rc = reduce_part(ctx, *p, p->w.data(), nullptr))) {
+            return rc;
+        }
     }
-    rc = reduce_part(ctx, *p, p->w.data(), nullptr);
-    if (rc) return rc;
     rc = copy_output(ctx, *p, dst, pinned);
     if (rc) return rc;
-    std::fill(p->submitted.begin(), p->submitted.end(), 0);
-    p->n_submitted = 0;
-    p->last_slot = -1;
+    reset_round(*p);
     return FA_OK;
+}
+
+// One launch per GPU for every batchable part (FedAvg, range layout, <= kMaxClients clients, same dtypes,
+// not taken by the phased kernel); the others launch one by one.  Marks the parts ready for finalize.
+int reduce_parts_impl(fa_ctx* ctx, int n_parts, const int* ids, const float* const* weights, hipStream_t s) {
+    std::vector<Part*> ps;
+    for (int i = 0; i < n_parts; ++i) {
+        Part* p;
+        int rc = check_part(ctx, ids[i], &p);
+        if (rc) return rc;
+        for (Part* q : ps)
+            if (q == p) return fail(FA_ERR_ARG, "part %d listed twice", ids[i]);
+        ps.push_back(p);
+    }
+    const fa::Tuning& tu = ctx->tuning.tu;
+    // group the batchable parts by dtype pair
+    std::map<std::pair<int, int>, std::vector<int>> groups;
+    std::vector<int> single;
+    for (int i = 0; i < n_parts; ++i) {
+        Part& p = *ps[(size_t)i];
+        bool batch = !p.rs && p.mode == FA_FEDAVG && p.D <= fa::kMaxClients;
+        for (int g = 0; batch && g < ctx->G; ++g) {
+            DeviceGuard dg(ctx->gpu[(size_t)g].dev);
+            batch = !fa::phased_takes(p.in, (int64_t)(p.cnt[(size_t)g] * dsize(p.in) / 16), p.D, tu);
+        }
+        if (batch) groups[{(int)p.in, (int)p.out}].push_back(i);
+        else single.push_back(i);
+    }
+    for (int i : single) {
+        Part& p = *ps[(size_t)i];
+        const float* w = weights && weights[i] ? weights[i] : p.w.data();
+        int rc = reduce_part(ctx, p, w, s);
+        if (rc) return rc;
+        p.ready = true;
+    }
+    for (auto& kv : groups) {
+        const fa_dtype in = (fa_dtype)kv.first.first, out = (fa_dtype)kv.first.second;
+        const auto& members = kv.second;
+        for (size_t m0 = 0; m0 < members.size(); m0 += kMaxSegments) {
+            const size_t m1 = std::min(members.size(), m0 + kMaxSegments);
+            for (int g = 0; g < ctx->G; ++g) {
+                GpuRes& r = ctx->gpu[(size_t)g];
+                DeviceGuard dg(r.dev);
+                hipStream_t st = s ? s : r.compute;
+                FA_HIP(hipEventSynchronize(r.seg_ev));  // the previous upload has read the host table
+                int64_t blocks = 0;
+                int nseg = 0, max_nc = 0;
+                const size_t V = 16 / dsize(in);
+                for (size_t m = m0; m < m1; ++m) {
+                    Part& p = *ps[(size_t)members[m]];
+                    const float* w = weights && weights[members[m]] ? weights[members[m]] : p.w.data();
+                    const size_t n = p.cnt[(size_t)g];
+                    if (n == 0) continue;
+                    fa::SegDesc& sd = r.seg_host[nseg++];
+                    sd.nvec = (int64_t)(n / V);
+                    sd.n = (int64_t)n;
+                    sd.nblk = std::max<int64_t>(1, (sd.nvec + tu.block - 1) / tu.block);
+                    sd.blk0 = blocks;
+                    blocks += sd.nblk;
+                    sd.out = p.dout[(size_t)g];
+                    sd.nc = p.D;
+                    for (int k = 0; k < p.D; ++k) {
+                        sd.src[k] = slot_ptr(p, g, k);
+                        sd.w[k] = w[k];
+                    }
+                    max_nc = std::max(max_nc, p.D);
+                }
+                int rc = wait_copies(ctx, g, st);
+                if (rc) return rc;
+                if (nseg > 0) {
+                    FA_HIP(hipMemcpyAsync(r.seg_dev, r.seg_host, sizeof(fa::SegDesc) * (size_t)nseg,
+                                          hipMemcpyHostToDevice, st));
+                    FA_HIP(hipEventRecord(r.seg_ev, st));
+                    FA_HIP(fa::launch_segments(r.seg_dev, nseg, blocks, in, out, max_nc, tu, st));
+                }
+                for (size_t m = m0; m < m1; ++m)
+                    if ((rc = mark_done(ctx, *ps[(size_t)members[m]], g, st))) return rc;
+            }
+            for (size_t m = m0; m < m1; ++m) {
+                Part& p = *ps[(size_t)members[m]];
+                set_range_runs(p, ctx->G);
+                p.ready = true;
+            }
+        }
+    }
+    return FA_OK;
+}
+
+int tuning_from(const fa_tuning* t, CtxTuning* io) {
+    if (!t) return fail(FA_ERR_ARG, "tuning is null");
+    CtxTuning nt = *io;
+    if (t->block) {
+        if (t->block != 64 && t->block != 128 && t->block != 256) return fail(FA_ERR_ARG, "block must be 64/128/256");
+        nt.tu.block = t->block;
+    }
+    if (t->max_blocks) nt.tu.max_blocks = t->max_blocks < 0 ? 0 : t->max_blocks;
+    if (t->unroll) {
+        if (t->unroll != 4 && t->unroll != 8 && t->unroll != 16) return fail(FA_ERR_ARG, "unroll must be 4/8/16");
+        nt.tu.unroll = t->unroll;
+    }
+    if (t->load_policy) {
+        if (t->load_policy < 1 || t->load_policy > 2) return fail(FA_ERR_ARG, "load_policy must be 1 or 2");
+        nt.tu.load_nt = t->load_policy == 2;
+    }
+    if (t->store_policy) {
+        if (t->store_policy < 1 || t->store_policy > 4) return fail(FA_ERR_ARG, "store_policy must be 1..4");
+        nt.tu.store_policy = t->store_policy - 1;
+    }
+    if (t->slot_skew) {
+        if (t->slot_skew > 0 && t->slot_skew % 16) return fail(FA_ERR_ARG, "slot_skew must be a multiple of 16");
+        nt.slot_skew = t->slot_skew < 0 ? 0 : (size_t)t->slot_skew;
+    }
+    if (t->walk) {
+        if (t->walk < 1 || t->walk > 6) return fail(FA_ERR_ARG, "walk must be 1..6");
+        nt.tu.walk = t->walk - 1;
+    }
+    if (t->rs_chunks) {
+        if (t->rs_chunks < 1 || t->rs_chunks > 1024) return fail(FA_ERR_ARG, "rs_chunks must be 1..1024");
+        nt.rs_chunks = t->rs_chunks;
+    }
+    *io = nt;
+    return FA_OK;
+}
+
+void tuning_to(const CtxTuning& c, fa_tuning* t) {
+    t->block = c.tu.block;
+    t->max_blocks = c.tu.max_blocks;
+    t->unroll = c.tu.unroll;
+    t->load_policy = c.tu.load_nt ? 2 : 1;
+    t->store_policy = c.tu.store_policy + 1;
+    t->slot_skew = (int)c.slot_skew;
+    t->walk = c.tu.walk + 1;
+    t->rs_chunks = c.rs_chunks;
 }
 
 }  // namespace
@@ -638,57 +980,44 @@ int fa_device_count(int* out) {
 
 int fa_set_tuning(const fa_tuning* t) {
     g_err.clear();
-    if (!t) return fail(FA_ERR_ARG, "tuning is null");
-    fa::Tuning nt = g_tuning;
-    size_t skew = g_slot_skew;
-    if (t->block) {
-        if (t->block != 64 && t->block != 128 && t->block != 256) return fail(FA_ERR_ARG, "block must be 64/128/256");
-        nt.block = t->block;
-    }
-    if (t->max_blocks) nt.max_blocks = t->max_blocks < 0 ? 0 : t->max_blocks;
-    if (t->unroll) {
-        if (t->unroll != 4 && t->unroll != 8 && t->unroll != 16) return fail(FA_ERR_ARG, "unroll must be 4/8/16");
-        nt.unroll = t->unroll;
-    }
-    if (t->load_policy) {
-        if (t->load_policy < 1 || t->load_policy > 2) return fail(FA_ERR_ARG, "load_policy must be 1 or 2");
-        nt.load_nt = t->load_policy == 2;
-    }
-    if (t->store_policy) {
-        if (t->store_policy < 1 || t->store_policy > 4) return fail(FA_ERR_ARG, "store_policy must be 1..4");
-        nt.store_policy = t->store_policy - 1;
-    }
-    if (t->slot_skew) {
-        if (t->slot_skew > 0 && t->slot_skew % 16) return fail(FA_ERR_ARG, "slot_skew must be a multiple of 16");
-        skew = t->slot_skew < 0 ? 0 : (size_t)t->slot_skew;
-    }
-    if (t->walk) {
-        if (t->walk < 1 || t->walk > 6) return fail(FA_ERR_ARG, "walk must be 1..6");
-        nt.walk = t->walk - 1;
-    }
-    int probes = g_placement_probes;
-    if (t->placement_probes) {
-        if (t->placement_probes > 16) return fail(FA_ERR_ARG, "placement_probes must be <= 16");
-        probes = t->placement_probes < 0 ? 1 : t->placement_probes;
-    }
-    g_tuning = nt;
-    g_slot_skew = skew;
-    g_placement_probes = probes;
-    return FA_OK;
+    std::lock_guard<std::mutex> g(g_defaults_mu);
+    return tuning_from(t, &g_defaults);
 }
 
 int fa_get_tuning(fa_tuning* t) {
     g_err.clear();
     if (!t) return fail(FA_ERR_ARG, "tuning is null");
-    t->block = g_tuning.block;
-    t->max_blocks = g_tuning.max_blocks;
-    t->unroll = g_tuning.unroll;
-    t->load_policy = g_tuning.load_nt ? 2 : 1;
-    t->store_policy = g_tuning.store_policy + 1;
-    t->slot_skew = (int)g_slot_skew;
-    t->placement_probes = g_placement_probes;
-    t->walk = g_tuning.walk + 1;
+    tuning_to(defaults(), t);
     return FA_OK;
+}
+
+int fa_ctx_set_tuning(fa_ctx* ctx, const fa_tuning* t) {
+    g_err.clear();
+    if (!ctx) return fail(FA_ERR_ARG, "ctx is null");
+    return tuning_from(t, &ctx->tuning);
+}
+
+int fa_ctx_get_tuning(fa_ctx* ctx, fa_tuning* t) {
+    g_err.clear();
+    if (!ctx || !t) return fail(FA_ERR_ARG, "ctx or tuning is null");
+    tuning_to(ctx->tuning, t);
+    return FA_OK;
+}
+
+int fa_rs_segments(size_t n, int n_gpus, int chunks, int gpu, size_t* lo_hi, int cap) {
+    g_err.clear();
+    if (n_gpus < 1 || gpu < 0 || gpu >= n_gpus || chunks < 1) return fail(FA_ERR_ARG, "bad n_gpus/gpu/chunks");
+    const size_t unit = (size_t)n_gpus * kShardUnit, npad = (n + unit - 1) / unit * unit;
+    int k = 0;
+    for (auto& pc : rs_pieces(npad, n_gpus, chunks)) {
+        const size_t q = (pc.second - pc.first) / (size_t)n_gpus, lo = pc.first + (size_t)gpu * q;
+        if (lo_hi && k < cap) {
+            lo_hi[2 * k] = lo;
+            lo_hi[2 * k + 1] = lo + q;
+        }
+        ++k;
+    }
+    return k;
 }
 
 int fa_create(fa_ctx** out, int n_gpus, int flags) {
@@ -701,15 +1030,19 @@ int fa_create_ex(fa_ctx** out, const int* device_ids, int n_gpus, int flags) {
     g_err.clear();
     if (!out) return fail(FA_ERR_ARG, "out is null");
     *out = nullptr;
+    if (flags & ~(FA_SHARD_RANGE | FA_SHARD_CLIENT_RS | FA_ACCUMULATE_ON_ARRIVAL | FA_TEST_SHARED_DEVICE))
+        return fail(FA_ERR_ARG, "unknown flags 0x%x", flags);
+    if ((flags & FA_SHARD_RANGE) && (flags & FA_SHARD_CLIENT_RS))
+        return fail(FA_ERR_ARG, "FA_SHARD_RANGE and FA_SHARD_CLIENT_RS exclude each other");
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return fail(FA_ERR_NODEV, "no HIP device visible");
-    if (n_gpus < 1 || n_gpus > count || (!device_ids && n_gpus > 0))
-        return fail(FA_ERR_ARG, "n_gpus=%d but %d device(s) visible", n_gpus, count);
-    if (n_gpus > 1 && !(flags & FA_SHARD_RANGE)) return fail(FA_ERR_ARG, "n_gpus > 1 needs FA_SHARD_RANGE");
+    if (n_gpus < 1 || !device_ids) return fail(FA_ERR_ARG, "n_gpus=%d with %d device(s) visible", n_gpus, count);
+    if (n_gpus > 1 && !(flags & (FA_SHARD_RANGE | FA_SHARD_CLIENT_RS)))
+        return fail(FA_ERR_ARG, "n_gpus > 1 needs FA_SHARD_RANGE or FA_SHARD_CLIENT_RS");
     for (int g = 0; g < n_gpus; ++g) {
         const int d = device_ids[g];
         if (d < 0 || d >= count) return fail(FA_ERR_ARG, "device id %d out of range [0,%d)", d, count);
-        for (int h = 0; h < g; ++h)
+        for (int h = 0; h < g && !(flags & FA_TEST_SHARED_DEVICE); ++h)
             if (device_ids[h] == d) return fail(FA_ERR_ARG, "device id %d listed twice", d);
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, d) != hipSuccess) return fail(FA_ERR_NODEV, "device %d unreadable", d);
@@ -719,13 +1052,22 @@ int fa_create_ex(fa_ctx** out, const int* device_ids, int n_gpus, int flags) {
     fa_ctx* ctx = new fa_ctx();
     ctx->G = n_gpus;
     ctx->flags = flags;
-    ctx->gpu.resize(n_gpus);
+    ctx->tuning = defaults();
+    ctx->gpu.resize((size_t)n_gpus);
+    const int threads = std::max(1, default_copy_threads() / n_gpus);
     for (int g = 0; g < n_gpus; ++g) {
-        GpuRes& r = ctx->gpu[g];
+        GpuRes& r = ctx->gpu[(size_t)g];
         r.dev = device_ids[g];
         DeviceGuard dg(r.dev);
         bool ok = hipStreamCreateWithFlags(&r.compute, hipStreamNonBlocking) == hipSuccess &&
-                  hipStreamCreateWithFlags(&r.copy, hipStreamNonBlocking) == hipSuccess;
+                  hipStreamCreateWithFlags(&r.copy, hipStreamNonBlocking) == hipSuccess &&
+                  hipStreamCreateWithFlags(&r.comm, hipStreamNonBlocking) == hipSuccess &&
+                  hipEventCreateWithFlags(&r.copy_ev, hipEventDisableTiming) == hipSuccess &&
+                  hipEventCreateWithFlags(&r.step_ev, hipEventDisableTiming) == hipSuccess &&
+                  hipEventCreateWithFlags(&r.seg_ev, hipEventDisableTiming) == hipSuccess &&
+                  hipHostMalloc((void**)&r.seg_host, sizeof(fa::SegDesc) * kMaxSegments, hipHostMallocDefault) ==
+                      hipSuccess &&
+                  hipMalloc((void**)&r.seg_dev, sizeof(fa::SegDesc) * kMaxSegments) == hipSuccess;
         for (int i = 0; ok && i < 2; ++i)
             ok = hipHostMalloc((void**)&r.stage[i], kStageBytes, hipHostMallocDefault) == hipSuccess &&
                  hipEventCreateWithFlags(&r.stage_ev[i], hipEventDisableTiming) == hipSuccess;
@@ -733,6 +1075,16 @@ int fa_create_ex(fa_ctx** out, const int* device_ids, int n_gpus, int flags) {
             fa_destroy(ctx);
             return fail(FA_ERR_NOMEM, "stream/staging setup failed on device %d", device_ids[g]);
         }
+        r.pool.reset(new CopyPool(threads));
+    }
+    if (flags & FA_SHARD_CLIENT_RS) {  // one RCCL communicator per GPU, all in this process
+        std::vector<ncclComm_t> comms((size_t)n_gpus, nullptr);
+        const ncclResult_t e = ncclCommInitAll(comms.data(), n_gpus, device_ids);
+        if (e != ncclSuccess) {
+            fa_destroy(ctx);
+            return fail(FA_ERR_NCCL, "ncclCommInitAll over %d GPU(s): %s", n_gpus, ncclGetErrorString(e));
+        }
+        for (int g = 0; g < n_gpus; ++g) ctx->gpu[(size_t)g].nccl = comms[(size_t)g];
     }
     *out = ctx;
     return FA_OK;
@@ -745,13 +1097,20 @@ void fa_destroy(fa_ctx* ctx) {
         DeviceGuard dg(r.dev);
         if (r.compute) (void)hipStreamSynchronize(r.compute);
         if (r.copy) (void)hipStreamSynchronize(r.copy);
+        if (r.comm) (void)hipStreamSynchronize(r.comm);
+        if (r.nccl) (void)ncclCommDestroy(r.nccl);
         for (int i = 0; i < 2; ++i) {
             if (r.stage[i]) (void)hipHostFree(r.stage[i]);
             if (r.stage_ev[i]) (void)hipEventDestroy(r.stage_ev[i]);
         }
+        if (r.seg_host) (void)hipHostFree(r.seg_host);
+        if (r.seg_dev) (void)hipFree(r.seg_dev);
+        for (hipEvent_t e : {r.copy_ev, r.step_ev, r.seg_ev})
+            if (e) (void)hipEventDestroy(e);
         if (r.scratch) (void)hipFree(r.scratch);
-        if (r.compute) (void)hipStreamDestroy(r.compute);
-        if (r.copy) (void)hipStreamDestroy(r.copy);
+        for (hipStream_t s : {r.compute, r.copy, r.comm})
+            if (s) (void)hipStreamDestroy(s);
+        r.pool.reset();
     }
     delete ctx;
 }
@@ -763,6 +1122,8 @@ int fa_bucket_define(fa_ctx* ctx, int part_id, size_t n_elems, fa_dtype in, fa_d
     if (!dvalid(in) || !dvalid(out)) return fail(FA_ERR_ARG, "bad dtype");
     if (mode != FA_FEDAVG && mode != FA_LITERAL) return fail(FA_ERR_ARG, "bad mode");
     if (n_clients < 1) return fail(FA_ERR_ARG, "n_clients must be >= 1");
+    const bool rs = (ctx->flags & FA_SHARD_CLIENT_RS) != 0;
+    if (rs && out != FA_F32) return fail(FA_ERR_ARG, "the rs layout reduce-scatters fp32 partials: out must be f32");
     auto it = ctx->parts.find(part_id);
     if (it != ctx->parts.end()) {
         free_part(ctx, it->second);
@@ -775,33 +1136,76 @@ int fa_bucket_define(fa_ctx* ctx, int part_id, size_t n_elems, fa_dtype in, fa_d
     p.D = n_clients;
     p.mode = mode;
     p.divisor = ctx->divisor;
-    p.w.assign(n_clients, 0.0f);
-    p.submitted.assign(n_clients, 0);
-    // Range shards: multiples of 64 elements so every shard keeps 16-B phase 0.
-    const size_t G = (size_t)ctx->G, unit = 64;
-    size_t per = ((n_elems + G - 1) / G + unit - 1) / unit * unit;
-    for (size_t g = 0; g < G; ++g) {
-        size_t lo = std::min(n_elems, g * per), hi = std::min(n_elems, lo + per);
-        p.off.push_back(lo);
-        p.cnt.push_back(hi - lo);
+    p.rs = rs;
+    p.w.assign((size_t)n_clients, 0.0f);
+    p.submitted.assign((size_t)n_clients, 0);
+    const size_t G = (size_t)ctx->G;
+    const bool eager = (ctx->flags & FA_ACCUMULATE_ON_ARRIVAL) && !rs && mode == FA_FEDAVG;
+    if (rs) {
+        const size_t unit = G * kShardUnit;
+        p.npad = (n_elems + unit - 1) / unit * unit;
+        for (size_t g = 0; g < G; ++g) {
+            int c0, c1;
+            client_bounds(n_clients, (int)G, (int)g, &c0, &c1);
+            p.c0.push_back(c0);
+            p.c1.push_back(c1);
+            p.off.push_back(0);
+            p.cnt.push_back(n_elems);
+        }
+    } else {
+        // Range shards: multiples of 64 elements so every shard keeps 16-B phase 0.
+        size_t per = ((n_elems + G - 1) / G + kShardUnit - 1) / kShardUnit * kShardUnit;
+        for (size_t g = 0; g < G; ++g) {
+            size_t lo = std::min(n_elems, g * per), hi = std::min(n_elems, lo + per);
+            p.off.push_back(lo);
+            p.cnt.push_back(hi - lo);
+            p.c0.push_back(0);
+            p.c1.push_back(n_clients);
+        }
     }
     p.pool.assign(G, nullptr);
-    p.slots.assign(G, nullptr);
     p.dout.assign(G, nullptr);
     p.stride.assign(G, 0);
-    p.probe_ms.assign(G, {});
-    p.chosen.assign(G, 0);
+    p.partial.assign(G, nullptr);
+    p.acc.assign(G, nullptr);
+    p.done.assign(G, nullptr);
+    p.runs.assign(G, {});
+    p.done_stream.assign(G, nullptr);
+    p.run_src.assign(G, nullptr);
     for (size_t g = 0; g < G; ++g) {
         DeviceGuard dg(ctx->gpu[g].dev);
-        p.stride[g] = slot_stride(p.cnt[g] * dsize(in));
-        const size_t bytes = (size_t)n_clients * p.stride[g] + std::max<size_t>(1, p.cnt[g] * dsize(out));
-        int rc = alloc_placed(ctx, (int)g, p, p.stride[g], bytes, &p.pool[g]);
-        if (rc) {
+        if (hipEventCreateWithFlags(&p.done[g], hipEventDisableTiming) != hipSuccess) {
             free_part(ctx, p);
-            return rc;
+            return fail(FA_ERR_HIP, "event creation failed");
         }
-        p.slots[g] = p.pool[g];
-        p.dout[g] = p.pool[g] + (size_t)n_clients * p.stride[g];
+        const size_t slot_elems = rs ? p.npad : p.cnt[g];
+        const size_t held = (size_t)(p.c1[g] - p.c0[g]);
+        p.stride[g] = slot_stride(slot_elems * dsize(in), ctx->tuning.slot_skew);
+        // one allocation: slots, then the output (range: cnt of `out`; rs: the fp32 shard), then the rs
+        // partial or the eager accumulator, each 4 KiB aligned
+        const size_t out_bytes = rs ? p.npad / G * 4 : p.cnt[g] * dsize(out);
+        const size_t out_off = held * p.stride[g];
+        const size_t extra_off = out_off + (out_bytes + 4095) / 4096 * 4096;
+        const size_t extra_bytes = rs ? p.npad * 4 : eager ? p.cnt[g] * 4 : 0;
+        const size_t bytes = std::max<size_t>(1, extra_off + extra_bytes);
+        if (hipMalloc((void**)&p.pool[g], bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            free_part(ctx, p);
+            return fail(FA_ERR_NOMEM, "device alloc of %zu B failed on GPU %zu", bytes, g);
+        }
+        p.dout[g] = p.pool[g] + out_off;
+        if (rs) {
+            p.partial[g] = reinterpret_cast<float*>(p.pool[g] + extra_off);
+            // the padding of every slot stays zero: the pieces past n reduce to 0
+            for (size_t k = 0; k < held && p.npad > n_elems; ++k)
+                if (hipMemset(p.pool[g] + k * p.stride[g] + n_elems * dsize(in), 0, (p.npad - n_elems) * dsize(in)) !=
+                    hipSuccess) {
+                    free_part(ctx, p);
+                    return fail(FA_ERR_HIP, "slot padding memset failed");
+                }
+        } else if (eager) {
+            p.acc[g] = reinterpret_cast<float*>(p.pool[g] + extra_off);
+        }
     }
     ctx->parts.emplace(part_id, std::move(p));
     return FA_OK;
@@ -872,6 +1276,21 @@ int fa_finalize_gather(fa_ctx* ctx, int part_id, int n_segments, void* const* ds
     return finalize_impl(ctx, part_id, Gather{n_segments, (const void* const*)dsts, bytes}, (flags & FA_HOST_PINNED) != 0);
 }
 
+int fa_reduce_parts(fa_ctx* ctx, int n_parts, const int* part_ids, const float* const* h_weights, void* hip_stream) {
+    g_err.clear();
+    if (!ctx) return fail(FA_ERR_ARG, "ctx is null");
+    if (n_parts < 0 || (n_parts > 0 && !part_ids)) return fail(FA_ERR_ARG, "bad part list");
+    if (hip_stream && ctx->G != 1) return fail(FA_ERR_ARG, "an explicit stream needs a single-GPU ctx");
+    for (int i = 0; i < n_parts; ++i) {
+        Part* p;
+        int rc = check_part(ctx, part_ids[i], &p);
+        if (rc) return rc;
+        if (p->mode == FA_FEDAVG && p->n_submitted != p->D && !(h_weights && h_weights[i]))
+            return fail(FA_ERR_STATE, "part %d: %d of %d clients submitted", part_ids[i], p->n_submitted, p->D);
+    }
+    return reduce_parts_impl(ctx, n_parts, part_ids, h_weights, static_cast<hipStream_t>(hip_stream));
+}
+
 int fa_host_alloc(size_t bytes, void** out) {
     g_err.clear();
     if (!out) return fail(FA_ERR_ARG, "out is null");
@@ -899,23 +1318,12 @@ int fa_bucket_slot(fa_ctx* ctx, int part_id, int gpu, int client_slot, void** d_
     if (rc) return rc;
     if (gpu < 0 || gpu >= ctx->G) return fail(FA_ERR_ARG, "gpu %d out of range", gpu);
     if (client_slot < 0 || client_slot >= p->D) return fail(FA_ERR_ARG, "client slot %d out of range", client_slot);
+    if (!holds(*p, gpu, client_slot))
+        return fail(FA_ERR_ARG, "client slot %d is not held by GPU %d (rs layout: slots [%d,%d))", client_slot, gpu,
+                    p->c0[(size_t)gpu], p->c1[(size_t)gpu]);
     if (d_ptr) *d_ptr = slot_ptr(*p, gpu, client_slot);
-    if (n_elems) *n_elems = p->cnt[gpu];
-    if (elem_offset) *elem_offset = p->off[gpu];
-    return FA_OK;
-}
-
-int fa_bucket_placement(fa_ctx* ctx, int part_id, int gpu, int* n_probes, float* probe_ms, int* chosen) {
-    g_err.clear();
-    Part* p;
-    int rc = check_part(ctx, part_id, &p);
-    if (rc) return rc;
-    if (gpu < 0 || gpu >= ctx->G) return fail(FA_ERR_ARG, "gpu %d out of range", gpu);
-    const auto& ms = p->probe_ms[(size_t)gpu];
-    if (n_probes) *n_probes = (int)ms.size();
-    if (probe_ms)
-        for (size_t i = 0; i < ms.size(); ++i) probe_ms[i] = ms[i];
-    if (chosen) *chosen = p->chosen[(size_t)gpu];
+    if (n_elems) *n_elems = p->cnt[(size_t)gpu];
+    if (elem_offset) *elem_offset = p->off[(size_t)gpu];
     return FA_OK;
 }
 
@@ -925,7 +1333,17 @@ int fa_bucket_output(fa_ctx* ctx, int part_id, int gpu, void** d_ptr) {
     int rc = check_part(ctx, part_id, &p);
     if (rc) return rc;
     if (gpu < 0 || gpu >= ctx->G) return fail(FA_ERR_ARG, "gpu %d out of range", gpu);
-    if (d_ptr) *d_ptr = p->dout[gpu];
+    if (d_ptr) *d_ptr = p->dout[(size_t)gpu];
+    return FA_OK;
+}
+
+int fa_bucket_progress(fa_ctx* ctx, int part_id, int* n_submitted, int* n_reduced) {
+    g_err.clear();
+    Part* p;
+    int rc = check_part(ctx, part_id, &p);
+    if (rc) return rc;
+    if (n_submitted) *n_submitted = p->n_submitted;
+    if (n_reduced) *n_reduced = p->ready ? p->D : p->reduced;
     return FA_OK;
 }
 
@@ -944,7 +1362,12 @@ int fa_copy_output(fa_ctx* ctx, int part_id, void* host_dst) {
     int rc = check_part(ctx, part_id, &p);
     if (rc) return rc;
     if (!host_dst && p->n) return fail(FA_ERR_ARG, "host_dst is null");
-    return copy_output_flat(ctx, *p, host_dst);
+    bool any = false;
+    for (auto& rr : p->runs) any = any || !rr.empty();
+    if (!any && p->n) return fail(FA_ERR_STATE, "part %d has not been reduced", part_id);
+    const size_t bytes = p->n * dsize(p->out);
+    const void* segs[1] = {host_dst};
+    return copy_output(ctx, *p, Gather{1, segs, &bytes}, false);
 }
 
 int fa_sync(fa_ctx* ctx) {
@@ -954,6 +1377,7 @@ int fa_sync(fa_ctx* ctx) {
         DeviceGuard dg(r.dev);
         FA_HIP(hipStreamSynchronize(r.copy));
         FA_HIP(hipStreamSynchronize(r.compute));
+        FA_HIP(hipStreamSynchronize(r.comm));
     }
     return FA_OK;
 }
@@ -967,10 +1391,11 @@ int fa_reduce_device(fa_ctx* ctx, int gpu, const void* const* d_clients, const f
     if (mode != FA_FEDAVG && mode != FA_LITERAL) return fail(FA_ERR_ARG, "bad mode");
     if (ctx && (gpu < 0 || gpu >= ctx->G)) return fail(FA_ERR_ARG, "gpu %d out of range", gpu);
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
-    int dev = ctx ? ctx->gpu[gpu].dev : gpu;
-    if (!s && ctx) s = ctx->gpu[gpu].compute;
+    const int dev = ctx ? ctx->gpu[(size_t)gpu].dev : gpu;
+    if (!s && ctx) s = ctx->gpu[(size_t)gpu].compute;
     DeviceGuard dg(dev);
-    return reduce_on(ctx, ctx ? gpu : 0, d_clients, h_weights, D, n, in, d_out, out, mode,
+    const CtxTuning tu = ctx ? ctx->tuning : defaults();
+    return reduce_on(ctx, ctx ? gpu : 0, tu.tu, d_clients, h_weights, D, n, in, d_out, out, mode,
                      ctx ? ctx->divisor : FA_DEFAULT_DIVISOR, d_init, s);
 }
 
@@ -982,12 +1407,13 @@ int fa_sync_device(fa_ctx* ctx, int gpu, void* const* d_clients, const float* h_
     if (!dvalid(dt)) return fail(FA_ERR_ARG, "bad dtype");
     if (ctx && (gpu < 0 || gpu >= ctx->G)) return fail(FA_ERR_ARG, "gpu %d out of range", gpu);
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
-    if (!s && ctx) s = ctx->gpu[gpu].compute;
+    if (!s && ctx) s = ctx->gpu[(size_t)gpu].compute;
     if (ctx) {
-        DeviceGuard dg(ctx->gpu[gpu].dev);
-        return sync_on(ctx, gpu, d_clients, h_weights, D, n, dt, s);
+        DeviceGuard dg(ctx->gpu[(size_t)gpu].dev);
+        return sync_on(ctx, gpu, ctx->tuning.tu, d_clients, h_weights, D, n, dt, s);
     }
-    return sync_on(nullptr, gpu, d_clients, h_weights, D, n, dt, s);
+    const CtxTuning tu = defaults();
+    return sync_on(nullptr, gpu, tu.tu, d_clients, h_weights, D, n, dt, s);
 }
 
 int fa_sync_part(fa_ctx* ctx, int part_id, const float* h_weights, void* hip_stream) {
@@ -996,15 +1422,17 @@ int fa_sync_part(fa_ctx* ctx, int part_id, const float* h_weights, void* hip_str
     int rc = check_part(ctx, part_id, &p);
     if (rc) return rc;
     if (p->mode != FA_FEDAVG) return fail(FA_ERR_ARG, "part %d is not a FedAvg part", part_id);
+    if (p->rs) return fail(FA_ERR_ARG, "part %d: state sync needs every client on every GPU (range layout)", part_id);
     if (hip_stream && ctx->G != 1) return fail(FA_ERR_ARG, "an explicit stream needs a single-GPU ctx");
     const float* w = h_weights ? h_weights : p->w.data();
-    std::vector<void*> ptrs(p->D);
+    std::vector<void*> ptrs((size_t)p->D);
     for (int g = 0; g < ctx->G; ++g) {
-        GpuRes& r = ctx->gpu[g];
+        GpuRes& r = ctx->gpu[(size_t)g];
         DeviceGuard dg(r.dev);
-        for (int k = 0; k < p->D; ++k) ptrs[k] = slot_ptr(*p, g, k);
+        for (int k = 0; k < p->D; ++k) ptrs[(size_t)k] = slot_ptr(*p, g, k);
         hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : r.compute;
-        if ((rc = sync_on(ctx, g, ptrs.data(), w, p->D, p->cnt[g], p->in, st))) return rc;
+        if ((rc = wait_copies(ctx, g, st))) return rc;  // the slots' submits land first
+        if ((rc = sync_on(ctx, g, ctx->tuning.tu, ptrs.data(), w, p->D, p->cnt[(size_t)g], p->in, st))) return rc;
     }
     return FA_OK;
 }

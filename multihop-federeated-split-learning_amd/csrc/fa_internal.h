@@ -17,6 +17,16 @@ struct ClientTable {
     float w[kMaxClients];
 };
 
+// One bucket of a batched launch (fedavg_segments_kernel): workgroups [blk0, blk0 + nblk) of the grid
+// reduce its nvec 16-byte vectors, the last of them also the scalar tail [nvec * V, n).  Device memory.
+struct SegDesc {
+    int64_t blk0, nblk, nvec, n;
+    void* out;
+    int nc, pad;
+    const void* src[kMaxClients];
+    float w[kMaxClients];
+};
+
 struct Tuning {
     int block;       // threads per workgroup: 64, 128 or 256
     int max_blocks;  // grid cap (grid-stride beyond it), <= 0: uncapped
@@ -40,6 +50,11 @@ hipError_t launch_sync(const ClientTable& t, int nc, fa_dtype dt, const float* i
 // slots t.src[0..nc) := acc (rounded to dt).
 hipError_t launch_broadcast(const ClientTable& t, int nc, fa_dtype dt, const float* acc, int64_t n,
                             const Tuning& tu, hipStream_t s);
+// One launch over nseg buckets (FedAvg, no init, every pointer 16-byte aligned); blocks = sum of nblk.
+hipError_t launch_segments(const SegDesc* d_segs, int nseg, int64_t blocks, fa_dtype in, fa_dtype out, int max_nc,
+                           const Tuning& tu, hipStream_t s);
+// Whether launch_chain takes the phased kernel for a bucket of nvec vectors and nc clients.
+bool phased_takes(fa_dtype in, int64_t nvec, int nc, const Tuning& tu);
 hipError_t launch_fill(void* dst, int64_t n, fa_dtype dt, uint64_t seed, uint32_t client, uint64_t idx0,
                        hipStream_t s);
 

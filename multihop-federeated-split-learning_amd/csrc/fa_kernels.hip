@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdlib>
 #include <mutex>
@@ -348,7 +349,7 @@ __device__ __forceinline__ void put(const ClientTable& t, int nc, void* out, int
 template <typename IN, typename OUT, bool INIT, int REGS, bool SYNC, int TH>
 __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, int nc, const float* init,
                                                                        void* out, int64_t head, int64_t nvec, int64_t n,
-                                                                       unsigned* sync, int slack) {
+                                                                       unsigned* sync, int slack, int rl_last) {
     constexpr int V = In<IN>::kVec, T = TH, RL = Phased<IN, REGS, TH>::RL, RR = Phased<IN, REGS, TH>::RR;
     constexpr int U = TH > 256 ? 8 : 16;  // loads in flight per wave (2 waves per SIMD at 512 threads)
     __shared__ float buf[RL * T * V];
@@ -364,9 +365,12 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
     const int64_t per_phase = G * T * (RL + RR);
     const int phases = (int)((nvec + per_phase - 1) / per_phase);
     for (int p = 0; p < phases; ++p) {
+        // LDS vectors per lane in this phase: RL in full phases; the last phase is balanced by the host
+        // (every lane the same share, registers first: phased_rl_last)
+        const int rl = p == phases - 1 ? rl_last : RL;
         const int64_t base = (int64_t)p * per_phase + (int64_t)blockIdx.x * T + threadIdx.x;
 #pragma unroll 1
-        for (int i = 0; i < RL; ++i) {
+        for (int i = 0; i < rl; ++i) {
             const int64_t v = base + (int64_t)i * G * T;
             if (v < nvec) {
                 float acc[V];
@@ -377,7 +381,7 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
         }
         // register part: this wave's contiguous chunk after the phase's LDS part
         const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-        const int64_t c0 = (int64_t)p * per_phase + G * T * RL + ((int64_t)blockIdx.x * (T / 64) + wave) * RR * 64;
+        const int64_t c0 = (int64_t)p * per_phase + G * T * rl + ((int64_t)blockIdx.x * (T / 64) + wave) * RR * 64;
         float keep[RR][V];
         const bool staged = stage_regs<IN, INIT, RR, U>(t, nc, init, head, c0, nvec, keep);
         if (!staged) {  // the chunk that holds the end of the bucket (or lies past it): no staging
@@ -402,7 +406,7 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
         }
         __syncthreads();
 #pragma unroll 1
-        for (int i = 0; i < RL; ++i) {
+        for (int i = 0; i < rl; ++i) {
             const int64_t v = base + (int64_t)i * G * T;
             if (v < nvec) put<OUT, V, SYNC>(t, nc, out, head + v * V, &buf[(i * T + threadIdx.x) * V]);
         }
@@ -537,6 +541,54 @@ __global__ __launch_bounds__(256) void literal_scalar_kernel(const void* x, void
     }
 }
 
+// ---------------------------------------------------------------- batched buckets (segment table)
+//
+// All model-part buckets of one aggregator phase (aggregator.cpp:108-150: model_part 2..L+1, e.g.
+// ResNet-18's 9,442,304 + 5,130 elements) reduced by ONE launch: segment s owns workgroups
+// [blk0, blk0 + nblk) of a one-shot grid; a workgroup finds its segment by binary search, copies the
+// segment's client table into LDS and runs the same ordered chain as fedavg_chain_kernel (so the bits
+// equal one launch per bucket).  Its last workgroup also takes the segment's scalar tail.  Tiny
+// buckets then cost a few workgroups instead of a launch each.
+
+template <typename IN, typename OUT, int U>
+__global__ __launch_bounds__(256) void fedavg_segments_kernel(const SegDesc* __restrict__ segs, int nseg) {
+    constexpr int V = In<IN>::kVec;
+    __shared__ ClientTable t;
+    __shared__ int s_seg;
+    if (threadIdx.x == 0) {
+        int lo = 0, hi = nseg - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (segs[mid].blk0 <= (int64_t)blockIdx.x) lo = mid;
+            else hi = mid - 1;
+        }
+        s_seg = lo;
+    }
+    __syncthreads();
+    const SegDesc* sd = segs + __builtin_amdgcn_readfirstlane(s_seg);
+    const int nc = sd->nc;
+    for (int i = threadIdx.x; i < nc; i += blockDim.x) {
+        t.src[i] = sd->src[i];
+        t.w[i] = sd->w[i];
+    }
+    __syncthreads();
+    const int64_t b = (int64_t)blockIdx.x - sd->blk0;
+    const int64_t nvec = sd->nvec;
+    const int64_t v = b * blockDim.x + threadIdx.x;
+    if (v < nvec) {
+        float acc[V];
+        chain_vec<IN, U, true, false>(t, nc, nullptr, v * V, acc);
+        Out<OUT>::template store<V, kStSc1>(sd->out, v * V, acc);
+    }
+    if (b == sd->nblk - 1) {
+        for (int64_t i = nvec * V + threadIdx.x; i < sd->n; i += blockDim.x) {
+            float acc = 0.0f;
+            for (int k = 0; k < nc; ++k) acc = __builtin_fmaf(In<IN>::scalar(t.src[k], i), t.w[k], acc);
+            Out<OUT>::scalar(sd->out, i, acc);
+        }
+    }
+}
+
 // ---------------------------------------------------------------- generator
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
@@ -569,6 +621,11 @@ inline int64_t grid_for(int64_t work, const Tuning& tu) {
     if (tu.max_blocks > 0 && g > tu.max_blocks) g = tu.max_blocks;
     return g;
 }
+
+// Grid of the one-element-per-lane kernels (scalar chain, literal, sync, broadcast): grid-stride loops,
+// so the grid is capped -- a bucket of 2^32 elements would otherwise ask for more than 2^32 threads.
+constexpr int64_t kScalarMaxBlocks = 1 << 16;
+inline int64_t grid_scalar(int64_t n, const Tuning& tu) { return std::min(grid_for(n, tu), kScalarMaxBlocks); }
 
 template <typename IN, typename OUT, int U, bool LNT, int SP>
 hipError_t launch_chain_u(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
@@ -642,14 +699,28 @@ PhasedDevice* phased_device() {
     return d.sync ? &d : nullptr;
 }
 
+// LDS vectors per lane in the last phase of a bucket of nvec vectors (fedavg_phased_kernel's rl_last):
+// the last phase's remainder is spread evenly over all `lanes` of the grid.  Up to RL vectors per lane it
+// goes to LDS alone; more fill every wave's register chunk (RR) and LDS takes the rest, so no lane holds
+// more than one vector above the average (filling LDS first and then whole register chunks left half the
+// waves of a partial phase idle while the others did RL + RR).
+inline int phased_rl_last(int64_t nvec, int64_t lanes, int RL, int RR) {
+    const int64_t per_phase = lanes * (RL + RR);
+    const int64_t rem = nvec % per_phase;
+    if (rem == 0) return RL;
+    const int64_t q = (rem + lanes - 1) / lanes;
+    if (q <= RL) return (int)q;
+    return (int)std::max<int64_t>(0, q - RR);
+}
+
 // Enqueue one phased launch on stream s, on the stream's counter slot.
 template <typename Kern>
 hipError_t phased_enqueue(PhasedDevice* d, Kern kern, int th, hipStream_t s, const ClientTable& t, int nc,
-                          const float* init, void* out, int64_t head, int64_t nvec, int64_t n) {
+                          const float* init, void* out, int64_t head, int64_t nvec, int64_t n, int rl_last) {
     const unsigned slot = (unsigned)(((uintptr_t)s >> 4) % kSyncSlots);
     const int slack = d->cus / 32;  // the write part starts once all but ~3% of the workgroups have arrived
     hipLaunchKernelGGL(kern, dim3((unsigned)d->cus), dim3(th), 0, s, t, nc, init, out, head, nvec, n,
-                       d->sync + slot * kSyncStride, slack);
+                       d->sync + slot * kSyncStride, slack, rl_last);
     return hipGetLastError();
 }
 
@@ -665,24 +736,62 @@ bool phased_fits(std::atomic<int>& occ, Kern kern, int th) {
 }
 
 // The phased kernel when it applies (walk 3 = fa_tuning.walk 4, vector path, at least one full phase
-// of work, one workgroup per CU co-resident); otherwise hipErrorNotSupported and the caller takes the
-// one-shot grid.
+// of work -- or any size when `sized`, see launch_phased --, one workgroup per CU co-resident); otherwise
+// hipErrorNotSupported and the caller takes the one-shot grid.
 template <typename IN, typename OUT, int REGS, int TH>
 hipError_t launch_phased_r(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
-                           int64_t n, hipStream_t s) {
+                           int64_t n, hipStream_t s, bool sized = false) {
     PhasedDevice* d = phased_device();
     if (!d) return hipErrorNotSupported;
-    const int64_t per_phase = (int64_t)d->cus * TH * (Phased<IN, REGS, TH>::RL + Phased<IN, REGS, TH>::RR);
+    constexpr int RL = Phased<IN, REGS, TH>::RL, RR = Phased<IN, REGS, TH>::RR;
+    const int64_t per_phase = (int64_t)d->cus * TH * (RL + RR);
     // experiment knob (tools/): FA_PHASED_MIN_VECS lowers the smallest bucket the phased kernel takes
     static const int64_t min_env = [] {
         const char* e = std::getenv("FA_PHASED_MIN_VECS");
         return e ? (int64_t)std::atoll(e) : (int64_t)-1;
     }();
-    if (nvec < (min_env >= 0 ? min_env : per_phase)) return hipErrorNotSupported;
+    if (!sized && nvec < (min_env >= 0 ? min_env : per_phase)) return hipErrorNotSupported;
     static std::atomic<int> occ[2] = {-1, -1};  // per INIT variant
     auto kern = init ? fedavg_phased_kernel<IN, OUT, true, REGS, false, TH> : fedavg_phased_kernel<IN, OUT, false, REGS, false, TH>;
     if (!phased_fits(occ[init ? 1 : 0], kern, TH)) return hipErrorNotSupported;
-    return phased_enqueue(d, kern, TH, s, t, nc, init, out, head, nvec, n);
+    return phased_enqueue(d, kern, TH, s, t, nc, init, out, head, nvec, n,
+                          phased_rl_last(nvec, (int64_t)d->cus * TH, RL, RR));
+}
+
+// Clients from which a bucket smaller than one phase takes a phase sized to it (launch_phased); fewer
+// clients make the output a larger share of the traffic, and its write burst after the meeting costs
+// more than the one-shot grid's interleaving (C2, D = 8: 0.085 vs 0.075 ms).
+int sized_min_clients() {
+    static const int v = [] {
+        const char* e = std::getenv("FA_SIZED_MIN_CLIENTS");
+        return e ? std::atoi(e) : 16;
+    }();
+    return v;
+}
+
+// One phase sized to a bucket below one full phase: q = vectors per lane; the register stage takes the
+// largest RR <= q from the instantiated set and LDS the rest (q - RR <= RL), so every lane holds q or
+// q - 1 vectors.  E.g. the strong-scaled north star at 4 ranks (16.8 M f32 elements per rank): q = 64 ->
+// 48 in registers + 16 in LDS, where the full-phase layout gave half the waves 88 and half 40.
+template <typename IN, typename OUT, int TH>
+hipError_t launch_phased_sized(const ClientTable& t, int nc, const float* init, void* out, int64_t head,
+                               int64_t nvec, int64_t n, hipStream_t s) {
+    PhasedDevice* d = phased_device();
+    if (!d || nc < sized_min_clients()) return hipErrorNotSupported;
+    const int64_t lanes = (int64_t)d->cus * TH;
+    const int64_t q = (nvec + lanes - 1) / lanes;
+    if constexpr (std::is_same<IN, float>::value) {  // V = 4: RR = REGS / 4
+        if (q >= 48) return launch_phased_r<IN, OUT, 192, TH>(t, nc, init, out, head, nvec, n, s, true);
+        if (q >= 32) return launch_phased_r<IN, OUT, 128, TH>(t, nc, init, out, head, nvec, n, s, true);
+        if (q >= 24) return launch_phased_r<IN, OUT, 96, TH>(t, nc, init, out, head, nvec, n, s, true);
+        if (q >= 16) return launch_phased_r<IN, OUT, 64, TH>(t, nc, init, out, head, nvec, n, s, true);
+        if (q >= 8) return launch_phased_r<IN, OUT, 32, TH>(t, nc, init, out, head, nvec, n, s, true);
+    } else {  // V = 8: RR = REGS / 8
+        if (q >= 12) return launch_phased_r<IN, OUT, 96, TH>(t, nc, init, out, head, nvec, n, s, true);
+        if (q >= 8) return launch_phased_r<IN, OUT, 64, TH>(t, nc, init, out, head, nvec, n, s, true);
+        if (q >= 4) return launch_phased_r<IN, OUT, 32, TH>(t, nc, init, out, head, nvec, n, s, true);
+    }
+    return hipErrorNotSupported;
 }
 
 // Smallest bucket (elements of dtype `in` per GPU) that the phased walk of `tu` takes on the current
@@ -705,10 +814,12 @@ hipError_t launch_phased(const ClientTable& t, int nc, const float* init, void* 
     if (tu.walk == 4) {  // the default: bf16 inputs take the 512-thread form (2 waves per SIMD hide the
                          // widening VALU work of 8 elements per load: C3 0.430 vs 0.439 ms), f32 the
                          // 256-thread one (C4 5.43 vs 5.49 ms, C5's share 2.55 vs 2.56), gpurun_out r01s25
-        if constexpr (std::is_same<IN, uint16_t>::value)
-            return launch_phased_r<IN, OUT, 96, 512>(t, nc, init, out, head, nvec, n, s);
-        else
-            return launch_phased_r<IN, OUT, 192, 256>(t, nc, init, out, head, nvec, n, s);
+        constexpr bool bf = std::is_same<IN, uint16_t>::value;
+        constexpr int TH = bf ? 512 : 256;
+        const hipError_t e = bf ? launch_phased_r<IN, OUT, 96, 512>(t, nc, init, out, head, nvec, n, s)
+                                : launch_phased_r<IN, OUT, 192, 256>(t, nc, init, out, head, nvec, n, s);
+        if (e != hipErrorNotSupported) return e;
+        return launch_phased_sized<IN, OUT, TH>(t, nc, init, out, head, nvec, n, s);
     }
     if (tu.walk == 5) return launch_phased_r<IN, OUT, 96, 512>(t, nc, init, out, head, nvec, n, s);
     return hipErrorNotSupported;
@@ -722,7 +833,7 @@ hipError_t launch_chain_t(const ClientTable& t, int nc, const float* init, void*
         if (e != hipErrorNotSupported) return e;
     }
     if (!vector_ok) {
-        const int64_t g = grid_for(n, tu);
+        const int64_t g = grid_scalar(n, tu);
         if (init)
             hipLaunchKernelGGL((fedavg_chain_scalar_kernel<IN, OUT, true>), dim3((unsigned)g), dim3(tu.block), 0, s,
                                t, nc, init, out, n);
@@ -755,7 +866,7 @@ template <typename IN, typename OUT>
 hipError_t launch_literal_t(const void* x, void* out, float divisor, int64_t head, int64_t nvec, int64_t n,
                             bool vector_ok, const Tuning& tu, hipStream_t s) {
     if (!vector_ok) {
-        hipLaunchKernelGGL((literal_scalar_kernel<IN, OUT>), dim3((unsigned)grid_for(n, tu)), dim3(tu.block), 0, s,
+        hipLaunchKernelGGL((literal_scalar_kernel<IN, OUT>), dim3((unsigned)grid_scalar(n, tu)), dim3(tu.block), 0, s,
                            x, out, divisor, n);
     } else {  // two streams only: nt loads, write-through stores
         hipLaunchKernelGGL((literal_kernel<IN, OUT, true, kStSc1>), dim3((unsigned)grid_for(nvec > 0 ? nvec : 1, tu)),
@@ -801,7 +912,8 @@ hipError_t launch_sync_phased_r(const ClientTable& t, int nc, int64_t head, int6
     static std::atomic<int> occ{-1};
     auto kern = fedavg_phased_kernel<T, T, false, REGS, true, TH>;
     if (!phased_fits(occ, kern, TH)) return hipErrorNotSupported;
-    return phased_enqueue(d, kern, TH, s, t, nc, (const float*)nullptr, (void*)nullptr, head, nvec, n);
+    return phased_enqueue(d, kern, TH, s, t, nc, (const float*)nullptr, (void*)nullptr, head, nvec, n,
+                          phased_rl_last(nvec, (int64_t)d->cus * TH, Phased<T, REGS, TH>::RL, Phased<T, REGS, TH>::RR));
 }
 
 template <typename T>
@@ -814,7 +926,7 @@ hipError_t launch_sync_t(const ClientTable& t, int nc, const float* init, int64_
         if (e != hipErrorNotSupported) return e;
     }
     if (!vector_ok) {
-        const int64_t g = grid_for(n, tu);
+        const int64_t g = grid_scalar(n, tu);
         if (init)
             hipLaunchKernelGGL((fedavg_sync_scalar_kernel<T, true>), dim3((unsigned)g), dim3(tu.block), 0, s, t, nc,
                                init, n);
@@ -840,12 +952,48 @@ hipError_t launch_sync(const ClientTable& t, int nc, fa_dtype dt, const float* i
 
 hipError_t launch_broadcast(const ClientTable& t, int nc, fa_dtype dt, const float* acc, int64_t n,
                             const Tuning& tu, hipStream_t s) {
-    const int64_t g = grid_for(n, tu);
+    const int64_t g = grid_scalar(n, tu);
     if (dt == FA_F32)
         hipLaunchKernelGGL((broadcast_kernel<float>), dim3((unsigned)g), dim3(tu.block), 0, s, t, nc, acc, n);
     else
         hipLaunchKernelGGL((broadcast_kernel<uint16_t>), dim3((unsigned)g), dim3(tu.block), 0, s, t, nc, acc, n);
     return hipGetLastError();
+}
+
+namespace {
+template <typename IN, typename OUT>
+hipError_t launch_segments_t(const SegDesc* d_segs, int nseg, int64_t blocks, int max_nc, int block,
+                             hipStream_t s) {
+    if (max_nc <= 8)
+        hipLaunchKernelGGL((fedavg_segments_kernel<IN, OUT, 8>), dim3((unsigned)blocks), dim3(block), 0, s, d_segs,
+                           nseg);
+    else
+        hipLaunchKernelGGL((fedavg_segments_kernel<IN, OUT, 16>), dim3((unsigned)blocks), dim3(block), 0, s,
+                           d_segs, nseg);
+    return hipGetLastError();
+}
+}  // namespace
+
+hipError_t launch_segments(const SegDesc* d_segs, int nseg, int64_t blocks, fa_dtype in, fa_dtype outdt, int max_nc,
+                           const Tuning& tu, hipStream_t s) {
+    if (nseg <= 0) return hipSuccess;
+    if (in == FA_F32 && outdt == FA_F32) return launch_segments_t<float, float>(d_segs, nseg, blocks, max_nc, tu.block, s);
+    if (in == FA_F32 && outdt == FA_BF16)
+        return launch_segments_t<float, uint16_t>(d_segs, nseg, blocks, max_nc, tu.block, s);
+    if (in == FA_BF16 && outdt == FA_F32)
+        return launch_segments_t<uint16_t, float>(d_segs, nseg, blocks, max_nc, tu.block, s);
+    return launch_segments_t<uint16_t, uint16_t>(d_segs, nseg, blocks, max_nc, tu.block, s);
+}
+
+bool phased_takes(fa_dtype in, int64_t nvec, int nc, const Tuning& tu) {
+    if (tu.walk < 3 || tu.walk > 5) return false;
+    const int64_t full = phased_min_elems_impl(in, tu) / (in == FA_F32 ? 4 : 8);
+    if (full <= 0) return false;
+    if (nvec >= full) return true;
+    if (tu.walk != 4 || nc < sized_min_clients()) return false;
+    PhasedDevice* d = phased_device();
+    const int64_t lanes = (int64_t)d->cus * (in == FA_F32 ? 256 : 512);
+    return (nvec + lanes - 1) / lanes >= (in == FA_F32 ? 8 : 4);
 }
 
 hipError_t launch_fill(void* dst, int64_t n, fa_dtype dt, uint64_t seed, uint32_t client, uint64_t idx0,

@@ -47,6 +47,9 @@ struct Options {
     fa_mode mode = FA_FEDAVG;
     float divisor = 1000.0f;  // kTrainSize_10, aggregator.cpp:48
     bool discover = false, pinned = true;
+    bool rs = false;     // --layout rs: clients dealt to the GPUs, RCCL reduce-scatter of fp32 partials
+    bool eager = false;  // --eager: accumulate on arrival (the chain advances with the in-order receipts)
+    int rs_chunks = 0;
     double link_mbps = 0;
     std::map<int, double> samples;  // client id -> n_k
 };
@@ -54,7 +57,8 @@ struct Options {
 void usage() {
     std::cerr << "usage: fa_aggregator -i ID -d DATA_OWNERS -c COMPUTE_NODES [--mode fedavg|literal] [--gpus G]\n"
                  "       [--rounds R] [--port-base P] [--discover] [--link-mbps M] [--samples id:n,...]\n"
-                 "       [--divisor K] [--last-layers L] [--no-pinned]\n";
+                 "       [--divisor K] [--last-layers L] [--no-pinned] [--layout range|rs] [--rs-chunks C]\n"
+                 "       [--eager]\n";
 }
 
 bool parse_args(int argc, char** argv, Options* o) {
@@ -77,6 +81,13 @@ bool parse_args(int argc, char** argv, Options* o) {
         else if (a == "--divisor") o->divisor = (float)std::atof(val("--divisor"));
         else if (a == "--discover") o->discover = true;
         else if (a == "--no-pinned") o->pinned = false;
+        else if (a == "--eager") o->eager = true;
+        else if (a == "--rs-chunks") o->rs_chunks = std::atoi(val("--rs-chunks"));
+        else if (a == "--layout") {
+            std::string l = val("--layout");
+            if (l == "rs") o->rs = true;
+            else if (l != "range") return false;
+        }
         else if (a == "--link-mbps") o->link_mbps = std::atof(val("--link-mbps"));
         else if (a == "--mode") {
             std::string m = val("--mode");
@@ -132,8 +143,15 @@ double secs_since(std::chrono::steady_clock::time_point t) {
 class Aggregator {
 public:
     Aggregator(const Options& o, NetLayer* net, const std::vector<int>& owners) : o_(o), net_(net) {
-        FA_CHECK(fa_create(&ctx_, o.gpus, o.gpus > 1 ? FA_SHARD_RANGE : 0));
+        int flags = o.rs ? FA_SHARD_CLIENT_RS : o.gpus > 1 ? FA_SHARD_RANGE : 0;
+        if (o.eager) flags |= FA_ACCUMULATE_ON_ARRIVAL;
+        FA_CHECK(fa_create(&ctx_, o.gpus, flags));
         FA_CHECK(fa_set_literal_divisor(ctx_, -1, o.divisor));
+        if (o.rs_chunks > 0) {
+            fa_tuning t{};
+            t.rs_chunks = o.rs_chunks;
+            FA_CHECK(fa_ctx_set_tuning(ctx_, &t));
+        }
         std::vector<int> order = owners;
         if ((int)order.size() != o.data_owners) {
             order = {0};
@@ -245,6 +263,16 @@ public:
     }
 
     size_t bytes_in(int mp) { return buckets_[mp].bytes_in; }
+
+    // The reductions of a phase's buckets as one batched launch (fa_reduce_parts: the last-part layers of
+    // phase 2, aggregator.cpp:108-150, are one segment table); the following reduce() calls then only
+    // copy each result into its reply.  With --eager the chains already ran as the receipts arrived.
+    void reduce_all(const std::vector<int>& mps) {
+        if (o_.eager || mps.size() < 2) return;
+        const auto t0 = std::chrono::steady_clock::now();
+        FA_CHECK(fa_reduce_parts(ctx_, (int)mps.size(), mps.data(), nullptr, nullptr));
+        st_.finalize_s += secs_since(t0);
+    }
 
     // Host-side time split since the last call: archive parse + slot staging (absorb), the GPU
     // reduction incl. its D2H copy (finalize), the reply archive + frame (frame).
@@ -379,7 +407,10 @@ int main(int argc, char** argv) {
         for (int mp = 2; mp <= L + 1; ++mp) in2 += agg.bytes_in(mp);
         auto t3 = std::chrono::steady_clock::now();
         std::vector<std::shared_ptr<const Bytes>> replies;
-        for (int mp = 2; mp <= L + 1; ++mp) replies.push_back(agg.reduce(mp));
+        std::vector<int> mps;
+        for (int mp = 2; mp <= L + 1; ++mp) mps.push_back(mp);
+        agg.reduce_all(mps);
+        for (int mp : mps) replies.push_back(agg.reduce(mp));
         const double red2 = secs_since(t3);
         const auto s2 = agg.take_stats();
         auto t4 = std::chrono::steady_clock::now();

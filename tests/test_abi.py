@@ -6,6 +6,7 @@ import os
 import re
 import subprocess
 
+import numpy as np
 import pytest
 
 from conftest import ROOT
@@ -52,12 +53,12 @@ def test_library_is_gfx950_code(fa, tmp_path):
 
 def test_version_and_errors_without_gpu(fa):
     L = fa.lib()
-    assert L.fa_version() == 3
+    assert L.fa_version() == 4
     # argument errors are reported before any device work
     rc = L.fa_reduce_device(None, 0, None, None, 0, 16, 0, None, 0, 0, None, None)
     assert rc == fa.ERR_ARG and "null" in fa.last_error()
     assert L.fa_fill_uniform(None, 4, 7, 0, 0, 0, None) == fa.ERR_ARG
-    t = fa._Tuning(96, 0, 0, 0, 0, 0)
+    t = fa._Tuning(96, 0, 0, 0, 0, 0, 0, 0)
     assert L.fa_set_tuning(ctypes.byref(t)) == fa.ERR_ARG
     assert L.fa_bucket_define(None, 1, 10, 0, 0, 1, 0) == fa.ERR_ARG
     assert fa.last_error() == "ctx is null"
@@ -71,25 +72,51 @@ def test_version_and_errors_without_gpu(fa):
 
 def test_tuning_roundtrip(fa):
     before = fa.get_tuning()
-    fa.set_tuning(block=128, unroll=16, load_policy=1, store_policy=4)
+    fa.set_tuning(block=128, unroll=16, load_policy=1, store_policy=4, rs_chunks=5)
     assert fa.get_tuning() == {"block": 128, "max_blocks": before["max_blocks"], "unroll": 16, "load_policy": 1,
-                               "store_policy": 4, "slot_skew": before["slot_skew"],
-                               "placement_probes": before["placement_probes"], "walk": before["walk"]}
+                               "store_policy": 4, "slot_skew": before["slot_skew"], "walk": before["walk"],
+                               "rs_chunks": 5}
     with pytest.raises(fa.FaError):
         fa.set_tuning(store_policy=5)
     assert fa.get_tuning()["store_policy"] == 4  # a rejected call changes nothing
     fa.set_tuning(slot_skew=-1)
     assert fa.get_tuning()["slot_skew"] == 0
-    fa.set_tuning(placement_probes=-1)
-    assert fa.get_tuning()["placement_probes"] == 1
-    with pytest.raises(fa.FaError):
-        fa.set_tuning(placement_probes=17)
-    with pytest.raises(fa.FaError):
-        fa.set_tuning(slot_skew=100)
-    with pytest.raises(fa.FaError):
-        fa.set_tuning(walk=7)
+    for bad in (dict(slot_skew=100), dict(walk=7), dict(rs_chunks=2000), dict(block=96)):
+        with pytest.raises(fa.FaError):
+            fa.set_tuning(**bad)
     fa.set_tuning(**{k: (v or -1) if k in ("max_blocks", "slot_skew") else v for k, v in before.items()})
     assert fa.get_tuning() == before
+
+
+def test_ctx_tuning_needs_a_ctx(fa):
+    L = fa.lib()
+    t = fa._Tuning()
+    assert L.fa_ctx_set_tuning(None, ctypes.byref(t)) == fa.ERR_ARG
+    assert L.fa_ctx_get_tuning(None, ctypes.byref(t)) == fa.ERR_ARG
+    assert L.fa_reduce_parts(None, 0, None, None, None) == fa.ERR_ARG
+    assert L.fa_bucket_progress(None, 1, None, None) == fa.ERR_ARG
+
+
+@pytest.mark.parametrize("n,world,chunks", [(64, 1, 1), (1000, 2, 1), (10_000, 2, 4), (7_777, 3, 5),
+                                            (123_457, 8, 16), (256 * 8, 8, 3), (1 << 20, 4, 8)])
+def test_rs_segments_match_shard_cyclic_bounds(fa, n, world, chunks):
+    """The C ABI's rs ownership (fa_rs_segments, used by FA_SHARD_CLIENT_RS to copy each GPU's shard out)
+    equals shard.cyclic_bounds, whose exchange the gloo tests check against the oracle; together the GPUs'
+    segments tile the padded bucket exactly once."""
+    import importlib
+    shard = importlib.import_module("mhfsl_amd.shard")
+    unit = world * shard.UNIT
+    npad = -(-n // unit) * unit
+    seen = np.zeros(npad, np.int32)
+    for g in range(world):
+        segs = fa.rs_segments(n, world, chunks, g)
+        assert segs == shard.cyclic_bounds(npad, world, g, chunks)
+        assert sum(b - a for a, b in segs) == npad // world
+        for a, b in segs:
+            seen[a:b] += 1
+    assert np.all(seen == 1)
+    with pytest.raises(fa.FaError):
+        fa.rs_segments(n, world, chunks, world)
 
 
 def test_no_device_fails_loudly(fa):

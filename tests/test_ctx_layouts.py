@@ -1,0 +1,228 @@
+"""GPU tests of the aggregation context's layouts and round shapes through the C ABI, against the oracle.
+
+* FA_SHARD_CLIENT_RS: clients dealt to the context's GPUs, fp32 partials summed by an RCCL reduce-scatter
+  (ncclCommInitAll in-process), pieces overlapped with the reduction; bit-exact at one GPU (a one-rank
+  reduce-scatter is a copy), within 1e-6 of sum_k |w_k x_k| at more.
+* FA_ACCUMULATE_ON_ARRIVAL: the chain advances over the in-order prefix of receipts (same bits).
+* fa_reduce_parts: every model-part bucket of a phase in one batched launch (segment table), the
+  aggregator's own bucket sizes (tests/golden/layouts: ResNet-18 split 3,8), same bits as per part.
+The reduction the reference performs here is aggregator.cpp:59-93 / :112-150.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def assert_bits(got, ref):
+    ut = np.uint16 if got.dtype == np.uint16 else np.uint32
+    bad = np.flatnonzero(got.view(ut) != ref.view(ut))
+    assert bad.size == 0, "%d/%d mismatches, first at %s: got %s ref %s" % (
+        bad.size, got.size, bad[:4], got[bad[:4]], ref[bad[:4]])
+
+
+def host_clients(O, seed, D, n, bf16=False):
+    return [O.gen(seed, k, n, dtype="bf16" if bf16 else "f32") for k in range(D)]
+
+
+def rs_ctx(fa, G):
+    """An rs context on G GPUs: real ones when visible, else G communicators on GPU 0 (test-only
+    FA_TEST_SHARED_DEVICE) -- RCCL may refuse two ranks on one device, then the case is skipped."""
+    if fa.device_count() >= G:
+        return fa.Aggregator(G, rs=True)
+    try:
+        return fa.Aggregator(devices=[0] * G, rs=True, shared_device=True)
+    except fa.FaError as e:
+        if e.code == fa.ERR_NCCL:
+            pytest.skip("RCCL refuses %d ranks on one GPU: %s" % (G, e))
+        raise
+
+
+# ----------------------------------------------------------------- FA_SHARD_CLIENT_RS
+
+@pytest.mark.parametrize("n,D,chunks,bf16", [(1_000_003, 5, 1, False), (4_194_304, 8, 8, False),
+                                             (333_333, 3, 4, True), (63, 2, 3, False), (2_000_000, 130, 2, False)])
+def test_rs_layout_one_gpu_bitexact(fa, O, torch_gpu, n, D, chunks, bf16):
+    """One GPU: the reduce-scatter over a one-rank communicator is a copy, so the pieces' chains are the
+    single chain -- bit-exact, whatever the piece count; the slot padding stays out of the result."""
+    w = O.weights(D)
+    xs = host_clients(O, 60 + D, D, n, bf16)
+    with fa.Aggregator(1, rs=True) as agg:
+        agg.set_tuning(rs_chunks=chunks)
+        assert agg.get_tuning()["rs_chunks"] == chunks
+        agg.define(1, n, fa.BF16 if bf16 else fa.F32, fa.F32, D, fa.FEDAVG)
+        for k in reversed(range(D)):
+            agg.submit(1, k, xs[k], w[k])
+        assert_bits(agg.finalize(1), O.fedavg(xs, w))
+        # the device-resident round on the same slots
+        agg.reduce(1, w)
+        assert_bits(agg.copy_output(1), O.fedavg(xs, w))
+
+
+def test_rs_layout_literal_and_errors(fa, O, torch_gpu):
+    n, D = 100_001, 3
+    xs = host_clients(O, 70, D, n)
+    with fa.Aggregator(1, rs=True) as agg:
+        with pytest.raises(fa.FaError):
+            agg.define(1, n, fa.F32, fa.BF16, D, fa.FEDAVG)  # rs sums fp32 partials: f32 out only
+        agg.define(1, n, fa.F32, fa.F32, D, fa.LITERAL)
+        for k in [0, 2, 1]:
+            agg.submit(1, k, xs[k])
+        assert_bits(agg.finalize(1), O.literal(xs[1]))
+        with pytest.raises(fa.FaError):
+            agg.sync_states(1)
+
+
+@pytest.mark.parametrize("G", [2, 4])
+def test_rs_layout_multi_gpu_tolerance(fa, O, torch_gpu, G):
+    """G communicators: every GPU's shard holds its cyclic blocks; the whole result within 1e-6 of
+    sum_k |w_k x_k| of the oracle's ordered chain (the reduce-scatter adds per-GPU partials)."""
+    n, D = 1_234_567, 7
+    w = O.weights(D)
+    xs = host_clients(O, 71, D, n)
+    with rs_ctx(fa, G) as agg:
+        agg.define(1, n, fa.F32, fa.F32, D, fa.FEDAVG)
+        for k in range(D):
+            agg.submit(1, k, xs[k], w[k])
+        got = agg.finalize(1)
+    ref = O.fedavg(xs, w)
+    absw = sum(abs(np.float64(wk)) * np.abs(x.astype(np.float64)) for wk, x in zip(w, xs))
+    err = np.abs(got.astype(np.float64) - ref) / (1e-6 * absw + 1e-30)
+    assert np.all(err <= 1.0), float(err.max())
+
+
+# ----------------------------------------------------------------- accumulate on arrival
+
+@pytest.mark.parametrize("G", [1, 2])
+def test_accumulate_on_arrival_same_bits(fa, O, torch_gpu, G):
+    """Receipts in order advance the chain one launch at a time (the phase end then only copies);
+    out of order they wait for the gap; a replaced receipt restarts the chain.  Every result equals
+    the one ordered chain bit for bit."""
+    n, D = 2_000_003, 6
+    w = O.weights(D)
+    xs = host_clients(O, 72, D, n)
+    ref = O.fedavg(xs, w)
+    ctx = fa.Aggregator(G, eager=True) if fa.device_count() >= G else \
+        fa.Aggregator(devices=[0] * G, eager=True, shared_device=True)
+    with ctx as agg:
+        agg.define(1, n, fa.F32, fa.F32, D, fa.FEDAVG)
+        for k in range(D):  # in order: the prefix grows with every receipt
+            agg.submit(1, k, xs[k], w[k])
+            assert agg.progress(1) == (k + 1, k + 1)
+        assert_bits(agg.finalize(1), ref)
+        assert agg.progress(1) == (0, 0)
+        order = [1, 0, 3, 2, 5, 4]
+        reduced = []
+        for k in order:  # out of order: the prefix only moves past gaps once they are filled
+            agg.submit(1, k, xs[k], w[k])
+            reduced.append(agg.progress(1)[1])
+        assert reduced == [0, 2, 2, 4, 4, 6]
+        assert_bits(agg.finalize(1), ref)
+        for k in range(D):
+            agg.submit(1, k, xs[k], w[k])
+        xs2 = list(xs)
+        xs2[2] = O.gen(73, 2, n)
+        agg.submit(1, 2, xs2[2], w[2])  # a replaced receipt: the chain restarts and catches up at once
+        assert agg.progress(1) == (D, D)
+        assert_bits(agg.finalize(1), O.fedavg(xs2, w))
+        # bf16 output, a part defined with D > kMaxClients (two passes from the accumulator)
+        agg.define(2, 50_001, fa.F32, fa.BF16, 130, fa.FEDAVG)
+        w130 = O.weights(130)
+        x130 = host_clients(O, 74, 130, 50_001)
+        for k in range(130):
+            agg.submit(2, k, x130[k], w130[k])
+        assert_bits(agg.finalize(2), O.f32_to_bf16(O.fedavg(x130, w130)))
+
+
+# ----------------------------------------------------------------- one launch per phase
+
+@pytest.mark.parametrize("device_resident", [True, False])
+def test_reduce_parts_batched_same_bits(fa, O, torch_gpu, device_resident):
+    """ResNet-18's split-3,8 buckets (83,584 / 9,442,304 / 5,130 elements, D = 8, the reference builders'
+    sizes) in one fa_reduce_parts call: the two last-part buckets are one segment-table launch; plus a
+    bf16 bucket and a D = 32 bucket large enough for the phased kernel in the same call.  Each result
+    equals the oracle (whole buckets up to 10 M elements)."""
+    torch = torch_gpu
+    D = 8
+    parts = {1: (83_584, D, False), 2: (9_442_304, D, False), 3: (5_130, D, False), 4: (77_777, 5, True),
+             5: (6_000_001, 32, False)}
+    with fa.Aggregator(1) as agg:
+        for pid, (n, d, bf16) in parts.items():
+            agg.define(pid, n, fa.BF16 if bf16 else fa.F32, fa.F32, d, fa.FEDAVG)
+        refs = {}
+        for pid, (n, d, bf16) in parts.items():
+            wd = O.weights(d)
+            xs = host_clients(O, 80 + pid, d, n, bf16)
+            refs[pid] = O.fedavg(xs, wd, threads=8)
+            for k in range(d):
+                if device_resident:
+                    ptr, cnt, _ = agg.slot(pid, 0, k)
+                    fa.fill_uniform(ptr, cnt, fa.BF16 if bf16 else fa.F32, 80 + pid, k)
+                else:
+                    agg.submit(pid, k, xs[k], wd[k])
+        torch.cuda.synchronize()
+        ids = list(parts)
+        if device_resident:
+            agg.reduce_parts(ids, weights=[O.weights(parts[p][1]) for p in ids])
+            for pid in ids:
+                assert_bits(agg.copy_output(pid), refs[pid])
+        else:
+            agg.reduce_parts(ids)
+            for pid in ids:
+                assert agg.progress(pid)[1] == parts[pid][1]  # ready: finalize only copies
+                assert_bits(agg.finalize(pid), refs[pid])
+        with pytest.raises(fa.FaError):
+            agg.reduce_parts([1, 1])
+
+
+def test_reduce_parts_two_gpus_and_literal(fa, O, torch_gpu):
+    """Range shards of a two-GPU context (two shards on one GPU when only one is visible): each GPU's
+    segment table holds its ranges; a literal part in the same call takes its own launch."""
+    ctx = fa.Aggregator(2) if fa.device_count() >= 2 else fa.Aggregator(devices=[0, 0], shared_device=True)
+    D = 4
+    w = O.weights(D)
+    with ctx as agg:
+        sizes = {1: 100_003, 2: 64, 3: 1}
+        for pid, n in sizes.items():
+            agg.define(pid, n, fa.F32, fa.F32, D, fa.FEDAVG)
+        agg.define(9, 5000, fa.F32, fa.F32, D, fa.LITERAL)
+        refs = {}
+        for pid, n in sizes.items():
+            xs = host_clients(O, 90 + pid, D, n)
+            refs[pid] = O.fedavg(xs, w)
+            for k in range(D):
+                agg.submit(pid, k, xs[k], w[k])
+        lit = host_clients(O, 99, D, 5000)
+        for k in [3, 1]:
+            agg.submit(9, k, lit[k])
+        agg.reduce_parts([1, 2, 3, 9])
+        for pid in sizes:
+            assert_bits(agg.finalize(pid), refs[pid])
+        assert_bits(agg.finalize(9), O.literal(lit[1]))
+
+
+def d2h(ptr, n):
+    """n fp32 elements at a raw device address, copied to the host (hipMemcpy, device to host)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    out = np.empty(n, np.float32)
+    assert hip.hipMemcpy(ctypes.c_void_p(out.ctypes.data), ctypes.c_void_p(ptr), ctypes.c_size_t(4 * n), 2) == 0
+    return out
+
+
+def test_sync_part_waits_for_submits(fa, O, torch_gpu):
+    """fa_submit then fa_sync_part with no fa_sync between: the state sync orders itself after the
+    submits' H2D copies, so every slot holds the FedAvg of the submitted receipts."""
+    n, D = 3_000_001, 5
+    w = O.weights(D)
+    xs = host_clients(O, 95, D, n)
+    with fa.Aggregator(1) as agg:
+        agg.define(1, n, fa.F32, fa.F32, D, fa.FEDAVG)
+        for k in range(D):
+            agg.submit(1, k, xs[k], w[k])
+        agg.sync_states(1)
+        agg.sync()
+        ref = O.fedavg(xs, w)
+        for k in (0, D - 1):
+            ptr, cnt, _ = agg.slot(1, 0, k)
+            assert_bits(d2h(ptr, cnt), ref)

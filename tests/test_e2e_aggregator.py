@@ -85,15 +85,22 @@ def _large_parts(d):
     return {mp: sum(p.numel() for p in m.parameters()) for mp, m in parts.items()}
 
 
-@pytest.mark.parametrize("pinned,sequential", [(True, False), (False, False), (True, True)])
-def test_multi_mb_parts_concurrent_owners(torch_gpu, tmp_path, pinned, sequential):
+@pytest.mark.parametrize("pinned,sequential,extra", [
+    (True, False, []), (False, False, []), (True, True, []),
+    (True, True, ["--eager"]),                          # chains advance as the in-order receipts land
+    (True, False, ["--eager"]),
+    (True, False, ["--layout", "rs", "--rs-chunks", "3"]),  # RCCL reduce-scatter layout (one GPU: a copy)
+])
+def test_multi_mb_parts_concurrent_owners(torch_gpu, tmp_path, pinned, sequential, extra):
     """D=6 owners sending at once (or one after another) multi-MB parts: pinned zero-copy ingest
     (fa_submit_gather_pinned from the received frame) and D2H into the reply frame
-    (fa_finalize_gather), or the pageable staging path with --no-pinned; bit-exact FedAvg every round."""
+    (fa_finalize_gather), or the pageable staging path with --no-pinned; phase 2's two buckets reduced
+    by one batched launch (fa_reduce_parts), or accumulated on arrival (--eager), or through the rs
+    layout; bit-exact FedAvg every round."""
     sizes = _large_parts(str(tmp_path))
     D, rounds = 6, 2
     base = pick_base()
-    cmd = [AGG, "-i", "-1", "-d", str(D), "-c", "1", "--rounds", str(rounds), "--port-base", str(base)]
+    cmd = [AGG, "-i", "-1", "-d", str(D), "-c", "1", "--rounds", str(rounds), "--port-base", str(base)] + extra
     agg = subprocess.Popen(cmd + ([] if pinned else ["--no-pinned"]), stdout=subprocess.PIPE,
                            stderr=subprocess.PIPE, text=True)
     try:

@@ -150,6 +150,47 @@ def test_phased_walk_same_bits(fa, O, torch_gpu, in_bf16, out_bf16, D, phases, o
     del clients
 
 
+LANES_F32, LANES_BF16 = 256 * 256, 256 * 512  # phased grid lanes (256 CUs): f32 256-thread, bf16 512-thread
+
+
+@pytest.mark.parametrize("in_bf16,D,q,frac", [
+    # buckets below one phase, D >= 16: one phase sized to the bucket, q vectors per lane
+    (False, 16, 9, 0.3), (False, 16, 20, 0.9), (False, 20, 26, 0.5), (False, 16, 40, 0.1), (False, 32, 64, 0.0),
+    (False, 17, 87, 0.7),
+    (True, 16, 5, 0.5), (True, 16, 9, 0.2), (True, 18, 20, 0.9),
+    # several phases whose last one is balanced: q_last in (RL, RR) -> registers only, > RR -> both
+    (False, 32, 88 + 44, 0.5), (False, 16, 88 * 2 + 70, 0.3), (True, 16, 22 + 15, 0.4),
+])
+def test_sized_phase_same_bits(fa, O, torch_gpu, in_bf16, D, q, frac):
+    """Phases sized to the bucket (launch_phased_sized) and the balanced last phase (phased_rl_last)
+    against the one-shot walk on the same device inputs, whole buckets bit for bit, plus sampled
+    elements against the oracle.  n = q vectors per lane minus a fraction of one lane-vector row, so
+    the last register chunk crosses the end of the bucket."""
+    torch = torch_gpu
+    lanes, V = (LANES_BF16, 8) if in_bf16 else (LANES_F32, 4)
+    n = q * lanes * V - int(frac * lanes * V) - 3
+    w = O.weights(D)
+    seed = 1300 + q
+    clients = [filled(fa, torch, n, in_bf16, seed, k) for k in range(D)]
+    before = fa.get_tuning()
+    outs = {}
+    try:
+        for walk in (2, 5):
+            fa.set_tuning(walk=walk)
+            out = dev_buf(torch, n, False)
+            fa.reduce_device(clients, w, n, fa.BF16 if in_bf16 else fa.F32, out, fa.F32, fa.FEDAVG)
+            torch.cuda.synchronize()
+            outs[walk] = out
+    finally:
+        fa.set_tuning(walk=before["walk"])
+    assert torch.equal(outs[2].view(torch.int32), outs[5].view(torch.int32))
+    if not in_bf16:
+        rng = np.random.default_rng(q)
+        idx = np.unique(np.concatenate([[0, n - 1], rng.integers(0, n, 512)]))
+        assert_bits(outs[5][torch.as_tensor(idx, device="cuda")].cpu().numpy(), O.fedavg_at(seed, w, idx))
+    del clients
+
+
 def test_fedavg_zero_elements_is_noop(fa, O, torch_gpu):
     torch = torch_gpu
     c = [dev_buf(torch, 4, False)]
@@ -405,13 +446,21 @@ def test_context_errors(fa, O, torch_gpu):
             agg.finalize(9)
 
 
-def test_context_multi_gpu_range_shards(fa, O, torch_gpu):
-    if fa.device_count() < 2:
-        pytest.skip("needs 2 GPUs in one process")
+def multi_gpu_ctx(fa, G, **kw):
+    """A G-GPU context: real GPUs when visible, else G shards of one context on GPU 0 (test-only
+    FA_TEST_SHARED_DEVICE), so the multi-GPU host logic (ranges, per-GPU staging, split gather/scatter,
+    per-GPU done events) runs on the one-GPU box."""
+    if fa.device_count() >= G:
+        return fa.Aggregator(G, **kw)
+    return fa.Aggregator(devices=[0] * G, shared_device=True, **kw)
+
+
+@pytest.mark.parametrize("G", [2, 3])
+def test_context_multi_gpu_range_shards(fa, O, torch_gpu, G):
     n, D = 1_000_001, 4
     w = O.weights(D)
     xs = host_clients(O, 49, D, n, False)
-    with fa.Aggregator(2) as agg:
+    with multi_gpu_ctx(fa, G) as agg:
         agg.define(1, n, fa.F32, fa.F32, D, fa.FEDAVG)
         for k in range(D):
             agg.submit(1, k, xs[k], w[k])
@@ -480,9 +529,8 @@ def test_context_submit_gather_matches_flat(fa, O, torch_gpu):
 def test_context_zero_copy_gather_in_and_out(fa, O, torch_gpu, pinned, gpus):
     """fa_submit_gather_pinned + fa_finalize_gather: receipts as ragged records at odd byte offsets of one
     pinned frame buffer (how the network layer hands them over), the result scattered into the records
-    of a reply buffer; == the flat path, bit for bit.  gpus=2 splits the ranges across record pieces."""
-    if gpus > fa.device_count():
-        gpus = 1
+    of a reply buffer; == the flat path, bit for bit.  gpus=2 splits the ranges across record pieces
+    (two shards on one GPU when only one is visible)."""
     n, D = 3_000_017, 3
     w = O.weights(D)
     xs = host_clients(O, 53, D, n, False)
@@ -503,7 +551,7 @@ def test_context_zero_copy_gather_in_and_out(fa, O, torch_gpu, pinned, gpus):
     rraw = reply.view() if pinned else np.zeros(4 * n + 100, np.uint8)
     out_cuts = [0, 1, 333_333, n]
     outs = [rraw[7 + 4 * a: 7 + 4 * b] for a, b in zip(out_cuts, out_cuts[1:])]
-    with fa.Aggregator(gpus) as agg:
+    with multi_gpu_ctx(fa, gpus) as agg:
         agg.define(1, n, fa.F32, fa.F32, D, fa.FEDAVG)
         for k in range(D):
             agg.submit_gather(1, k, pieces[k], w[k], pinned=pinned)
@@ -518,40 +566,6 @@ def test_context_zero_copy_gather_in_and_out(fa, O, torch_gpu, pinned, gpus):
         f.close()
     if reply:
         reply.close()
-
-
-def test_placement_probing_keeps_bits_and_records(fa, O, torch_gpu):
-    """A >= 1 GiB FedAvg pool is placed by probing (fa_bucket_define) under a one-shot walk: the record
-    lists the candidates' probe times and the kept one is the fastest; results stay bit-exact; probing
-    off gives no record.  Under the phased walk (same speed in every pool) the pool is not probed."""
-    n, D = 80_000_000, 4  # 4 x 320 MB slots + output: 1.6 GB pool
-    w = O.weights(D)
-    idx = np.unique(np.concatenate([np.arange(0, 4096), np.arange(n - 4096, n),
-                                    np.random.default_rng(5).integers(0, n, 4096)]))
-    before = fa.get_tuning()
-    try:
-        for probes, walk in ((3, 2), (-1, 2), (3, 5)):
-            fa.set_tuning(placement_probes=probes, walk=walk)
-            with fa.Aggregator(1) as agg:
-                agg.define(1, n, fa.F32, fa.F32, D, fa.FEDAVG)
-                rec = agg.placement(1)
-                if walk == 5:
-                    assert rec["probe_ms"] == []
-                elif probes > 0:
-                    assert 1 <= len(rec["probe_ms"]) <= probes
-                    assert rec["probe_ms"][rec["chosen"]] == min(rec["probe_ms"])
-                else:
-                    assert rec["probe_ms"] == []
-                for k in range(D):
-                    ptr, cnt, _ = agg.slot(1, 0, k)
-                    fa.fill_uniform(ptr, cnt, fa.F32, 71, k)
-                torch_gpu.cuda.synchronize()
-                agg.reduce(1, w)
-                out = np.empty(n, np.float32)
-                agg.copy_output(1, out)
-                assert_bits(out[idx], O.fedavg_at(71, w, idx))
-    finally:
-        fa.set_tuning(placement_probes=before["placement_probes"], walk=before["walk"])
 
 
 # ----------------------------------------------------------------- IEEE special values

@@ -21,7 +21,7 @@ for s in $STEPS; do
     echo "== $s $(date +%T)" | tee -a "$OUT/session.log"
     case $s in
     test)
-        timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rf --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
+        timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rfs --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
         rc=$?; tail -5 "$OUT/pytest_gpu.log"; ok_or_fail $rc test ;;
     smoke)
         timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
@@ -50,9 +50,8 @@ for s in $STEPS; do
     outexp)
         timeout -k 10 600 python tools/exp_out.py 25 10 > "$OUT/exp_out.jsonl" 2> "$OUT/exp_out.err"
         rc=$?; cat "$OUT/exp_out.jsonl"; tail -2 "$OUT/exp_out.err"; ok_or_fail $rc outexp ;;
-    ranks)  # multi-rank rehearsal of the driver's N>1 launch: 2 ranks share the one GPU over gloo
-        timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-            --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2 --dist-backend gloo > "$OUT/bench_2ranks.json" 2> "$OUT/bench_2ranks.err"
+    ranks)  # multi-rank rehearsal of the driver's N>1 launch: bench.py spawns 2 ranks, which share the one GPU over gloo
+        timeout -k 10 600 python bench.py --gpus 2 --steps 5 --warmup 2 > "$OUT/bench_2ranks.json" 2> "$OUT/bench_2ranks.err"
         rc=$?; cat "$OUT/bench_2ranks.json"; tail -3 "$OUT/bench_2ranks.err"; ok_or_fail $rc ranks ;;
     vmm)  # physical placement of the client pool via the VMM API (tools/exp_vmm.hip)
         hipcc --offload-arch=gfx950 -O2 tools/exp_vmm.hip -Iinclude -Lmultihop-federeated-split-learning_amd/lib -lfa \
@@ -110,6 +109,11 @@ for s in $STEPS; do
             timeout -k 10 300 python tools/rs_launch.py $W 16 10 >> "$OUT/rs_launch.jsonl" 2>> "$OUT/rs_launch.err"
             rc=$?; tail -1 "$OUT/rs_launch.jsonl"; ok_or_fail $rc rslaunch_$W
         done ;;
+    slices)  # one rank's share of the strong-scaled north star at W = 1, 2, 4, 8 (tools/strong_slices.py)
+        timeout -k 10 300 python tools/strong_slices.py 20 > "$OUT/slices.jsonl" 2> "$OUT/slices.err"
+        rc=$?; cat "$OUT/slices.jsonl"; tail -2 "$OUT/slices.err"; ok_or_fail $rc slices
+        FA_PHASED_MIN_VECS=0 timeout -k 10 300 python tools/strong_slices.py 20 > "$OUT/slices_phased.jsonl" 2>> "$OUT/slices.err"
+        rc=$?; cat "$OUT/slices_phased.jsonl"; ok_or_fail $rc slices_phased ;;
     e2e)
         timeout -k 10 900 python tools/e2e_bench.py 4 3 > "$OUT/e2e_bench.json" 2> "$OUT/e2e_bench.err"
         rc=$?; cat "$OUT/e2e_bench.json"; tail -3 "$OUT/e2e_bench.err"; ok_or_fail $rc e2e ;;
