@@ -67,7 +67,9 @@ typedef enum {
  * clients that came late or out of order.  Same bits as one chain. */
 #define FA_ACCUMULATE_ON_ARRIVAL 0x4
 /* Test only: accept a device id more than once (several shards of one context on one GPU), so the
- * multi-GPU host logic runs on a one-GPU box. */
+ * multi-GPU host logic runs on a one-GPU box.  RCCL refuses two ranks on one device, so with
+ * FA_SHARD_CLIENT_RS the reduce-scatter is replaced by its definition (each shard block := the sum of
+ * the GPUs' partials in rank order, a device launch); everything else of the layout is unchanged. */
 #define FA_TEST_SHARED_DEVICE 0x100
 
 int fa_version(void);

@@ -505,6 +505,28 @@ int chain_range(fa_ctx* ctx, Part& p, int g, int k0, int k1, const float* w, hip
                      last ? p.out : FA_F32, FA_FEDAVG, p.divisor, init, st);
 }
 
+// FA_TEST_SHARED_DEVICE with FA_SHARD_CLIENT_RS: RCCL refuses two ranks on one device, so the
+// reduce-scatter of piece [a, a + G q) is replaced by its definition -- shard g block [off, off + q) :=
+// sum over h of partial_h[a + g q, a + (g + 1) q) in rank order, one launch per shard on its exchange
+// stream after every shard's piece reduction -- so that the rest of the layout (client dealing, pieces,
+// padding, shard offsets, copy-out runs) runs on a one-GPU box.  Never used with distinct devices.
+int emulated_reduce_scatter(fa_ctx* ctx, Part& p, size_t a, size_t q, size_t off) {
+    const int G = ctx->G;
+    for (int g = 0; g < G; ++g)
+        for (int h = 0; h < G; ++h) FA_HIP(hipStreamWaitEvent(ctx->gpu[(size_t)g].comm, ctx->gpu[(size_t)h].step_ev, 0));
+    std::vector<const void*> ptrs((size_t)G);
+    const std::vector<float> ones((size_t)G, 1.0f);
+    for (int g = 0; g < G; ++g) {
+        GpuRes& r = ctx->gpu[(size_t)g];
+        DeviceGuard dg(r.dev);
+        for (int h = 0; h < G; ++h) ptrs[(size_t)h] = p.partial[(size_t)h] + a + (size_t)g * q;
+        int rc = reduce_on(ctx, g, ctx->tuning.tu, ptrs.data(), ones.data(), G, q, FA_F32,
+                           static_cast<float*>(p.dout[(size_t)g]) + off, FA_F32, FA_FEDAVG, 1.0f, nullptr, r.comm);
+        if (rc) return rc;
+    }
+    return FA_OK;
+}
+
 // Enqueue the full reduction of part p on every GPU (the ctx's streams, or `s` for a one-GPU ctx):
 // range -> each GPU's shard; rs -> the clients' fp32 partials, piece by piece, each piece's RCCL
 // reduce-scatter (ring over xGMI) overlapping the reduction of the next.
@@ -577,6 +599,12 @@ int reduce_part(fa_ctx* ctx, Part& p, const float* w, hipStream_t s) {
             }
             FA_HIP(hipEventRecord(r.step_ev, st));
             FA_HIP(hipStreamWaitEvent(r.comm, r.step_ev, 0));
+        }
+        if (ctx->flags & FA_TEST_SHARED_DEVICE) {  // test only: every shard on one GPU, no RCCL (below)
+            int rc = emulated_reduce_scatter(ctx, p, a, q, off);
+            if (rc) return rc;
+            off += q;
+            continue;
         }
         FA_NCCL(ncclGroupStart());
         for (int g = 0; g < G; ++g) {
@@ -1077,7 +1105,7 @@ int fa_create_ex(fa_ctx** out, const int* device_ids, int n_gpus, int flags) {
         }
         r.pool.reset(new CopyPool(threads));
     }
-    if (flags & FA_SHARD_CLIENT_RS) {  // one RCCL communicator per GPU, all in this process
+    if ((flags & FA_SHARD_CLIENT_RS) && !(flags & FA_TEST_SHARED_DEVICE)) {  // one RCCL communicator per GPU
         std::vector<ncclComm_t> comms((size_t)n_gpus, nullptr);
         const ncclResult_t e = ncclCommInitAll(comms.data(), n_gpus, device_ids);
         if (e != ncclSuccess) {

@@ -74,6 +74,14 @@ bool fail(std::string* err, const std::string& m) {
     return false;
 }
 
+// [off, off + len) lies inside a buffer of `size` bytes (no overflow for any 64-bit inputs).
+bool in_bounds(uint64_t off, uint64_t len, uint64_t size) { return off <= size && len <= size - off; }
+
+// Largest decompressed code record accepted (libtorch's code/ records are a few KiB to a few MiB).
+constexpr uint64_t kMaxCodeRecord = 64ull << 20;
+// Nesting of modules the walk follows (a pickle can make an object its own child through the memo).
+constexpr int kMaxModuleDepth = 256;
+
 // ------------------------------------------------------------------ pickle objects
 
 struct PObj;
@@ -287,7 +295,8 @@ P unpickle(const uint8_t* p, size_t n, std::string* err) {
             }
             case 'Q': {  // BINPERSID: ('storage', <StorageType global>, key, location, numel)
                 P pid = pop();
-                if (!pid || pid->kind != PObj::Tuple || pid->items.size() < 3 || pid->items[2]->kind != PObj::Str)
+                if (!pid || pid->kind != PObj::Tuple || pid->items.size() < 3 || pid->items[2]->kind != PObj::Str ||
+                    pid->items[1]->kind != PObj::Global)
                     return fail(err, "pickle: unsupported persistent id"), nullptr;
                 P st = make(PObj::Storage);
                 st->s = pid->items[2]->s;
@@ -308,13 +317,23 @@ P unpickle(const uint8_t* p, size_t n, std::string* err) {
                 P args = pop(), fn = pop();
                 if (!fn || !args || args->kind != PObj::Tuple) return fail(err, "pickle: bad REDUCE"), nullptr;
                 if (fn->kind == PObj::Global && fn->s == "torch._utils _rebuild_tensor_v2") {
-                    if (args->items.size() < 4 || args->items[0]->kind != PObj::Storage)
+                    // (storage, storage_offset, size tuple, stride tuple, ...): every index non-negative
+                    if (args->items.size() < 4 || args->items[0]->kind != PObj::Storage ||
+                        args->items[1]->kind != PObj::Int || args->items[2]->kind != PObj::Tuple ||
+                        args->items[3]->kind != PObj::Tuple ||
+                        args->items[2]->items.size() != args->items[3]->items.size() || args->items[1]->i < 0)
                         return fail(err, "pickle: bad _rebuild_tensor_v2"), nullptr;
                     P t = make(PObj::Tensor);
                     t->storage = args->items[0];
                     t->offset = args->items[1]->i;
-                    for (auto& x : args->items[2]->items) t->sizes.push_back(x->i);
-                    for (auto& x : args->items[3]->items) t->strides.push_back(x->i);
+                    for (auto& x : args->items[2]->items) {
+                        if (x->kind != PObj::Int || x->i < 0) return fail(err, "pickle: bad tensor size"), nullptr;
+                        t->sizes.push_back(x->i);
+                    }
+                    for (auto& x : args->items[3]->items) {
+                        if (x->kind != PObj::Int || x->i < 0) return fail(err, "pickle: bad tensor stride"), nullptr;
+                        t->strides.push_back(x->i);
+                    }
                     stack.push_back(t);
                 } else if (fn->kind == PObj::Global && fn->s == "collections OrderedDict") {
                     stack.push_back(make(PObj::Dict));
@@ -397,27 +416,34 @@ bool TorchArchive::parse(const uint8_t* bytes, size_t size, std::string* err) {
     uint64_t n_entries = rd16(bytes + eocd + 10), cd_off = rd32(bytes + eocd + 16);
     if (eocd >= 20 && rd32(bytes + eocd - 20) == 0x07064b50) {  // zip64 locator
         const uint64_t z64 = rd64(bytes + eocd - 20 + 8);
-        if (z64 + 56 > size || rd32(bytes + z64) != 0x06064b50) return fail(err, "zip: bad zip64 record");
+        if (!in_bounds(z64, 56, size) || rd32(bytes + z64) != 0x06064b50) return fail(err, "zip: bad zip64 record");
         n_entries = rd64(bytes + z64 + 32);
         cd_off = rd64(bytes + z64 + 48);
     }
     uint64_t q = cd_off;
     for (uint64_t e = 0; e < n_entries; ++e) {
-        if (q + 46 > size || rd32(bytes + q) != 0x02014b50) return fail(err, "zip: bad central directory");
+        if (!in_bounds(q, 46, size) || rd32(bytes + q) != 0x02014b50) return fail(err, "zip: bad central directory");
         const uint16_t method = rd16(bytes + q + 10), nlen = rd16(bytes + q + 28), xlen = rd16(bytes + q + 30),
                        clen = rd16(bytes + q + 32);
+        if (!in_bounds(q, 46ull + nlen + xlen + clen, size)) return fail(err, "zip: central directory entry out of bounds");
         ZipEntry z;
         z.crc = rd32(bytes + q + 16);
         uint64_t csize = rd32(bytes + q + 20), usize = rd32(bytes + q + 24), loff = rd32(bytes + q + 42);
         z.name.assign((const char*)bytes + q + 46, nlen);
         // zip64 extended information: only the fields that are 0xFFFFFFFF are present, in this order
-        for (uint64_t x = q + 46 + nlen; x + 4 <= q + 46 + nlen + xlen;) {
+        const uint64_t xend = q + 46 + nlen + xlen;
+        for (uint64_t x = q + 46 + nlen; x + 4 <= xend;) {
             const uint16_t id = rd16(bytes + x), len = rd16(bytes + x + 2);
+            if (x + 4 + len > xend) return fail(err, "zip: extra field of " + z.name + " out of bounds");
             if (id == 0x0001) {
                 uint64_t f = x + 4;
-                if (usize == 0xFFFFFFFFu) usize = rd64(bytes + f), f += 8;
-                if (csize == 0xFFFFFFFFu) csize = rd64(bytes + f), f += 8;
-                if (loff == 0xFFFFFFFFu) loff = rd64(bytes + f), f += 8;
+                const uint64_t fend = f + len;
+                for (uint64_t* v : {&usize, &csize, &loff}) {
+                    if (*v != 0xFFFFFFFFu) continue;
+                    if (f + 8 > fend) return fail(err, "zip: short zip64 field in " + z.name);
+                    *v = rd64(bytes + f);
+                    f += 8;
+                }
             }
             x += 4 + len;
         }
@@ -425,16 +451,17 @@ bool TorchArchive::parse(const uint8_t* bytes, size_t size, std::string* err) {
         if (method == 0 && csize != usize) return fail(err, "zip: stored record " + z.name + " has mismatched sizes");
         z.method = method;
         z.comp_size = csize;
-        if (loff + 30 > size || rd32(bytes + loff) != 0x04034b50) return fail(err, "zip: bad local header");
+        if (!in_bounds(loff, 30, size) || rd32(bytes + loff) != 0x04034b50) return fail(err, "zip: bad local header");
         const uint16_t lflags = rd16(bytes + loff + 6);
         z.data_offset = loff + 30 + rd16(bytes + loff + 26) + rd16(bytes + loff + 28);
         z.size = usize;
         z.cd_offset = q;
         z.local_offset = loff;
-        if (z.data_offset + z.comp_size > size) return fail(err, "zip: record " + z.name + " out of bounds");
+        if (!in_bounds(z.data_offset, z.comp_size, size)) return fail(err, "zip: record " + z.name + " out of bounds");
         if (lflags & 0x08) {  // data descriptor follows the data, optionally with its signature
             uint64_t d = z.data_offset + z.comp_size;
-            if (d + 4 <= size && rd32(bytes + d) == 0x08074b50) d += 4;
+            if (in_bounds(d, 4, size) && rd32(bytes + d) == 0x08074b50) d += 4;
+            if (!in_bounds(d, 4, size)) return fail(err, "zip: data descriptor of " + z.name + " out of bounds");
             z.desc_offset = d;
         }
         entries_.push_back(z);
@@ -459,7 +486,7 @@ bool TorchArchive::parse(const uint8_t* bytes, size_t size, std::string* err) {
     // -- exactly named_parameters(recurse=true) / named_buffers(recurse=true).
     std::string werr;
     std::map<std::string, std::string> code_cache;
-    std::function<bool(const P&, const std::string&, std::vector<TensorView>*, bool)> walk;
+    std::function<bool(const P&, const std::string&, std::vector<TensorView>*, bool, int)> walk;
     auto code_for = [&](const std::string& global) -> std::pair<std::string, std::string> {
         // "__torch__.___torch_mangle_0 Module" -> (code/__torch__/___torch_mangle_0.py, "Module")
         const size_t sp = global.find(' ');
@@ -472,7 +499,8 @@ bool TorchArchive::parse(const uint8_t* bytes, size_t size, std::string* err) {
             std::string text;
             if (z && z->method == 0) {
                 text.assign((const char*)bytes + z->data_offset, z->size);
-            } else if (z) {  // raw deflate (libtorch compresses some code records)
+            } else if (z && z->size <= kMaxCodeRecord && z->size / 1032 <= z->comp_size) {
+                // raw deflate (libtorch compresses some code records); deflate expands at most ~1032:1
                 text.resize(z->size);
                 z_stream zs{};
                 if (inflateInit2(&zs, -MAX_WBITS) == Z_OK) {
@@ -491,8 +519,10 @@ bool TorchArchive::parse(const uint8_t* bytes, size_t size, std::string* err) {
         }
         return {it->second, cls};
     };
-    walk = [&](const P& obj, const std::string& prefix, std::vector<TensorView>* out, bool want_params) -> bool {
+    walk = [&](const P& obj, const std::string& prefix, std::vector<TensorView>* out, bool want_params,
+               int depth) -> bool {
         if (!obj || obj->kind != PObj::Object || !obj->state || obj->state->kind != PObj::Dict) return true;
+        if (depth > kMaxModuleDepth) return fail(&werr, "archive: module tree deeper than 256 (a cycle?)");
         auto code = code_for(obj->cls ? obj->cls->s : std::string());
         const std::vector<std::string> pnames = class_parameters(code.first, code.second);
         std::vector<std::pair<P, std::string>> children;
@@ -511,8 +541,16 @@ bool TorchArchive::parse(const uint8_t* bytes, size_t size, std::string* err) {
                 tv.sizes = v->sizes;
                 tv.strides = v->strides;
                 tv.storage_offset = v->offset;
-                tv.numel = 1;
-                for (auto s : tv.sizes) tv.numel *= s;
+                // sizes, strides and the offset are non-negative (unpickle); the element count and the
+                // last index are computed in 128 bits and must fit the storage record
+                __int128 numel = 1, max_index = tv.storage_offset;
+                for (size_t d = 0; d < tv.sizes.size(); ++d) {
+                    numel *= tv.sizes[d];
+                    if (numel > ((__int128)1 << 50)) return fail(&werr, "archive: tensor " + tv.name + " too large");
+                }
+                tv.numel = (int64_t)numel;
+                for (size_t d = 0; d < tv.sizes.size(); ++d)
+                    if (tv.sizes[d] > 0) max_index += (__int128)(tv.sizes[d] - 1) * tv.strides[d];
                 int64_t expect = 1;
                 tv.contiguous = true;
                 for (size_t d = tv.sizes.size(); d-- > 0;) {
@@ -524,11 +562,10 @@ bool TorchArchive::parse(const uint8_t* bytes, size_t size, std::string* err) {
                 tv.record = it->second;
                 const ZipEntry& z = entries_[tv.record];
                 if (z.method != 0) return fail(&werr, "archive: tensor record " + z.name + " is compressed");
-                int64_t max_index = tv.storage_offset;
-                for (size_t d = 0; d < tv.sizes.size(); ++d)
-                    if (tv.sizes[d] > 0) max_index += (tv.sizes[d] - 1) * tv.strides[d];
-                if (tv.numel > 0 && (uint64_t)(max_index + 1) * tv.elem_size > z.size)
+                if (tv.numel > 0 && (max_index + 1) * (__int128)tv.elem_size > (__int128)z.size)
                     return fail(&werr, "archive: tensor " + tv.name + " exceeds its storage");
+                if (tv.numel == 0 && (__int128)tv.storage_offset * tv.elem_size > (__int128)z.size)
+                    return fail(&werr, "archive: tensor " + tv.name + " starts past its storage");
                 tv.data = bytes + z.data_offset + (uint64_t)tv.storage_offset * tv.elem_size;
                 out->push_back(tv);
             } else if (v->kind == PObj::Object) {
@@ -536,10 +573,10 @@ bool TorchArchive::parse(const uint8_t* bytes, size_t size, std::string* err) {
             }
         }
         for (auto& c : children)
-            if (!walk(c.first, c.second, out, want_params)) return false;
+            if (!walk(c.first, c.second, out, want_params, depth + 1)) return false;
         return true;
     };
-    if (!walk(root, "", &params_, true) || !walk(root, "", &buffers_, false)) return fail(err, werr);
+    if (!walk(root, "", &params_, true, 0) || !walk(root, "", &buffers_, false, 0)) return fail(err, werr);
     return true;
 }
 

@@ -159,12 +159,14 @@ void NetLayer::stop() {
         std::lock_guard<std::mutex> lk(m_tx_);
     }
     cv_tx_.notify_all();
+    // wake the receiver's poll/accept, and close the socket only after it has left: closing under it
+    // raced its reads of listen_fd_ (TSan, tests/test_host_sanitizers.py) and could hand it a reused fd
+    if (listen_fd_ >= 0) shutdown(listen_fd_, SHUT_RDWR);
+    if (rx_.joinable()) rx_.join();
     if (listen_fd_ >= 0) {
-        shutdown(listen_fd_, SHUT_RDWR);
         close(listen_fd_);
         listen_fd_ = -1;
     }
-    if (rx_.joinable()) rx_.join();
     for (auto& s : senders_) {
         if (s->th.joinable()) s->th.join();
         for (auto& kv : s->open) close(kv.second);
@@ -174,19 +176,11 @@ void NetLayer::stop() {
 
 NetLayer::Item NetLayer::parse_frame(std::shared_ptr<Bytes> text, bool* keep) {
     Item it;
-    // Parse the header without touching the archive: the header is the text before "values : ".
-    const size_t scan = std::min<size_t>(text->size(), 4096);
-    const char* base = text->data();
-    const char* v = nullptr;
-    for (size_t i = 0; i + 9 <= scan; ++i)
-        if (std::memcmp(base + i, "values : ", 9) == 0 && (i == 0 || base[i - 1] == '\n')) {
-            v = base + i;
-            break;
-        }
-    std::string head = v ? std::string(base, v - base) + "values : ,\n}" : std::string(base, scan);
+    // Parse the header without touching the archive (split_receipt, wire.h).
     Message m;
     std::string err;
-    if (!decode(head, &m, &err)) {
+    size_t blob_off = 0, blob_len = 0;
+    if (!split_receipt(text->data(), text->size(), &m, &blob_off, &blob_len, &err)) {
         std::cerr << "[net] dropping malformed frame: " << err << "\n";
         return it;
     }
@@ -199,10 +193,8 @@ NetLayer::Item NetLayer::parse_frame(std::shared_ptr<Bytes> text, bool* keep) {
         r.model_part = m.model_part;
         r.type_op = m.type_op;
         r.t_start = m.t_start;
-        if (v) {
-            r.blob_off = (size_t)(v - base) + 9;
-            r.blob_len = text->size() >= r.blob_off + 3 ? text->size() - 3 - r.blob_off : 0;
-        }
+        r.blob_off = blob_off;
+        r.blob_len = blob_len;
         if (link_mbps_ > 0) {  // network_layer.cpp:654-665, opt-in
             const long due = r.t_start + (long)(text->size() * 8.0 / (link_mbps_ * 1e6) * 1000.0);
             const long now = now_ms();
@@ -256,14 +248,14 @@ void NetLayer::receiver_loop() {
             }
         }
     };
+    const int lfd = listen_fd_;  // stop() closes it only after this thread has been joined
     while (running_) {
-        if (listen_fd_ < 0) break;
-        pollfd p{listen_fd_, POLLIN, 0};
+        pollfd p{lfd, POLLIN, 0};
         if (poll(&p, 1, 200) <= 0) {
             reap(false);
             continue;
         }
-        int fd = accept(listen_fd_, nullptr, nullptr);
+        int fd = accept(lfd, nullptr, nullptr);
         if (fd < 0) continue;
         big_buffers(fd);
         conns.emplace_back(new Conn());
@@ -383,7 +375,11 @@ Receipt NetLayer::next_receipt() {
 
 bool NetLayer::try_next_receipt(Receipt* r, int timeout_ms) {
     std::unique_lock<std::mutex> lk(m_rx_);
-    if (!cv_rx_.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return !receipts_.empty(); })) return false;
+    // wait_until on the system clock (pthread_cond_timedwait): libstdc++'s steady-clock wait_for goes
+    // through pthread_cond_clockwait, which ThreadSanitizer (gcc 11) does not intercept -- it then
+    // misses the unlock inside the wait and reports the receiver's next lock as a double lock.
+    const auto until = std::chrono::system_clock::now() + std::chrono::milliseconds(timeout_ms);
+    if (!cv_rx_.wait_until(lk, until, [&] { return !receipts_.empty(); })) return false;
     *r = std::move(receipts_.front());
     receipts_.pop_front();
     return true;

@@ -1,7 +1,9 @@
 // wire.cpp -- Message.h frame encoder/decoder (see wire.h for the grammar).
 #include "wire.h"
 
+#include <algorithm>
 #include <cstring>
+#include <stdexcept>
 #include <map>
 #include <sstream>
 
@@ -186,7 +188,43 @@ std::string frame(const Message& m) {
     return std::string(b->data(), b->size());
 }
 
+namespace {
+bool decode_impl(const std::string& text, Message* m, std::string* err);
+}
+
+// Integer fields that do not parse (std::stoi / std::stol throw) fail the decode instead of throwing
+// out of the receiver thread.
 bool decode(const std::string& text, Message* m, std::string* err) {
+    try {
+        return decode_impl(text, m, err);
+    } catch (const std::exception& e) {
+        if (err) *err = std::string("bad field value: ") + e.what();
+        return false;
+    }
+}
+
+bool split_receipt(const char* base, size_t size, Message* m, size_t* blob_off, size_t* blob_len, std::string* err) {
+    // The header is the text before "values : " (at a line start, within the first 4 KiB); the archive
+    // runs from there to the closing ",\n}" (Message.h:514-518), parsed without touching its bytes.
+    const size_t scan = std::min<size_t>(size, 4096);
+    const char* v = nullptr;
+    for (size_t i = 0; i + 9 <= scan; ++i)
+        if (std::memcmp(base + i, "values : ", 9) == 0 && (i == 0 || base[i - 1] == '\n')) {
+            v = base + i;
+            break;
+        }
+    const std::string head = v ? std::string(base, v - base) + "values : ,\n}" : std::string(base, scan);
+    if (!decode(head, m, err)) return false;
+    *blob_off = *blob_len = 0;
+    if (v) {
+        *blob_off = (size_t)(v - base) + 9;
+        *blob_len = size >= *blob_off + 3 ? size - 3 - *blob_off : 0;
+    }
+    return true;
+}
+
+namespace {
+bool decode_impl(const std::string& text, Message* m, std::string* err) {
     // fromStr_toJson (Message.h:499-569): split on ",\n", name/value on " : "; `values`
     // swallows the rest of the text minus the closing ",\n}".
     std::map<std::string, std::string> kv;
@@ -251,5 +289,6 @@ bool decode(const std::string& text, Message* m, std::string* err) {
     *m = std::move(r);
     return true;
 }
+}  // namespace
 
 }  // namespace fahost

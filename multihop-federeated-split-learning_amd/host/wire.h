@@ -102,6 +102,9 @@ std::string operation_header(const Message& m);
 std::shared_ptr<Bytes> operation_frame(const Message& m, size_t values_len, char** values);
 // Parses the text of a frame; false (with *err) when a field is missing or malformed.
 bool decode(const std::string& text, Message* m, std::string* err);
+// A received OPERATION frame's text (no length prefix): the header fields decoded into *m, and where
+// the torch::save archive (`values`) lies inside it; false for a malformed header.
+bool split_receipt(const char* base, size_t size, Message* m, size_t* blob_off, size_t* blob_len, std::string* err);
 // Length-prefixed frame as it goes on the socket (one copy of m.values).
 std::string frame(const Message& m);
 std::shared_ptr<Bytes> frame_bytes(const Message& m);
