@@ -197,6 +197,59 @@ class Setup:
         return self.D * self.n * self.s_in
 
 
+# The buckets one aggregation round forms (tests/golden/layouts, the reference builders): phase 1 reduces
+# model_part 1 (aggregator.cpp:59-93), phase 2 the last-part layers 2..L+1 (:108-150).
+ROUNDS = {
+    # name: (clients, dtype, phase-1 bucket, phase-2 buckets, description)
+    "round_c2": (8, "f32", 83_584, [9_442_304, 5_130], "ResNet-18 split 3,8, 8 owners, fp32"),
+    "round_c3": (32, "bf16", 2_594_688, [29_511_680, 5_130], "ResNet-101 split 10,19, 32 owners, bf16"),
+    "round_c4": (64, "f32", 38_720, [2_359_808, 119_586_826], "VGG-19 split 3,19, 64 owners, fp32"),
+}
+
+
+class RoundSetup:
+    """One aggregator round on the device: phase 1 = fa_reduce_part of model_part 1, phase 2 =
+    fa_reduce_parts over the last-part layers (one batched launch for the small ones, the phased kernel for
+    a large one).  `batched=False` launches every part on its own (the round-1 aggregator)."""
+
+    def __init__(self, fa, torch, name, device, batched=True, min_rotate_bytes=ROTATE_MIN_BYTES):
+        D, dt, p1, p2, self.desc = ROUNDS[name]
+        self.fa, self.D, self.batched = fa, D, batched
+        self.in_dt = fa.F32 if dt == "f32" else fa.BF16
+        self.s = 4 if dt == "f32" else 2
+        self.sizes = [p1] + list(p2)
+        set_bytes = D * sum(self.sizes) * self.s
+        self.nsets = max(1, -(-min_rotate_bytes // set_bytes))
+        self.agg = fa.Aggregator(devices=[device])
+        for st in range(self.nsets):
+            for j, n in enumerate(self.sizes):
+                pid = 10 * st + j + 1
+                self.agg.define(pid, n, self.in_dt, self.in_dt, D, fa.FEDAVG)
+                for k in range(D):
+                    ptr, cnt, _ = self.agg.slot(pid, 0, k)
+                    fa.fill_uniform(ptr, cnt, self.in_dt, 0x5EED + 100 * st + j, k)
+        self.w = Setup._weights(D)
+
+    def launch(self, step, stream):
+        base = 10 * (step % self.nsets)
+        self.agg.reduce(base + 1, self.w, stream=stream)  # phase 1
+        p2 = [base + j + 1 for j in range(1, len(self.sizes))]
+        if self.batched:
+            self.agg.reduce_parts(p2, weights=[self.w] * len(p2), stream=stream)
+        else:
+            for pid in p2:
+                self.agg.reduce(pid, self.w, stream=stream)
+
+    def algo_bytes(self):
+        return sum((self.D + 1) * n * self.s for n in self.sizes)
+
+    def input_bytes(self):
+        return sum(self.D * n * self.s for n in self.sizes)
+
+    def close(self):
+        self.agg.close()
+
+
 class SyncSetup(Setup):
     """Compute-node state sync (fa_sync_part): every client slot := the FedAvg of all, in place.
     Algorithmic bytes per launch = D*n*s read + D*n*s written."""
@@ -535,6 +588,22 @@ def single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier):
                      "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                      "input_sets_rotated": s.nsets}
         s.close()
+
+    # the buckets of one aggregator round as it forms them: per-round device time and roofline fraction,
+    # phase 2 batched (fa_reduce_parts) and, for comparison, one launch per part
+    for name in sorted(ROUNDS):
+        for batched in (True, False):
+            s = RoundSetup(fa, torch, name, device, batched=batched)
+            torch.cuda.synchronize()
+            w2, km = timed_loop(torch, s, max(10, args.steps), 3, stream, dist, barrier)
+            ka = statistics.mean(km)
+            sec[name + ("" if batched else "_unbatched")] = {
+                "description": "one aggregator round: " + s.desc + ", buckets " + "/".join(map(str, s.sizes)) +
+                               (" (phase 2 batched: fa_reduce_parts)" if batched else " (one launch per part)"),
+                "round_ms_avg": round(ka, 4), "algorithmic_bytes_per_round": s.algo_bytes(),
+                "achieved_GBs": round(s.algo_bytes() / (ka * 1e-3) / 1e9, 1),
+                "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "input_sets_rotated": s.nsets}
+            s.close()
 
     def one(key, s, desc):
         torch.cuda.synchronize()

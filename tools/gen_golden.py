@@ -40,8 +40,8 @@ WSEED = 7
 CONFIGS = [
     ("lenet5_c1", (2, 0, 6, 1, 10), 2, -1),       # C1: LeNet-5, 2 data owners
     ("resnet18_c2", (1, 1, 9, 3, 10), 8, -1),     # C2: ResNet-18 split "3,8", 8 owners
-    ("resnet101_c3", (1, 4, 20, 10, 10), 4, 0),   # C3 layout (split "10,19"); D=4 pins the chain
-    ("vgg19_c4", (0, 6, 20, 3, 10), 3, 0),        # C4 layout (split "3,19"); D=3 pins the chain
+    ("resnet101_c3", (1, 4, 20, 10, 10), 32, 0),  # C3: ResNet-101 split "10,19", 32 data owners
+    ("vgg19_c4", (0, 6, 20, 3, 10), 64, 0),       # C4: VGG-19 split "3,19", 64 data owners
 ]
 
 
@@ -72,7 +72,10 @@ def main():
     if not os.path.exists(HARNESS):
         sys.exit("build oracle/_ref first: make -f oracle/Makefile.ref")
     os.makedirs(os.path.join(GOLD, "layouts"), exist_ok=True)
+    only = set(sys.argv[1:])  # optional: regenerate only the named configs
     for name, spec, D, blob_mp in CONFIGS:
+        if only and name not in only:
+            continue
         layout = run(["layout", *spec])
         layout["spec"] = dict(zip(["model_name", "model_type", "start", "end", "num_classes"], spec))
         with open(os.path.join(GOLD, "layouts", name + ".json"), "w") as f:

@@ -114,6 +114,12 @@ for s in $STEPS; do
         rc=$?; cat "$OUT/slices.jsonl"; tail -2 "$OUT/slices.err"; ok_or_fail $rc slices
         FA_PHASED_MIN_VECS=0 timeout -k 10 300 python tools/strong_slices.py 20 > "$OUT/slices_phased.jsonl" 2>> "$OUT/slices.err"
         rc=$?; cat "$OUT/slices_phased.jsonl"; ok_or_fail $rc slices_phased ;;
+    rounds)  # one aggregator round on its own buckets, batched vs per part (tools/rounds.py) + kernel trace
+        timeout -k 10 300 python tools/rounds.py 20 round_c2,round_c3,round_c4 > "$OUT/rounds.jsonl" 2> "$OUT/rounds.err"
+        rc=$?; cat "$OUT/rounds.jsonl"; tail -2 "$OUT/rounds.err"; ok_or_fail $rc rounds
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/rounds_prof" -o run -- \
+            python3 tools/rounds.py 20 round_c2,round_c3 > "$OUT/rounds_prof.jsonl" 2> "$OUT/rounds_prof.err"
+        rc=$?; tail -2 "$OUT/rounds_prof.err"; ok_or_fail $rc rounds_prof ;;
     e2e)
         timeout -k 10 900 python tools/e2e_bench.py 4 3 > "$OUT/e2e_bench.json" 2> "$OUT/e2e_bench.err"
         rc=$?; cat "$OUT/e2e_bench.json"; tail -3 "$OUT/e2e_bench.err"; ok_or_fail $rc e2e ;;
