@@ -77,35 +77,49 @@ def cpu_threads():
 
 
 def cpu_baseline(D, sample_elems, reps):
-    """libtorch CPU FedAvg (acc.add_(x_k, w_k) in client order) on a bounded sample of the workload.
+    """CPU baselines on the GPU box's host cores, before the GPU is initialised (child processes).
 
-    Preferred: oracle/_ref/ref_harness (built from the reference's sources, linked with libtorch, the
-    library the reference's arithmetic runs in) -> kind "reference".  Fallback: the C oracle -> "port".
-    Run BEFORE the GPU is initialised: the baseline is a child process.
+    oracle/_ref/ref_harness is built from the reference's own sources (model builders, State) linked with
+    libtorch, the library the reference's arithmetic runs in -> kind "reference".  value = the FedAvg
+    metric restated in that library: acc.add_(x_k, w_k) in client order over a bounded sample of the
+    workload (the reference itself never computes FedAvg), all cores and one core.  Beside
+    it, the reference's own receive loop (aggregator.cpp:59-93: torch::load of each receipt into the
+    global module + (p+p)/1000 + copy_) on C2's largest bucket, with and without the torch::load decode.
+    Fallback without the harness: the C oracle ("port").
     """
     threads = cpu_threads()
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
     sample = "D=%d clients x %d fp32 elements (%.0f MiB per client), %d timed reps after 1 warm-up" % (
         D, sample_elems, sample_elems * 4 / 2**20, reps)
+
+    def run(args, timeout=600):
+        out = subprocess.run([harness] + [str(a) for a in args], capture_output=True, text=True, timeout=timeout,
+                             check=True).stdout
+        return json.loads(out.strip().splitlines()[-1])
     if os.access(harness, os.X_OK):
         try:
-            out = subprocess.run([harness, "bench-fedavg", str(sample_elems), str(D), str(threads), str(reps)],
-                                 capture_output=True, text=True, timeout=600, check=True).stdout
-            r = json.loads(out.strip().splitlines()[-1])
+            r = run(["bench-fedavg", sample_elems, D, threads, reps])
             res = {"value": round(r["gib_s"], 3), "unit": "GiB/s", "cores": threads, "kind": "reference",
-                   "sample": sample + "; libtorch at::set_num_threads(%d)" % threads}
-            # the reference aggregator's own receive loop (aggregator.cpp:59-93: torch::load of each receipt
-            # into the global module + (p+p)/1000 + copy_), on C2's largest bucket, 8 receipts
+                   "path": "restatement in the reference's library: libtorch acc.add_(x_k, w_k) chain, "
+                           "at::set_num_threads(%d)" % threads,
+                   "sample": sample}
+            extra = {}
             try:
-                out = subprocess.run([harness, "bench-literal", "1", "1", "9", "3", "10", "8", str(threads), "2"],
-                                     capture_output=True, text=True, timeout=300, check=True).stdout
-                lit = json.loads(out.strip().splitlines()[-1])
-                res["reference_receive_loop"] = {
-                    "value": round(lit["gib_s"], 3), "unit": "GiB/s of parameters received",
-                    "sample": "ResNet-18 (C2) model_part 2 (%d fp32 params), 8 receipts: torch::load + (p+p)/1000 "
-                              "+ copy_ per receipt, %d threads" % (lit["numel"], threads)}
-            except Exception as e:  # noqa: BLE001 -- optional second figure
-                print("cpu baseline: reference receive loop not timed (%s)" % e, file=sys.stderr)
+                r1 = run(["bench-fedavg", sample_elems, D, 1, max(2, reps // 4)])
+                extra["fedavg_1_core"] = {"value": round(r1["gib_s"], 3), "unit": "GiB/s", "cores": 1}
+                for t in (threads, 1):
+                    for mode in ("", "arith"):
+                        lit = run(["bench-literal", 1, 1, 9, 3, 10, 8, t, 2] + ([mode] if mode else []), timeout=300)
+                        key = "reference_receive_loop" + ("_arith_only" if mode else "") + ("_1_core" if t == 1 else "")
+                        extra[key] = {
+                            "value": round(lit["gib_s"], 3), "unit": "GiB/s of parameters received", "cores": t,
+                            "path": "the reference's receive loop (aggregator.cpp:59-93): " +
+                                    ("(p+p)/1000 + copy_ on receipts decoded before the clock"
+                                     if mode else "torch::load of each receipt + (p+p)/1000 + copy_"),
+                            "sample": "ResNet-18 (C2) model_part 2 (%d fp32 params), 8 receipts" % lit["numel"]}
+            except Exception as e:  # noqa: BLE001 -- optional figures
+                print("cpu baseline: variant not timed (%s)" % e, file=sys.stderr)
+            res.update(extra)
             return res
         except Exception as e:  # noqa: BLE001 -- fall through to the port
             print("cpu baseline: ref_harness failed (%s), timing the oracle port" % e, file=sys.stderr)

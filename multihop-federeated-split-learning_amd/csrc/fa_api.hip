@@ -217,6 +217,7 @@ struct GpuRes {
     fa::SegDesc* seg_host = nullptr;  // pinned segment table of the batched launch
     fa::SegDesc* seg_dev = nullptr;
     hipEvent_t seg_ev = nullptr;      // the table's last upload (the host copy is rewritten after it)
+    size_t seg_uploaded = 0;          // bytes of the table seg_dev holds (== seg_host's first bytes)
     std::unique_ptr<CopyPool> pool;
     ncclComm_t nccl = nullptr;
 };
@@ -892,41 +893,79 @@ int reduce_parts_impl(fa_ctx* ctx, int n_parts, const int* ids, const float* con
     for (auto& kv : groups) {
         const fa_dtype in = (fa_dtype)kv.first.first, out = (fa_dtype)kv.first.second;
         const auto& members = kv.second;
+        const size_t V = 16 / dsize(in);
         for (size_t m0 = 0; m0 < members.size(); m0 += kMaxSegments) {
             const size_t m1 = std::min(members.size(), m0 + kMaxSegments);
             for (int g = 0; g < ctx->G; ++g) {
                 GpuRes& r = ctx->gpu[(size_t)g];
                 DeviceGuard dg(r.dev);
                 hipStream_t st = s ? s : r.compute;
-                FA_HIP(hipEventSynchronize(r.seg_ev));  // the previous upload has read the host table
-                int64_t blocks = 0;
-                int nseg = 0, max_nc = 0;
-                const size_t V = 16 / dsize(in);
-                for (size_t m = m0; m < m1; ++m) {
-                    Part& p = *ps[(size_t)members[m]];
-                    const float* w = weights && weights[members[m]] ? weights[members[m]] : p.w.data();
-                    const size_t n = p.cnt[(size_t)g];
-                    if (n == 0) continue;
-                    fa::SegDesc& sd = r.seg_host[nseg++];
-                    sd.nvec = (int64_t)(n / V);
-                    sd.n = (int64_t)n;
-                    sd.nblk = std::max<int64_t>(1, (sd.nvec + tu.block - 1) / tu.block);
-                    sd.blk0 = blocks;
-                    blocks += sd.nblk;
-                    sd.out = p.dout[(size_t)g];
-                    sd.nc = p.D;
-                    for (int k = 0; k < p.D; ++k) {
-                        sd.src[k] = slot_ptr(p, g, k);
-                        sd.w[k] = w[k];
-                    }
-                    max_nc = std::max(max_nc, p.D);
-                }
                 int rc = wait_copies(ctx, g, st);
                 if (rc) return rc;
-                if (nseg > 0) {
-                    FA_HIP(hipMemcpyAsync(r.seg_dev, r.seg_host, sizeof(fa::SegDesc) * (size_t)nseg,
-                                          hipMemcpyHostToDevice, st));
-                    FA_HIP(hipEventRecord(r.seg_ev, st));
+                // the buckets of this GPU: their ranges, clients and weights
+                int nseg = 0, max_nc = 0, clients = 0;
+                for (size_t m = m0; m < m1; ++m) {
+                    Part& p = *ps[(size_t)members[m]];
+                    if (p.cnt[(size_t)g] == 0) continue;
+                    ++nseg;
+                    clients += p.D;
+                    max_nc = std::max(max_nc, p.D);
+                }
+                auto each = [&](const std::function<void(Part&, const float*, size_t)>& fn) {
+                    for (size_t m = m0; m < m1; ++m) {
+                        Part& p = *ps[(size_t)members[m]];
+                        if (p.cnt[(size_t)g] == 0) continue;
+                        fn(p, weights && weights[members[m]] ? weights[members[m]] : p.w.data(), p.cnt[(size_t)g]);
+                    }
+                };
+                if (nseg > 0 && nseg <= fa::kSegArgMax && clients <= fa::kSegArgClients) {
+                    fa::SegArgs a{};  // the whole table in the kernel arguments
+                    int i = 0, c = 0;
+                    int64_t blocks = 0;
+                    each([&](Part& p, const float* w, size_t n) {
+                        a.nc[i] = p.D;
+                        a.src0[i] = c;
+                        a.blk0[i] = blocks;
+                        a.nvec[i] = (int64_t)(n / V);
+                        a.n[i] = (int64_t)n;
+                        a.out[i] = p.dout[(size_t)g];
+                        blocks += std::max<int64_t>(1, (a.nvec[i] + tu.block - 1) / tu.block);
+                        for (int k = 0; k < p.D; ++k, ++c) {
+                            a.src[c] = slot_ptr(p, g, k);
+                            a.w[c] = w[k];
+                        }
+                        ++i;
+                    });
+                    a.nseg = i;
+                    a.blk0[i] = blocks;
+                    FA_HIP(fa::launch_segargs(a, in, out, max_nc, tu, st));
+                } else if (nseg > 0) {  // a device table, uploaded only when it changed since the last batch
+                    std::vector<fa::SegDesc> tab((size_t)nseg);
+                    int i = 0;
+                    int64_t blocks = 0;
+                    each([&](Part& p, const float* w, size_t n) {
+                        fa::SegDesc& sd = tab[(size_t)i++];
+                        std::memset(&sd, 0, sizeof sd);
+                        sd.nvec = (int64_t)(n / V);
+                        sd.n = (int64_t)n;
+                        sd.nblk = std::max<int64_t>(1, (sd.nvec + tu.block - 1) / tu.block);
+                        sd.blk0 = blocks;
+                        blocks += sd.nblk;
+                        sd.out = p.dout[(size_t)g];
+                        sd.nc = p.D;
+                        for (int k = 0; k < p.D; ++k) {
+                            sd.src[k] = slot_ptr(p, g, k);
+                            sd.w[k] = w[k];
+                        }
+                    });
+                    const size_t bytes = sizeof(fa::SegDesc) * (size_t)nseg;
+                    if (r.seg_uploaded != bytes || std::memcmp(r.seg_host, tab.data(), bytes) != 0) {
+                        FA_HIP(hipEventSynchronize(r.seg_ev));  // the previous upload has read the host table
+                        std::memcpy(r.seg_host, tab.data(), bytes);
+                        FA_HIP(hipMemcpyAsync(r.seg_dev, r.seg_host, bytes, hipMemcpyHostToDevice, st));
+                        FA_HIP(hipEventRecord(r.seg_ev, st));
+                        r.seg_uploaded = bytes;
+                    }
                     FA_HIP(fa::launch_segments(r.seg_dev, nseg, blocks, in, out, max_nc, tu, st));
                 }
                 for (size_t m = m0; m < m1; ++m)

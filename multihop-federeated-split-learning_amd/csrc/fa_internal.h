@@ -27,6 +27,18 @@ struct SegDesc {
     float w[kMaxClients];
 };
 
+// A small batch in the kernel arguments: segment s = workgroups [blk0[s], blk0[s+1]), its clients are
+// src/w[src0[s], src0[s] + nc[s]).
+constexpr int kSegArgMax = 8, kSegArgClients = 192;
+struct SegArgs {
+    int nseg;
+    int nc[kSegArgMax], src0[kSegArgMax];
+    int64_t blk0[kSegArgMax + 1], nvec[kSegArgMax], n[kSegArgMax];
+    void* out[kSegArgMax];
+    const void* src[kSegArgClients];
+    float w[kSegArgClients];
+};
+
 struct Tuning {
     int block;       // threads per workgroup: 64, 128 or 256
     int max_blocks;  // grid cap (grid-stride beyond it), <= 0: uncapped
@@ -53,6 +65,8 @@ hipError_t launch_broadcast(const ClientTable& t, int nc, fa_dtype dt, const flo
 // One launch over nseg buckets (FedAvg, no init, every pointer 16-byte aligned); blocks = sum of nblk.
 hipError_t launch_segments(const SegDesc* d_segs, int nseg, int64_t blocks, fa_dtype in, fa_dtype out, int max_nc,
                            const Tuning& tu, hipStream_t s);
+// The same with the table in the kernel arguments (a.nseg <= kSegArgMax, sum of nc <= kSegArgClients).
+hipError_t launch_segargs(const SegArgs& a, fa_dtype in, fa_dtype out, int max_nc, const Tuning& tu, hipStream_t s);
 // Whether launch_chain takes the phased kernel for a bucket of nvec vectors and nc clients.
 bool phased_takes(fa_dtype in, int64_t nvec, int nc, const Tuning& tu);
 hipError_t launch_fill(void* dst, int64_t n, fa_dtype dt, uint64_t seed, uint32_t client, uint64_t idx0,

@@ -150,8 +150,8 @@ __device__ __forceinline__ void chain_scalar_edges(const ClientTable& t, int nc,
 // loop that the compiler emits as load / wait / fma per client -- one HBM round trip per client, which
 // a bucket with D < U (e.g. C2, D = 8 under U = 16) would otherwise pay for every vector.  G = 8 keeps
 // the f32 kernel at 64 VGPRs (8 waves per SIMD); a 15-wide group would take 72.
-template <typename IN, int U, bool LNT, int V>
-__device__ __forceinline__ void chain_tail(const ClientTable& t, int k, int r, int64_t e, float* acc) {
+template <typename IN, int U, bool LNT, int V, class Tab = ClientTable>
+__device__ __forceinline__ void chain_tail(const Tab& t, int k, int r, int64_t e, float* acc) {
     constexpr int G = U < 8 ? U : 8;
     for (; r > 0; k += G, r -= G) {
         u32x4 raw[G];
@@ -173,8 +173,10 @@ __device__ __forceinline__ void chain_tail(const ClientTable& t, int k, int r, i
 
 // The ordered chain for the V elements of every client bucket starting at element e: groups of U
 // loads in flight before their FMAs, then the grouped tail.  acc starts at +0 or at init[e..].
-template <typename IN, int U, bool LNT, bool INIT>
-__device__ __forceinline__ void chain_vec(const ClientTable& t, int nc, const float* init, int64_t e, float* acc) {
+// Tab: anything with t.src[k] / t.w[k] (the kernarg ClientTable, or a SegView into a batched launch's
+// kernel arguments).
+template <typename IN, int U, bool LNT, bool INIT, class Tab = ClientTable>
+__device__ __forceinline__ void chain_vec(const Tab& t, int nc, const float* init, int64_t e, float* acc) {
     constexpr int V = In<IN>::kVec;
     if constexpr (INIT) {
 #pragma unroll
@@ -201,7 +203,7 @@ __device__ __forceinline__ void chain_vec(const ClientTable& t, int nc, const fl
             for (int j = 0; j < V; ++j) acc[j] = __builtin_fmaf(x[j], w, acc[j]);
         }
     }
-    chain_tail<IN, U, LNT, V>(t, k, nc - k, e, acc);
+    chain_tail<IN, U, LNT, V, Tab>(t, k, nc - k, e, acc);
 }
 
 // Vector body over nvec lane-vectors starting at element `head`; lane-vector v
@@ -585,6 +587,37 @@ __global__ __launch_bounds__(256) void fedavg_segments_kernel(const SegDesc* __r
             float acc = 0.0f;
             for (int k = 0; k < nc; ++k) acc = __builtin_fmaf(In<IN>::scalar(t.src[k], i), t.w[k], acc);
             Out<OUT>::scalar(sd->out, i, acc);
+        }
+    }
+}
+
+// The same over a small batch whose whole table travels in the kernel arguments (SegArgs: up to
+// kSegArgMax buckets and kSegArgClients client pointers): no table upload before the launch (a 4 us
+// blit on the stream, gpurun_out r02s07) and no dependent load of the table inside the kernel.
+struct SegView {
+    const void* const* src;
+    const float* w;
+};
+
+template <typename IN, typename OUT, int U>
+__global__ __launch_bounds__(256) void fedavg_segargs_kernel(const SegArgs a) {
+    constexpr int V = In<IN>::kVec;
+    int s = 0;
+    while (s + 1 < a.nseg && a.blk0[s + 1] <= (int64_t)blockIdx.x) ++s;
+    const SegView t{&a.src[a.src0[s]], &a.w[a.src0[s]]};
+    const int nc = a.nc[s];
+    const int64_t b = (int64_t)blockIdx.x - a.blk0[s], nvec = a.nvec[s];
+    const int64_t v = b * blockDim.x + threadIdx.x;
+    if (v < nvec) {
+        float acc[V];
+        chain_vec<IN, U, true, false, SegView>(t, nc, nullptr, v * V, acc);
+        Out<OUT>::template store<V, kStSc1>(a.out[s], v * V, acc);
+    }
+    if (b == a.blk0[s + 1] - a.blk0[s] - 1) {
+        for (int64_t i = nvec * V + threadIdx.x; i < a.n[s]; i += blockDim.x) {
+            float acc = 0.0f;
+            for (int k = 0; k < nc; ++k) acc = __builtin_fmaf(In<IN>::scalar(t.src[k], i), t.w[k], acc);
+            Out<OUT>::scalar(a.out[s], i, acc);
         }
     }
 }
@@ -973,6 +1006,24 @@ hipError_t launch_segments_t(const SegDesc* d_segs, int nseg, int64_t blocks, in
     return hipGetLastError();
 }
 }  // namespace
+
+namespace {
+template <typename IN, typename OUT>
+hipError_t launch_segargs_t(const SegArgs& a, int max_nc, int block, hipStream_t s) {
+    const unsigned blocks = (unsigned)a.blk0[a.nseg];
+    if (max_nc <= 8) hipLaunchKernelGGL((fedavg_segargs_kernel<IN, OUT, 8>), dim3(blocks), dim3(block), 0, s, a);
+    else hipLaunchKernelGGL((fedavg_segargs_kernel<IN, OUT, 16>), dim3(blocks), dim3(block), 0, s, a);
+    return hipGetLastError();
+}
+}  // namespace
+
+hipError_t launch_segargs(const SegArgs& a, fa_dtype in, fa_dtype outdt, int max_nc, const Tuning& tu, hipStream_t s) {
+    if (a.nseg <= 0) return hipSuccess;
+    if (in == FA_F32 && outdt == FA_F32) return launch_segargs_t<float, float>(a, max_nc, tu.block, s);
+    if (in == FA_F32 && outdt == FA_BF16) return launch_segargs_t<float, uint16_t>(a, max_nc, tu.block, s);
+    if (in == FA_BF16 && outdt == FA_F32) return launch_segargs_t<uint16_t, float>(a, max_nc, tu.block, s);
+    return launch_segargs_t<uint16_t, uint16_t>(a, max_nc, tu.block, s);
+}
 
 hipError_t launch_segments(const SegDesc* d_segs, int nseg, int64_t blocks, fa_dtype in, fa_dtype outdt, int max_nc,
                            const Tuning& tu, hipStream_t s) {

@@ -19,7 +19,7 @@
 //   layout  <name> <type> <start> <end> <nc>
 //   golden  <name> <type> <start> <end> <nc> <D> <seed> <wseed> <outdir> [blob_mp; -1 = every bucket <= 200k]
 //   bench-fedavg <n> <D> <threads> <reps>
-//   bench-literal <name> <type> <start> <end> <nc> <D> <threads> <model_part>
+//   bench-literal <name> <type> <start> <end> <nc> <D> <threads> <model_part> [arith]
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -264,25 +264,40 @@ int cmd_bench_fedavg(char** argv) {
     return 0;
 }
 
-// The reference-literal receive loop (torch::load + (p+p)/1000 + copy_) timed per receipt.
-int cmd_bench_literal(char** argv) {
+// The reference-literal receive loop (torch::load + (p+p)/1000 + copy_) timed per receipt; with
+// `arith` the receipts are decoded before the clock starts and only the arithmetic of aggregator.cpp:72-88
+// is timed (p <- div(x + x, 1000), copy_ into the global part, per named parameter).
+int cmd_bench_literal(int argc, char** argv) {
     int name = atoi(argv[2]), type = atoi(argv[3]), start = atoi(argv[4]), end = atoi(argv[5]), nc = atoi(argv[6]);
     int D = atoi(argv[7]), threads = atoi(argv[8]), model_part = atoi(argv[9]);
+    const bool arith = argc > 10 && std::string(argv[10]) == "arith";
     at::set_num_threads(threads);
     AggState agg = build_state(name, type, start, end, nc);
     Bucket b = buckets_of(agg)[model_part - 1];
     std::vector<std::string> blobs;
+    std::vector<torch::nn::Sequential> decoded;
     for (int k = 0; k < D; ++k) {
         auto cm = client_module(name, type, start, end, nc, model_part);
         fill_client(cm, bucket_seed(0x5EED, model_part), k);
-        blobs.push_back(save_blob(cm));
+        if (arith) decoded.push_back(cm);
+        else blobs.push_back(save_blob(cm));
     }
     double t0 = now_s();
-    for (int k = 0; k < D; ++k) literal_receipt(b, blobs[k], 1000);
+    if (arith) {
+        torch::NoGradGuard ng;
+        auto g = b.global->named_parameters(true);
+        for (int k = 0; k < D; ++k) {
+            auto x = decoded[(size_t)k]->named_parameters(true);
+            for (size_t j = 0; j < g.size(); ++j) g[j].value().copy_(torch::div(x[j].value() + x[j].value(), 1000));
+        }
+    } else {
+        for (int k = 0; k < D; ++k) literal_receipt(b, blobs[k], 1000);
+    }
     double dt = now_s() - t0;
     double bytes = (double)D * param_numel(b.global) * 4;
-    printf("{\"mode\":\"literal\",\"model_part\":%d,\"numel\":%lld,\"D\":%d,\"threads\":%d,\"s\":%.6f,\"gib_s\":%.4f}\n",
-           model_part, (long long)param_numel(b.global), D, threads, dt, bytes / dt / (1ull << 30));
+    printf("{\"mode\":\"%s\",\"model_part\":%d,\"numel\":%lld,\"D\":%d,\"threads\":%d,\"s\":%.6f,\"gib_s\":%.4f}\n",
+           arith ? "literal-arith" : "literal", model_part, (long long)param_numel(b.global), D, threads, dt,
+           bytes / dt / (1ull << 30));
     return 0;
 }
 
@@ -308,7 +323,7 @@ int main(int argc, char** argv) {
     } else if (mode == "bench-fedavg" && argc >= 6) {
         rc = cmd_bench_fedavg(argv);
     } else if (mode == "bench-literal" && argc >= 10) {
-        rc = cmd_bench_literal(argv);
+        rc = cmd_bench_literal(argc, argv);
     } else {
         fprintf(stderr, "bad arguments\n");
     }

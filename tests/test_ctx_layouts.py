@@ -226,3 +226,39 @@ def test_sync_part_waits_for_submits(fa, O, torch_gpu):
         for k in (0, D - 1):
             ptr, cnt, _ = agg.slot(1, 0, k)
             assert_bits(d2h(ptr, cnt), ref)
+
+
+def test_reduce_parts_device_table_and_reuse(fa, O, torch_gpu):
+    """A batch beyond the kernel-argument table (more than 8 buckets, or more than 192 clients) goes
+    through a device-side segment table, uploaded only when it changed: the same batch twice (no
+    upload), then new weights (upload), every time bit-exact."""
+    torch = torch_gpu
+    sizes = [1, 4, 63, 64, 65, 1000, 4099, 77_777, 5, 300_001, 12]
+    D = 6
+    with fa.Aggregator(1) as agg:
+        xs = {}
+        for pid, n in enumerate(sizes, start=1):
+            agg.define(pid, n, fa.F32, fa.F32, D, fa.FEDAVG)
+            xs[pid] = host_clients(O, 200 + pid, D, n)
+            for k in range(D):
+                ptr, cnt, _ = agg.slot(pid, 0, k)
+                fa.fill_uniform(ptr, cnt, fa.F32, 200 + pid, k)
+        torch.cuda.synchronize()
+        ids = list(range(1, len(sizes) + 1))
+        for w in (O.weights(D), O.weights(D), O.weights(D, seed=99)):
+            agg.reduce_parts(ids, weights=[w] * len(ids))
+            for pid in ids:
+                assert_bits(agg.copy_output(pid), O.fedavg(xs[pid], w))
+        # many clients: 2 buckets x 130 clients (> 192 in the kernel arguments, and > 128 per bucket: those
+        # take their own multi-pass launch) and 2 x 100 (device table)
+        for pid, (n, d) in {20: (5000, 130), 21: (777, 100), 22: (4096, 100)}.items():
+            agg.define(pid, n, fa.F32, fa.F32, d, fa.FEDAVG)
+            xs[pid] = host_clients(O, 300 + pid, d, n)
+            for k in range(d):
+                ptr, cnt, _ = agg.slot(pid, 0, k)
+                fa.fill_uniform(ptr, cnt, fa.F32, 300 + pid, k)
+        torch.cuda.synchronize()
+        ws = {pid: O.weights(len(xs[pid])) for pid in (20, 21, 22)}
+        agg.reduce_parts([20, 21, 22], weights=[ws[20], ws[21], ws[22]])
+        for pid in (20, 21, 22):
+            assert_bits(agg.copy_output(pid), O.fedavg(xs[pid], ws[pid]))
