@@ -482,7 +482,9 @@ def main():
     torch.cuda.synchronize()
 
     # the dominant kernel alone (roofline), HIP events on its stream
+    timeouts0 = fa.phased_timeouts(device)
     wall_k, kern_ms = timed_loop(torch, setup, args.steps, args.warmup, stream, dist, barrier)
+    timeouts = fa.phased_timeouts(device) - timeouts0  # > 0: the persistent grid was not co-resident
     if args.layout == "range":
         wall = wall_k
     else:
@@ -519,7 +521,8 @@ def main():
                      "kernel_ms_avg": round(kavg, 4), "kernel_ms_min": round(min(kern_ms), 4),
                      "kernel_ms_median": round(statistics.median(kern_ms), 4),
                      "kernel": "rank %d's launch (%s)" % (rank, "its range of every bucket" if args.layout == "range"
-                                                         else "its clients' local reduction")},
+                                                         else "its clients' local reduction"),
+                     "phased_meeting_timeouts": timeouts},
         "cpu_baseline": cpu,
     }
     if world > 1:

@@ -191,6 +191,12 @@ int fa_sync_device(fa_ctx* ctx, int gpu, void* const* d_clients, const float* h_
                    void* hip_stream);
 int fa_sync_part(fa_ctx* ctx, int part_id, const float* h_weights, void* hip_stream);
 
+/* Phased-kernel meetings on HIP device `device` that stopped waiting for the rest of the grid since the
+ * process started (each counts one workgroup's bounded wait running out).  Non-zero means the persistent
+ * grid was not co-resident -- the GPU was shared with other kernels -- and those launches ran slower;
+ * results are unaffected.  Synchronizes with the device. */
+int fa_phased_timeouts(int device, uint64_t* count);
+
 /* Literal mode divisor used by fa_reduce_device when ctx == NULL. */
 #define FA_DEFAULT_DIVISOR 1000.0f
 

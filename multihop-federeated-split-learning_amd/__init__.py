@@ -83,6 +83,7 @@ def lib():
         "fa_ctx_set_tuning": (I, [P, ctypes.POINTER(_Tuning)]),
         "fa_ctx_get_tuning": (I, [P, ctypes.POINTER(_Tuning)]),
         "fa_rs_segments": (I, [S, I, I, I, ctypes.POINTER(S), I]),
+        "fa_phased_timeouts": (I, [I, ctypes.POINTER(U64)]),
         "fa_reduce_device": (I, [P, I, P, P, I, S, I, P, I, I, P, P]),
         "fa_fill_uniform": (I, [P, S, I, U64, U32, U64, P]),
         "fa_set_tuning": (I, [ctypes.POINTER(_Tuning)]),
@@ -181,6 +182,14 @@ def set_tuning(block=0, max_blocks=0, unroll=0, load_policy=0, store_policy=0, s
     slot_skew -1 = none."""
     t = _Tuning(block, max_blocks, unroll, load_policy, store_policy, slot_skew, walk, rs_chunks)
     check(lib().fa_set_tuning(ctypes.byref(t)))
+
+
+def phased_timeouts(device=0):
+    """fa_phased_timeouts: phased-kernel meetings on `device` whose bounded wait ran out (grid not
+    co-resident) since the process started."""
+    c = ctypes.c_uint64()
+    check(lib().fa_phased_timeouts(device, ctypes.byref(c)))
+    return c.value
 
 
 def rs_segments(n, n_gpus, chunks, gpu):

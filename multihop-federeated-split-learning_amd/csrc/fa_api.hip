@@ -414,9 +414,9 @@ std::vector<std::pair<size_t, size_t>> rs_pieces(size_t npad, int G, int chunks)
 
 // HBM placement of a bucket's slots.  Client buckets that start at the same address modulo a large
 // power of two put the U simultaneous loads of a wave (and its store) on the same HBM channels; a small
-// per-slot skew spreads them.  Measured on MI355X (profiles/r01_summary.json, tools/exp_layout.py):
+// per-slot skew spreads them.  Measured on MI355X (round 1, profiles/r01_summary.json):
 // 256-512 B skew -> 1.30-1.32 ms for 32 x 256 MiB vs 1.47-1.51 ms unskewed; re-laid out inside the
-// same six pools (tools/exp_skew.hip), 2048 B beat 512 B in every one (by 0.6-2.9%); 8 KiB + 512 and
+// same six pools (round 1), 2048 B beat 512 B in every one (by 0.6-2.9%); 8 KiB + 512 and
 // 2 MiB + 512 are 7-12% slower.  Slots stay 16-byte aligned.
 size_t slot_stride(size_t bytes, size_t skew) { return (bytes + 4095) / 4096 * 4096 + skew; }
 
@@ -1501,6 +1501,13 @@ int fa_sync_part(fa_ctx* ctx, int part_id, const float* h_weights, void* hip_str
         if ((rc = wait_copies(ctx, g, st))) return rc;  // the slots' submits land first
         if ((rc = sync_on(ctx, g, ctx->tuning.tu, ptrs.data(), w, p->D, p->cnt[(size_t)g], p->in, st))) return rc;
     }
+    return FA_OK;
+}
+
+int fa_phased_timeouts(int device, uint64_t* count) {
+    g_err.clear();
+    if (!count) return fail(FA_ERR_ARG, "count is null");
+    FA_HIP(fa::phased_timeouts(device, count));
     return FA_OK;
 }
 

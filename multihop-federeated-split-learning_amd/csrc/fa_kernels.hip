@@ -26,6 +26,7 @@
 #include <cstdlib>
 #include <mutex>
 #include <type_traits>
+#include <vector>
 
 #include "fa_internal.h"
 
@@ -242,7 +243,7 @@ __global__ __launch_bounds__(256) void fedavg_chain_kernel(const ClientTable t, 
 // 32 input streams of the north star read at 7.1 TB/s in every HBM pool, and a write-only stream
 // runs at 6.2 TB/s, but interleaved they lose 0.07 ms (fast pools) to 0.2 ms (slow pools) to
 // read/write turnaround -- which of the two a pool gets depends only on where the allocation of the
-// INPUTS lands physically (tools/exp_slow.hip, exp_cross.hip).  Here a persistent grid
+// INPUTS lands physically (round-1 experiments, profiles/r01_summary.json).  Here a persistent grid
 // (one 256-thread workgroup per CU) works in phases: every lane reduces RL vectors into LDS (160 KiB
 // per CU) and RR more into registers, the workgroups meet at a chip-wide counter, then all of them
 // write the phase's results.  With the larger register stage (REGS 192, walk 5) three phases cover
@@ -401,10 +402,12 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
             unsigned* arrive = sync + 4 + (unsigned)((ticket / (unsigned long long)G) % kSyncRing);
             __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const unsigned target = (unsigned)(G * (p + 1) - slack);
-            for (int spins = 0; __hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
-                                spins < (1 << 16);
+            int spins = 0;
+            for (; __hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target && spins < (1 << 16);
                  ++spins)
                 __builtin_amdgcn_s_sleep(1);
+            if (spins == (1 << 16))  // the grid was not co-resident (GPU shared): counted, fa_phased_timeouts
+                __hip_atomic_fetch_add(sync + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
 #pragma unroll 1
@@ -882,6 +885,16 @@ hipError_t launch_chain_t(const ClientTable& t, int nc, const float* init, void*
 }  // namespace
 
 int64_t phased_min_elems(fa_dtype in, const Tuning& tu) { return phased_min_elems_impl(in, tu); }
+
+hipError_t phased_timeouts(int dev, uint64_t* count) {
+    *count = 0;
+    if (dev < 0 || dev >= kMaxDevices || !g_phased[dev].sync) return hipSuccess;  // no phased launch yet
+    std::vector<unsigned> tab((size_t)kSyncStride * kSyncSlots);
+    const hipError_t e = hipMemcpy(tab.data(), g_phased[dev].sync, tab.size() * sizeof(unsigned), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return e;
+    for (int slot = 0; slot < kSyncSlots; ++slot) *count += tab[(size_t)slot * kSyncStride + 2];
+    return hipSuccess;
+}
 
 hipError_t launch_chain(const ClientTable& t, int nc, fa_dtype in, fa_dtype outdt, const float* init, void* out,
                         int64_t head, int64_t nvec, int64_t n, bool vector_ok, const Tuning& tu, hipStream_t s) {

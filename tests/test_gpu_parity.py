@@ -733,6 +733,22 @@ def test_phased_streams_sharing_a_counter(fa, O, torch_gpu):
         fa.set_tuning(walk=before["walk"])
 
 
+def test_phased_meeting_timeouts_counter(fa, O, torch_gpu):
+    """fa_phased_timeouts: on a quiet GPU a phased launch never runs out of its bounded wait (the grid is
+    co-resident), so the counter does not move; the call itself synchronizes and reads the device table."""
+    torch = torch_gpu
+    n, D = int(PHASE_ELEMS * 1.2), 16
+    w = O.weights(D)
+    clients = [filled(fa, torch, n, False, 77, k) for k in range(D)]
+    out = dev_buf(torch, n, False)
+    before = fa.phased_timeouts(0)
+    for _ in range(3):
+        fa.reduce_device(clients, w, n, fa.F32, out, fa.F32)
+    torch.cuda.synchronize()
+    assert fa.phased_timeouts(0) == before
+    assert fa.phased_timeouts(63) == 0  # a device that never ran a phased launch
+
+
 def test_phased_graph_replays(fa, O, torch_gpu):
     """A phased launch captured in a graph and replayed: each replay is one epoch of the counter ring,
     results stay bit-exact, and an eager launch afterwards runs at its usual speed."""

@@ -194,6 +194,7 @@ int main(int argc, char** argv) {
                 frames[p.mp].push_back(std::move(f));
             }
         }
+        std::cerr << "[owners] round " << round << ": frames ready, sending\n";
         const auto t0 = std::chrono::steady_clock::now();
         std::vector<Receipt> replies;
         for (int phase = 1; phase <= 2 && ok; ++phase) {

@@ -9,7 +9,7 @@ reports the data owners' round time and the aggregator's per-phase split.
 Beside it, oracle/_ref/ref_harness times the reference-literal receive loop
 (torch::load + (p+p)/1000 + copy_, aggregator.cpp:63-88) on the VGG FC part.
 
-  python tools/e2e_bench.py [D] [rounds]
+  python tools/e2e_bench.py [D] [rounds] [aggregator args...]   (e.g. --layout rs, --eager)
 """
 import json
 import os
@@ -42,16 +42,32 @@ def vgg_c4_parts(d):
     return sizes
 
 
+def heartbeat(every=20):
+    """A progress line on stderr every `every` s: large rounds (D = 64 VGG owners, 30 GB of receipts per
+    round over loopback) run for minutes with nothing else to print."""
+    import threading
+    t0 = time.time()
+
+    def beat():
+        while True:
+            time.sleep(every)
+            print("e2e_bench: %.0f s" % (time.time() - t0), file=sys.stderr, flush=True)
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main():
+    heartbeat()
     D = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 2
-    out = {"workload": "VGG-19 C4 model parts (split 3,19), %d data owners, loopback TCP" % D}
+    extra = sys.argv[3:]
+    out = {"workload": "VGG-19 C4 model parts (split 3,19), %d data owners, loopback TCP" % D,
+           "aggregator_args": extra}
     with tempfile.TemporaryDirectory() as d:
         sizes = vgg_c4_parts(d)
         out["params_per_part"] = sizes
         base = random.randrange(10000, 32000, 100)  # below the ephemeral port range
         agg = subprocess.Popen([AGG, "-i", "-1", "-d", str(D), "-c", "1", "--rounds", str(rounds), "--port-base",
-                                str(base)], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+                                str(base)] + extra, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
         time.sleep(0.5)
         t0 = time.perf_counter()
         r = subprocess.run([OWNERS, "--blobs", d, "--parts", "1,2,3", "-d", str(D), "-c", "1", "--rounds",
@@ -68,7 +84,7 @@ def main():
         out.update({"ok": owners["ok"], "round_ms_owner_view": owners["round_ms"], "aggregator_phases": phases,
                     "bytes_in_per_round": in_bytes, "wall_s": round(wall, 3),
                     "ingest_GBs_per_round": [round(in_bytes / (ms / 1e3) / 1e9, 2) for ms in owners["round_ms"]]})
-    if os.access(REF, os.X_OK):
+    if os.access(REF, os.X_OK) and not os.environ.get("E2E_NO_REF"):
         threads = str(min(16, len(os.sched_getaffinity(0))))
         lit = subprocess.run([REF, "bench-literal", "0", "6", "20", "3", "10", str(D), threads, "3"],
                              capture_output=True, text=True, timeout=900)

@@ -39,71 +39,22 @@ for s in $STEPS; do
                 python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-secondary > "$OUT/pmc_$c.json" 2> "$OUT/pmc_$c.err"
             rc=$?; tail -2 "$OUT/pmc_$c.err"; ok_or_fail $rc pmc_$c
         done ;;
+    pmcw)  # the same passes for the secondary workloads whose traffic bench.py reports
+        bash tools/pmc_workloads.sh "$TAG" ${PMC_WORKLOADS:-c2 c3 c4 ns_w4 ns_w8}
+        rc=$?; ok_or_fail $rc pmcw ;;
     layouts)
         for L in rs chain; do
             timeout -k 10 300 python bench.py --layout $L --steps 10 --no-cpu-baseline --no-secondary > "$OUT/bench_$L.json" 2> "$OUT/bench_$L.err"
             rc=$?; cat "$OUT/bench_$L.json"; tail -2 "$OUT/bench_$L.err"; ok_or_fail $rc layout_$L
         done ;;
     h2d)
-        timeout -k 10 600 python tools/h2d_rate.py 8 26 3 > "$OUT/h2d.jsonl" 2> "$OUT/h2d.err"
-        rc=$?; cat "$OUT/h2d.jsonl"; tail -2 "$OUT/h2d.err"; ok_or_fail $rc h2d ;;
-    outexp)
-        timeout -k 10 600 python tools/exp_out.py 25 10 > "$OUT/exp_out.jsonl" 2> "$OUT/exp_out.err"
-        rc=$?; cat "$OUT/exp_out.jsonl"; tail -2 "$OUT/exp_out.err"; ok_or_fail $rc outexp ;;
+        for G in 1 2 4; do
+            timeout -k 10 600 python tools/h2d_rate.py 8 26 3 $G >> "$OUT/h2d.jsonl" 2>> "$OUT/h2d.err"
+            rc=$?; tail -1 "$OUT/h2d.jsonl"; tail -2 "$OUT/h2d.err"; ok_or_fail $rc h2d_$G
+        done ;;
     ranks)  # multi-rank rehearsal of the driver's N>1 launch: bench.py spawns 2 ranks, which share the one GPU over gloo
         timeout -k 10 600 python bench.py --gpus 2 --steps 5 --warmup 2 > "$OUT/bench_2ranks.json" 2> "$OUT/bench_2ranks.err"
         rc=$?; cat "$OUT/bench_2ranks.json"; tail -3 "$OUT/bench_2ranks.err"; ok_or_fail $rc ranks ;;
-    vmm)  # physical placement of the client pool via the VMM API (tools/exp_vmm.hip)
-        hipcc --offload-arch=gfx950 -O2 tools/exp_vmm.hip -Iinclude -Lmultihop-federeated-split-learning_amd/lib -lfa \
-            -Wl,-rpath,$PWD/multihop-federeated-split-learning_amd/lib -o "$OUT/exp_vmm" > "$OUT/vmm_build.log" 2>&1 &&
-        timeout -k 10 400 "$OUT/exp_vmm" ${VMM_ARGS:-26 3} > "$OUT/exp_vmm.jsonl" 2> "$OUT/exp_vmm.err"
-        rc=$?; cat "$OUT/exp_vmm.jsonl"; tail -3 "$OUT/exp_vmm.err"; ok_or_fail $rc vmm ;;
-    outplace)  # where the output is written (tools/exp_out.hip)
-        hipcc --offload-arch=gfx950 -O2 tools/exp_out.hip -Iinclude -Lmultihop-federeated-split-learning_amd/lib -lfa \
-            -Wl,-rpath,$PWD/multihop-federeated-split-learning_amd/lib -o "$OUT/exp_out" > "$OUT/out_build.log" 2>&1 &&
-        timeout -k 10 400 "$OUT/exp_out" ${OUT_ARGS:-26 4} > "$OUT/exp_out.jsonl" 2> "$OUT/exp_out.err"
-        rc=$?; cat "$OUT/exp_out.jsonl"; tail -3 "$OUT/exp_out.err"; ok_or_fail $rc outplace ;;
-    pick)  # K pools allocated in sequence, timed interleaved (tools/exp_pick.hip)
-        hipcc --offload-arch=gfx950 -O2 tools/exp_pick.hip -Iinclude -Lmultihop-federeated-split-learning_amd/lib -lfa \
-            -Wl,-rpath,$PWD/multihop-federeated-split-learning_amd/lib -o "$OUT/exp_pick" > "$OUT/pick_build.log" 2>&1 &&
-        timeout -k 10 400 "$OUT/exp_pick" ${PICK_ARGS:-26 8 3} > "$OUT/exp_pick.jsonl" 2> "$OUT/exp_pick.err" &&
-        timeout -k 10 400 "$OUT/exp_pick" ${PICK_ARGS2:-26 4 3 100} >> "$OUT/exp_pick.jsonl" 2>> "$OUT/exp_pick.err"
-        rc=$?; cat "$OUT/exp_pick.jsonl"; tail -3 "$OUT/exp_pick.err"; ok_or_fail $rc pick ;;
-    slow)  # where a slow pool loses its time (tools/exp_slow.hip)
-        hipcc --offload-arch=gfx950 -O2 tools/exp_slow.hip -Iinclude -Lmultihop-federeated-split-learning_amd/lib -lfa \
-            -Wl,-rpath,$PWD/multihop-federeated-split-learning_amd/lib -o "$OUT/exp_slow" > "$OUT/slow_build.log" 2>&1 &&
-        timeout -k 10 400 "$OUT/exp_slow" ${SLOW_ARGS:-26 6 3} > "$OUT/exp_slow.jsonl" 2> "$OUT/exp_slow.err"
-        rc=$?; cat "$OUT/exp_slow.jsonl"; tail -3 "$OUT/exp_slow.err"; ok_or_fail $rc slow ;;
-    skew)  # per-slot skew inside the same pool (tools/exp_skew.hip)
-        hipcc --offload-arch=gfx950 -O2 tools/exp_skew.hip -Iinclude -Lmultihop-federeated-split-learning_amd/lib -lfa \
-            -Wl,-rpath,$PWD/multihop-federeated-split-learning_amd/lib -o "$OUT/exp_skew" > "$OUT/skew_build.log" 2>&1 &&
-        timeout -k 10 400 "$OUT/exp_skew" ${SKEW_ARGS:-26 6 3} > "$OUT/exp_skew.jsonl" 2> "$OUT/exp_skew.err"
-        rc=$?; cat "$OUT/exp_skew.jsonl"; tail -3 "$OUT/exp_skew.err"; ok_or_fail $rc skew ;;
-    cross)  # inputs of pool p into the output of pool q (tools/exp_cross.hip)
-        hipcc --offload-arch=gfx950 -O2 tools/exp_cross.hip -Iinclude -Lmultihop-federeated-split-learning_amd/lib -lfa \
-            -Wl,-rpath,$PWD/multihop-federeated-split-learning_amd/lib -o "$OUT/exp_cross" > "$OUT/cross_build.log" 2>&1 &&
-        timeout -k 10 400 "$OUT/exp_cross" ${CROSS_ARGS:-26 5 3} > "$OUT/exp_cross.jsonl" 2> "$OUT/exp_cross.err"
-        rc=$?; cat "$OUT/exp_cross.jsonl"; tail -3 "$OUT/exp_cross.err"; ok_or_fail $rc cross ;;
-    order)  # walk order of the grid over the buckets vs the slow-pool penalty (tools/exp_order.hip)
-        hipcc --offload-arch=gfx950 -O2 tools/exp_order.hip -Iinclude -Lmultihop-federeated-split-learning_amd/lib -lfa \
-            -Wl,-rpath,$PWD/multihop-federeated-split-learning_amd/lib -o "$OUT/exp_order" > "$OUT/order_build.log" 2>&1 &&
-        timeout -k 10 400 "$OUT/exp_order" ${ORDER_ARGS:-26 5 3} > "$OUT/exp_order.jsonl" 2> "$OUT/exp_order.err"
-        rc=$?; cat "$OUT/exp_order.jsonl"; tail -3 "$OUT/exp_order.err"; ok_or_fail $rc order ;;
-    phase)  # reads and writes separated in time (tools/exp_phase.hip)
-        hipcc --offload-arch=gfx950 -O2 tools/exp_phase.hip -Iinclude -Lmultihop-federeated-split-learning_amd/lib -lfa \
-            -Wl,-rpath,$PWD/multihop-federeated-split-learning_amd/lib -o "$OUT/exp_phase" > "$OUT/phase_build.log" 2>&1 &&
-        timeout -k 10 300 "$OUT/exp_phase" ${PHASE_ARGS:-26 5 3} > "$OUT/exp_phase.jsonl" 2> "$OUT/exp_phase.err"
-        rc=$?; cat "$OUT/exp_phase.jsonl"; tail -3 "$OUT/exp_phase.err"; ok_or_fail $rc phase ;;
-    phase2)  # variants of the phased kernel (tools/exp_phase2.hip)
-        hipcc --offload-arch=gfx950 -O2 tools/exp_phase2.hip -Iinclude -Lmultihop-federeated-split-learning_amd/lib -lfa \
-            -Wl,-rpath,$PWD/multihop-federeated-split-learning_amd/lib -o "$OUT/exp_phase2" > "$OUT/phase2_build.log" 2>&1 &&
-        timeout -k 10 300 "$OUT/exp_phase2" ${PHASE_ARGS:-26 4 3} > "$OUT/exp_phase2.jsonl" 2> "$OUT/exp_phase2.err"
-        rc=$?; cat "$OUT/exp_phase2.jsonl"; tail -3 "$OUT/exp_phase2.err"; ok_or_fail $rc phase2 ;;
-    phase3)  # register-staged phases and soft barriers (tools/exp_phase3.hip)
-        hipcc --offload-arch=gfx950 -O2 tools/exp_phase3.hip -Iinclude -Lmultihop-federeated-split-learning_amd/lib -lfa \
-            -Wl,-rpath,$PWD/multihop-federeated-split-learning_amd/lib -o "$OUT/exp_phase3" > "$OUT/phase3_build.log" 2>&1 &&
-        timeout -k 10 300 "$OUT/exp_phase3" ${PHASE_ARGS:-26 4 3} > "$OUT/exp_phase3.jsonl" 2> "$OUT/exp_phase3.err"
-        rc=$?; cat "$OUT/exp_phase3.jsonl"; tail -3 "$OUT/exp_phase3.err"; ok_or_fail $rc phase3 ;;
     rslaunch)  # local launch pattern of the rs / chain layouts at 4 and 8 ranks (tools/rs_launch.py)
         for W in 8 4; do
             timeout -k 10 300 python tools/rs_launch.py $W 16 10 >> "$OUT/rs_launch.jsonl" 2>> "$OUT/rs_launch.err"
@@ -123,6 +74,11 @@ for s in $STEPS; do
     e2e)
         timeout -k 10 900 python tools/e2e_bench.py 4 3 > "$OUT/e2e_bench.json" 2> "$OUT/e2e_bench.err"
         rc=$?; cat "$OUT/e2e_bench.json"; tail -3 "$OUT/e2e_bench.err"; ok_or_fail $rc e2e ;;
+    e2e_c4)  # C4's own client count through the drop-in process: D = 64 VGG-19 owners, range / eager / rs layouts
+        for L in "" "--eager" "--layout rs"; do
+            E2E_NO_REF=1 timeout -k 10 600 python tools/e2e_bench.py 64 3 $L >> "$OUT/e2e_c4.jsonl" 2>> "$OUT/e2e_c4.err"
+            rc=$?; tail -c 600 "$OUT/e2e_c4.jsonl"; echo; ok_or_fail $rc "e2e_c4 $L"
+        done ;;
     probe)
         hipcc --offload-arch=gfx950 -O3 tools/hbm_probe.hip -o "$OUT/hbm_probe" > "$OUT/probe_build.log" 2>&1 &&
         timeout -k 10 300 "$OUT/hbm_probe" > "$OUT/hbm_probe.json" 2> "$OUT/probe.err"
@@ -149,33 +105,6 @@ for s in $STEPS; do
             timeout -k 10 300 python bench.py --no-cpu-baseline --no-secondary > "$OUT/bench3_$i.json" 2> "$OUT/bench3_$i.err"
             rc=$?; cat "$OUT/bench3_$i.json"; ok_or_fail $rc bench3_$i
         done ;;
-    data)  # value dependence of the reduction time (tools/exp_data.py)
-        timeout -k 10 300 python tools/exp_data.py 3 10 > "$OUT/exp_data.jsonl" 2> "$OUT/exp_data.err"
-        rc=$?; cat "$OUT/exp_data.jsonl"; tail -2 "$OUT/exp_data.err"; ok_or_fail $rc data ;;
-    layout)
-        timeout -k 10 600 python tools/exp_layout.py > "$OUT/exp_layout.jsonl" 2> "$OUT/exp_layout.err"
-        rc=$?; head -8 "$OUT/exp_layout.jsonl"; tail -3 "$OUT/exp_layout.err"; ok_or_fail $rc layout ;;
-    alloc)
-        timeout -k 10 600 python tools/exp_alloc.py > "$OUT/exp_alloc.jsonl" 2> "$OUT/exp_alloc.err"
-        rc=$?; cat "$OUT/exp_alloc.jsonl"; tail -3 "$OUT/exp_alloc.err"; ok_or_fail $rc alloc ;;
-    allocpmc)
-        timeout -k 10 600 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum --kernel-trace \
-            --output-format csv -d "$OUT/allocpmc1" -o run -- python3 tools/exp_alloc.py 25 3 > "$OUT/allocpmc1.jsonl" 2> "$OUT/allocpmc1.err"
-        rc=$?; cat "$OUT/allocpmc1.jsonl"; ok_or_fail $rc allocpmc1
-        timeout -k 10 600 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum --kernel-trace \
-            --output-format csv -d "$OUT/allocpmc2" -o run -- python3 tools/exp_alloc.py 25 3 > "$OUT/allocpmc2.jsonl" 2> "$OUT/allocpmc2.err"
-        rc=$?; cat "$OUT/allocpmc2.jsonl"; ok_or_fail $rc allocpmc2 ;;
-    stride)
-        timeout -k 10 600 python tools/exp_stride.py 25 > "$OUT/exp_stride.jsonl" 2> "$OUT/exp_stride.err"
-        rc=$?; cat "$OUT/exp_stride.jsonl"; tail -2 "$OUT/exp_stride.err"; ok_or_fail $rc stride
-        timeout -k 10 600 python tools/exp_stride.py 26 >> "$OUT/exp_stride.jsonl" 2>> "$OUT/exp_stride.err"
-        rc=$?; tail -2 "$OUT/exp_stride.jsonl"; ok_or_fail $rc stride26 ;;
-    map)
-        timeout -k 10 600 python tools/exp_map.py 200 > "$OUT/exp_map.jsonl" 2> "$OUT/exp_map.err"
-        rc=$?; cat "$OUT/exp_map.jsonl"; tail -2 "$OUT/exp_map.err"; ok_or_fail $rc map ;;
-    counters)
-        timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1
-        rc=$?; grep -i -E "utcl|tlb|translat" "$OUT/counters.txt" | head -30; ok_or_fail $rc counters ;;
     *)
         echo "unknown step $s" ;;
     esac

@@ -7,7 +7,11 @@ One round = D x fa_submit (or fa_submit_pinned) + fa_finalize (reduce + D2H).
 Reports GiB/s of client input per round, for pageable and pinned host buffers,
 and the device-resident rate of the same round for comparison.
 
-  python tools/h2d_rate.py [D] [n_log2] [rounds]
+  python tools/h2d_rate.py [D] [n_log2] [rounds] [shards]
+
+shards > 1 runs a range-sharded context of that many shards; on a one-GPU box they share GPU 0
+(FA_TEST_SHARED_DEVICE), so the PCIe link is the same and an unchanged rate shows that the shards'
+copies overlap (the host side issues every shard's H2D / D2H before it waits for any).
 """
 import json
 import os
@@ -26,6 +30,7 @@ def main():
     D = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     n = 1 << int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 26
     rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+    shards = int(sys.argv[4]) if len(sys.argv) > 4 else 1
     w = bench.Setup._weights(D)
     rng = np.random.default_rng(0)
     # at most 8 distinct host buffers, client k uses buffer k % 8 (timing does not depend on values; keeps
@@ -37,8 +42,15 @@ def main():
         t.numpy()[:] = x
         pinned.append(t)
     out = np.empty(n, np.float32)
-    res = {"D": D, "n": n, "bytes_per_client": n * 4, "distinct_host_buffers": len(pageable)}
-    with fa.Aggregator(1) as agg:
+    res = {"D": D, "n": n, "bytes_per_client": n * 4, "distinct_host_buffers": len(pageable), "shards": shards}
+    if shards == 1:
+        ctx = fa.Aggregator(1)
+    elif fa.device_count() >= shards:
+        ctx = fa.Aggregator(shards)
+    else:
+        ctx = fa.Aggregator(devices=[0] * shards, shared_device=True)
+        res["shared_device"] = True
+    with ctx as agg:
         agg.define(1, n, fa.F32, fa.F32, D, fa.FEDAVG)
         for mode in ("pageable", "pinned"):
             times = []
@@ -54,6 +66,9 @@ def main():
             t = min(times[1:])
             res[mode] = {"round_s": round(t, 4), "GiB_s_input": round(D * n * 4 / t / 2**30, 2),
                          "GB_s_pcie_bytes": round((D + 1) * n * 4 / t / 1e9, 2)}
+        if shards > 1:
+            print(json.dumps(res))
+            return
         # device-resident round on the same slots
         stream = torch.cuda.Stream()
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]

@@ -62,8 +62,7 @@ def main():
             line = json.loads(open(bj).read().strip().splitlines()[-1])
             summary["bench_under_profiler"] = line["roofline"]
             steps = int(line["steps"])
-        # calls include fa_bucket_define's placement-probe launches (slow candidates among them); the
-        # bench's timed launches are the last `steps` of the dominant kernel
+        # the bench's timed launches are the last `steps` of the dominant kernel (warm-ups come first)
         summary["kernels"] = []
         for k, v in sorted(g.items(), key=lambda kv: -sum(kv[1])):
             rec = {"kernel": k[0], "grid": k[1], "calls": len(v), "avg_ns": round(sum(v) / len(v), 1), "min_ns": min(v)}
@@ -74,19 +73,27 @@ def main():
 
     fetch = os.path.join(src, "pmc_FETCH_SIZE", "run_counter_collection.csv")
     write = os.path.join(src, "pmc_WRITE_SIZE", "run_counter_collection.csv")
+    if workload != "northstar" or not os.path.exists(fetch):  # tools/pmc_workloads.sh layout
+        fetch = os.path.join(src, "pmc_%s_FETCH_SIZE" % workload, "run_counter_collection.csv")
+        write = os.path.join(src, "pmc_%s_WRITE_SIZE" % workload, "run_counter_collection.csv")
     if os.path.exists(fetch) and os.path.exists(write):
         fk, fv = dominant(per_kernel(fetch, "Counter_Value", "FETCH_SIZE"))
         wg = per_kernel(write, "Counter_Value", "WRITE_SIZE")
         wv = wg[fk]
         f_kib, w_kib = sum(fv) / len(fv), sum(wv) / len(wv)
         traffic = (2 * f_kib + w_kib) * 1024
-        summary["pmc"] = {"kernel": fk[0], "grid": fk[1], "launches": len(fv), "FETCH_SIZE_KiB": f_kib,
-                          "WRITE_SIZE_KiB": w_kib, "hbm_bytes_per_launch": round(traffic),
-                          "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count correction)"}
+        rec = {"kernel": fk[0], "grid": fk[1], "launches": len(fv), "FETCH_SIZE_KiB": f_kib,
+               "WRITE_SIZE_KiB": w_kib, "hbm_bytes_per_launch": round(traffic),
+               "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count correction)"}
+        if workload == "northstar":
+            summary["pmc"] = rec
+        else:
+            summary.setdefault("pmc_workloads", {})[workload] = rec
         tp = os.path.join(prof, "pmc_traffic.json")
         d = json.load(open(tp)) if os.path.exists(tp) else {}
         d[workload] = {"hbm_bytes_per_launch": round(traffic), "kernel": fk[0], "grid": fk[1],
-                       "source": "profiles/%s_summary.json" % rnd}
+                       "FETCH_SIZE_KiB": f_kib, "WRITE_SIZE_KiB": w_kib, "round": rnd,
+                       "source": "profiles/%s_summary.json (gpurun_out/%s)" % (rnd, os.path.basename(os.path.normpath(src)))}
         json.dump(d, open(tp, "w"), indent=1)
     for extra in ("hbm_probe.json",):
         p = os.path.join(src, extra)
