@@ -148,7 +148,7 @@ def traffic_from_profile(workload, n_gpus):
     rec = d.get(workload)
     if not rec:
         return None, None
-    return rec.get("hbm_bytes_per_launch"), rec.get("source")
+    return rec.get("hbm_bytes_per_launch"), "%s, kernel %s" % (rec.get("source"), rec.get("kernel", "?").split("(")[0])
 
 
 class Setup:
@@ -356,7 +356,7 @@ def load_shard():
     return importlib.import_module("mhfsl_amd.shard")
 
 
-def spawn_ranks(n, argv):
+def spawn_ranks(n, argv, script=None):
     """`--gpus N` (N > 1) without a launcher: start N rank processes (RANK / LOCAL_RANK / WORLD_SIZE /
     MASTER_* in their environment, one GPU each) and wait for them.  Runs before this process touches
     torch or HIP, so nothing is exec'd after GPU init; returns the worst exit code.  Should one rank
@@ -370,7 +370,7 @@ def spawn_ranks(n, argv):
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + argv, env=env))
+        procs.append(subprocess.Popen([sys.executable, "-u", script or os.path.abspath(__file__)] + argv, env=env))
     grace = float(os.environ.get("FA_BENCH_RANK_GRACE", "60"))
     failed_at = None
     while True:
