@@ -336,18 +336,30 @@ def layout_desc_of(layout, D, world, chunks):
 
 
 class LinePrinter:
-    """Rank 0 prints the one JSON line exactly once (from the main thread or the watchdog)."""
+    """Rank 0 prints the one JSON line exactly once (from the main thread or the watchdog), on the process's
+    original stdout; everything else that writes to fd 1 (RCCL's version banner, library chatter) has been
+    moved to stderr by quiet_stdout(), so the driver's stdout carries that one line only."""
 
-    def __init__(self, rank):
+    def __init__(self, rank, out=None):
         self.rank = rank
+        self.out = out or sys.stdout
         self.lock = threading.Lock()
         self.done = False
 
     def emit(self, line):
         with self.lock:
             if self.rank == 0 and not self.done:
-                print(json.dumps(line), flush=True)
+                self.out.write(json.dumps(line) + "\n")
+                self.out.flush()
             self.done = True
+
+
+def quiet_stdout():
+    """fd 1 -> stderr for the rest of the process; returns a file on the original stdout."""
+    sys.stdout.flush()
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    return out
 
 
 def load_shard():
@@ -413,10 +425,16 @@ def main():
     ap.add_argument("--dist-backend", default="auto",
                     help="auto (nccl = RCCL over xGMI when every rank has its own GPU, else gloo), nccl or gloo")
     ap.add_argument("--tune", default="", help="block,max_blocks,unroll,load_policy,store_policy (fa_tuning)")
+    ap.add_argument("--ctx-multi", default="", choices=["", "range", "rs"],
+                    help="one process over every visible GPU through the C ABI: FA_SHARD_RANGE or FA_SHARD_CLIENT_RS "
+                         "(RCCL reduce-scatter); prints one JSON object (a secondary of the N = 1 run)")
     args = ap.parse_args()
+    if args.ctx_multi:
+        return ctx_multi(args)
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    line_out = quiet_stdout()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -531,8 +549,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_secondary:
         setup.close()
         line["secondary"] = single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier)
+        if n_dev >= 2:
+            line["secondary"].update(ctx_multi_secondaries(n_dev))
 
-    printer = LinePrinter(rank)
+    printer = LinePrinter(rank, line_out)
     if world > 1 and not args.no_secondary and args.layout == "range":
         # the other layouts on the same ranks, as secondaries: weak-scaled range (every rank a full 256 MiB
         # slice), and the client-sharded RCCL legs (reduce-scatter, p2p chain) on the same strong problem.
@@ -584,6 +604,65 @@ def main():
     printer.emit(line)
     if world > 1:
         dist.destroy_process_group()
+
+
+def ctx_multi(args):
+    """Device-resident rounds of one fa_ctx over every visible GPU (`--ctx-multi range|rs`): the in-process
+    multi-GPU layouts of the C ABI that fa_aggregator --gpus G uses.  Slots are filled in place on their
+    GPUs; a step is fa_reduce_part (range: each GPU its element range; rs: each GPU its clients' fp32
+    partials + ncclReduceScatter piece by piece); the steps are timed back to back, then fa_sync."""
+    import torch
+    fa = load_pkg()
+    fa.lib()
+    G = torch.cuda.device_count()
+    D, n, in_dt, _, desc = WORKLOADS[args.workload]
+    idt = fa.F32 if in_dt == "f32" else fa.BF16
+    s_in = 4 if in_dt == "f32" else 2
+    rs = args.ctx_multi == "rs"
+    agg = fa.Aggregator(G, rs=rs)
+    agg.define(1, n, idt, fa.F32, D, fa.FEDAVG)
+    for g in range(G):
+        with torch.cuda.device(g):
+            for k in range(D):
+                try:
+                    ptr, cnt, off = agg.slot(1, g, k)
+                except fa.FaError:  # rs: the client lives on another GPU
+                    continue
+                fa.fill_uniform(ptr, cnt, idt, 0x5EED, k, idx0=off)
+    for g in range(G):
+        torch.cuda.synchronize(g)
+    w = Setup._weights(D)
+    for _ in range(args.warmup):
+        agg.reduce(1, w)
+    agg.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        agg.reduce(1, w)
+    agg.sync()
+    dt = (time.perf_counter() - t0) / args.steps
+    out = {"layout": args.ctx_multi, "gpus": G, "workload": args.workload, "description": desc, "clients": D,
+           "elems_per_client": n, "ms_per_round": round(dt * 1e3, 4),
+           "gib_s": round(D * n * s_in / dt / 2**30, 1), "steps": args.steps,
+           "tuning": agg.get_tuning()}
+    agg.close()
+    print(json.dumps(out), flush=True)
+
+
+def ctx_multi_secondaries(n_dev, timeout=240):
+    """On a node with several visible GPUs, the N = 1 run also times the in-process multi-GPU layouts over
+    all of them (child processes, time-limited: a stalled collective cannot take the main line with it)."""
+    res = {}
+    for layout, workload in (("range", "northstar"), ("rs", "northstar"), ("rs", "c4")):
+        key = "ctx_%s_%s_%dgpu" % (layout, workload, n_dev)
+        try:
+            r = subprocess.run([sys.executable, os.path.abspath(__file__), "--ctx-multi", layout, "--workload",
+                                workload, "--steps", "10", "--warmup", "2"], capture_output=True, text=True,
+                               timeout=timeout)
+            res[key] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
+                {"error": "rc %d: %s" % (r.returncode, r.stderr[-300:])}
+        except Exception as e:  # noqa: BLE001 -- reported, never fatal
+            res[key] = {"error": repr(e)[:300]}
+    return res
 
 
 def single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier):

@@ -580,6 +580,9 @@ int reduce_part(fa_ctx* ctx, Part& p, const float* w, hipStream_t s) {
         hipStream_t st = s ? s : r.compute;
         int rc = wait_copies(ctx, g, st);
         if (rc) return rc;
+        // the previous round's exchange still reads the partials (back-to-back device-resident rounds)
+        FA_HIP(hipEventRecord(r.step_ev, r.comm));
+        FA_HIP(hipStreamWaitEvent(st, r.step_ev, 0));
         if (p.c1[(size_t)g] == p.c0[(size_t)g])  // a GPU without clients contributes zeros
             FA_HIP(hipMemsetAsync(p.partial[(size_t)g], 0, p.npad * 4, st));
     }

@@ -359,6 +359,7 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
     // thread 0 takes the ticket; its value is first needed at the phase-0 meeting, so the atomic's
     // latency hides under the phase's loads
     unsigned long long ticket = 0;
+    int wait_budget = 1 << 16;  // thread 0: spins per meeting; 0 after one ran out (the grid is not co-resident)
     if (threadIdx.x == 0)
         ticket = __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(sync), 1ull, __ATOMIC_RELAXED,
                                         __HIP_MEMORY_SCOPE_AGENT);
@@ -403,11 +404,15 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
             __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const unsigned target = (unsigned)(G * (p + 1) - slack);
             int spins = 0;
-            for (; __hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target && spins < (1 << 16);
+            for (; __hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target && spins < wait_budget;
                  ++spins)
                 __builtin_amdgcn_s_sleep(1);
-            if (spins == (1 << 16))  // the grid was not co-resident (GPU shared): counted, fa_phased_timeouts
+            if (wait_budget && spins == wait_budget) {
+                // the grid was not co-resident (GPU shared with other kernels): counted (fa_phased_timeouts),
+                // and this workgroup stops waiting at the launch's later meetings, which would run out too
                 __hip_atomic_fetch_add(sync + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                wait_budget = 0;
+            }
         }
         __syncthreads();
 #pragma unroll 1

@@ -83,7 +83,8 @@ def test_rs_layout_multi_gpu_tolerance(fa, O, torch_gpu, G, D, chunks):
         for k in range(D):
             agg.submit(1, k, xs[k], w[k])
         got = agg.finalize(1)
-        agg.reduce(1, w)
+        for _ in range(3):  # back-to-back device-resident rounds: each waits for the previous exchange
+            agg.reduce(1, w)
         assert_bits(agg.copy_output(1), got)
     ref = O.fedavg(xs, w)
     absw = sum(abs(np.float64(wk)) * np.abs(x.astype(np.float64)) for wk, x in zip(w, xs))
