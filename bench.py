@@ -138,10 +138,15 @@ def cpu_baseline(D, sample_elems, reps):
 
 # ------------------------------------------------------------------ device measurement
 
-def traffic_from_profile(workload, n_gpus):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), if present."""
+def traffic_from_profile(workload, n_gpus, strong_range=False):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), if present.  At N > 1 a
+    rank's launch of the strong-scaled north star is the per-rank share measured as ns_w<N>."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if n_gpus != 1 or not os.path.exists(p):
+    if n_gpus != 1:
+        if not (strong_range and workload == "northstar"):
+            return None, None
+        workload = "ns_w%d" % n_gpus
+    if not os.path.exists(p):
         return None, None
     with open(p) as f:
         d = json.load(f)
@@ -428,6 +433,9 @@ def main():
     ap.add_argument("--ctx-multi", default="", choices=["", "range", "rs"],
                     help="one process over every visible GPU through the C ABI: FA_SHARD_RANGE or FA_SHARD_CLIENT_RS "
                          "(RCCL reduce-scatter); prints one JSON object (a secondary of the N = 1 run)")
+    ap.add_argument("--h2d", action="store_true",
+                    help="with --ctx-multi: host-inclusive rounds (fa_submit_pinned of every client from host "
+                         "memory, overlapped per GPU, + fa_finalize into host memory)")
     args = ap.parse_args()
     if args.ctx_multi:
         return ctx_multi(args)
@@ -458,6 +466,9 @@ def main():
         backend = "nccl" if n_dev >= world else "gloo"
     torch.cuda.set_device(device)
     fa.lib()
+    shared_gpus = n_dev < world
+    if shared_gpus:  # rehearsal: ranks share GPUs, and the phased kernel's persistent grid needs a whole GPU
+        fa.set_tuning(walk=2)
     if args.tune:
         b, mb, u, lp, sp = [int(x) for x in args.tune.split(",")]
         fa.set_tuning(block=b, max_blocks=mb, unroll=u, load_policy=lp, store_policy=sp)
@@ -512,7 +523,7 @@ def main():
 
     kavg = statistics.mean(kern_ms)
     achieved = setup.algo_bytes() / (kavg * 1e-3) / 1e9
-    traffic, traffic_src = traffic_from_profile(args.workload, world)
+    traffic, traffic_src = traffic_from_profile(args.workload, world, strong and args.layout == "range")
     line = {
         "metric": "GiB/s aggregated (device-resident), D-client fp32 bucket FedAvg reduce",
         "value": round(total_bytes * args.steps / wall / 2**30, 3),
@@ -531,6 +542,7 @@ def main():
                    "layout": layout_desc, "parallelism": "%s%d" % (args.layout, world),
                    "world_size": dist.get_world_size() if world > 1 else 1,
                    "dist_backend": backend if world > 1 else None,
+                   "ranks_share_gpus": shared_gpus,
                    "tuning": setup.agg.get_tuning(), "input_sets_rotated": setup.nsets},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -632,16 +644,32 @@ def ctx_multi(args):
     for g in range(G):
         torch.cuda.synchronize(g)
     w = Setup._weights(D)
+    if args.h2d:
+        # client buckets in pinned host memory (8 distinct buffers, client k uses k % 8: timing does not depend on
+        # values and C5 stays at 8 GiB of host memory), submitted each round; the result lands in host memory
+        import numpy as np
+        hosts = [fa.PinnedBuffer(n * s_in) for _ in range(min(D, 8))]
+        for i, h in enumerate(hosts):
+            h.view(np.float32)[:] = 0.25 * (i + 1)  # any finite values: the timing does not depend on them
+        res = np.empty(n, np.float32)
+
+        def step():
+            for k in range(D):
+                agg.submit(1, k, hosts[k % len(hosts)].view(np.uint8), w[k], pinned=True)
+            agg.finalize(1, res)
+    else:
+        def step():
+            agg.reduce(1, w)
     for _ in range(args.warmup):
-        agg.reduce(1, w)
+        step()
     agg.sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        agg.reduce(1, w)
+        step()
     agg.sync()
     dt = (time.perf_counter() - t0) / args.steps
     out = {"layout": args.ctx_multi, "gpus": G, "workload": args.workload, "description": desc, "clients": D,
-           "elems_per_client": n, "ms_per_round": round(dt * 1e3, 4),
+           "elems_per_client": n, "host_inclusive": args.h2d, "ms_per_round": round(dt * 1e3, 4),
            "gib_s": round(D * n * s_in / dt / 2**30, 1), "steps": args.steps,
            "tuning": agg.get_tuning()}
     agg.close()
@@ -652,11 +680,14 @@ def ctx_multi_secondaries(n_dev, timeout=240):
     """On a node with several visible GPUs, the N = 1 run also times the in-process multi-GPU layouts over
     all of them (child processes, time-limited: a stalled collective cannot take the main line with it)."""
     res = {}
-    for layout, workload in (("range", "northstar"), ("rs", "northstar"), ("rs", "c4")):
-        key = "ctx_%s_%s_%dgpu" % (layout, workload, n_dev)
+    for layout, workload, h2d in (("range", "northstar", False), ("rs", "northstar", False), ("rs", "c4", False),
+                                  ("range", "c5", True)):
+        # the last: BASELINE C5, 128 x 1 GiB buckets arriving from host memory, H2D overlapped over every GPU's link
+        key = "ctx_%s_%s%s_%dgpu" % (layout, workload, "_h2d" if h2d else "", n_dev)
         try:
             r = subprocess.run([sys.executable, os.path.abspath(__file__), "--ctx-multi", layout, "--workload",
-                                workload, "--steps", "10", "--warmup", "2"], capture_output=True, text=True,
+                                workload] + (["--h2d", "--steps", "3", "--warmup", "1"] if h2d else
+                                             ["--steps", "10", "--warmup", "2"]), capture_output=True, text=True,
                                timeout=timeout)
             res[key] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
                 {"error": "rc %d: %s" % (r.returncode, r.stderr[-300:])}
