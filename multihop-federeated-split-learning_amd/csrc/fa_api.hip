@@ -18,6 +18,7 @@
 // returns FA_ERR_NODEV.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <condition_variable>
@@ -59,6 +60,17 @@ CtxTuning defaults() {
     std::lock_guard<std::mutex> g(g_defaults_mu);
     return g_defaults;
 }
+
+// A roctx range around a host-side entry (submit, finalize, batched reduce, ...), so that
+// `rocprofv3 --marker-trace` shows the aggregation round's host phases beside its kernels and copies.
+struct Trace {
+    explicit Trace(const char* fmt, int a = -1, int b = -1) {
+        char buf[96];
+        snprintf(buf, sizeof buf, fmt, a, b);
+        roctxRangePushA(buf);
+    }
+    ~Trace() { roctxRangePop(); }
+};
 
 int fail(int code, const char* fmt, ...) {
     char buf[512];
@@ -532,6 +544,7 @@ int emulated_reduce_scatter(fa_ctx* ctx, Part& p, size_t a, size_t q, size_t off
 // range -> each GPU's shard; rs -> the clients' fp32 partials, piece by piece, each piece's RCCL
 // reduce-scatter (ring over xGMI) overlapping the reduction of the next.
 int reduce_part(fa_ctx* ctx, Part& p, const float* w, hipStream_t s) {
+    Trace tr(p.rs ? "fa_reduce rs D %d" : "fa_reduce D %d", p.D);
     const int G = ctx->G;
     if (!p.rs) {
         for (int g = 0; g < G; ++g) {
@@ -682,6 +695,7 @@ int advance_prefix(fa_ctx* ctx, Part& p) {
     int j = p.reduced;
     while (j < p.D && p.submitted[(size_t)j]) ++j;
     if (j == p.reduced) return FA_OK;
+    Trace tr("fa_accumulate slots %d..%d", p.reduced, j);
     for (int g = 0; g < ctx->G; ++g) {
         GpuRes& r = ctx->gpu[(size_t)g];
         DeviceGuard dg(r.dev);
@@ -698,6 +712,7 @@ int advance_prefix(fa_ctx* ctx, Part& p) {
 }
 
 int submit_impl(fa_ctx* ctx, int part_id, int slot, const Gather& src, float weight, bool pinned) {
+    Trace tr("fa_submit part %d slot %d", part_id, slot);
     Part* p;
     int rc = check_part(ctx, part_id, &p);
     if (rc) return rc;
@@ -754,6 +769,7 @@ int submit_impl(fa_ctx* ctx, int part_id, int slot, const Gather& src, float wei
 // GPU's copies wait on that GPU's done event (no device-wide synchronization); pinned copies of all GPUs
 // are issued before any is waited for, staged ones run on one host thread per GPU.
 int copy_output(fa_ctx* ctx, Part& p, const Gather& dst, bool pinned) {
+    Trace tr("fa_copy_output n %d", (int)std::min<size_t>(p.n, 0x7fffffff));
     const size_t so = p.rs ? 4 : dsize(p.out);
     if (dst.total() != p.n * dsize(p.out))
         return fail(FA_ERR_ARG, "output of %zu bytes expected, destination holds %zu", p.n * dsize(p.out),
@@ -833,6 +849,7 @@ void reset_round(Part& p) {
 // The end of a phase: wait for the submits, reduce on every GPU (unless the round's reduction is done
 // already: accumulate on arrival reached D, or fa_reduce_parts), copy the result out, reset the round.
 int finalize_impl(fa_ctx* ctx, int part_id, const Gather& dst, bool pinned) {
+    Trace tr("fa_finalize part %d", part_id);
     Part* p;
     int rc = check_part(ctx, part_id, &p);
     if (rc) return rc;
@@ -863,6 +880,7 @@ int finalize_impl(fa_ctx* ctx, int part_id, const Gather& dst, bool pinned) {
 // One launch per GPU for every batchable part (FedAvg, range layout, <= kMaxClients clients, same dtypes,
 // not taken by the phased kernel); the others launch one by one.  Marks the parts ready for finalize.
 int reduce_parts_impl(fa_ctx* ctx, int n_parts, const int* ids, const float* const* weights, hipStream_t s) {
+    Trace tr("fa_reduce_parts n %d", n_parts);
     std::vector<Part*> ps;
     for (int i = 0; i < n_parts; ++i) {
         Part* p;
