@@ -22,12 +22,14 @@
 // --mode literal reproduces the reference's arithmetic bit-for-bit
 // (fl(fl(x_last + x_last) / 1000)); --mode fedavg (default) is
 // the north star's weighted mean (weights n_k/N from --samples, else 1/D).
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <iostream>
 #include <map>
+#include <set>
 #include <memory>
 #include <sstream>
 #include <string>
@@ -51,6 +53,9 @@ struct Options {
     bool eager = false;  // --eager: accumulate on arrival (the chain advances with the in-order receipts)
     int rs_chunks = 0;
     double link_mbps = 0;
+    // failure detection: after stall_report_s without a receipt, name the data owners still missing;
+    // after receipt_timeout_s (0 = wait forever, the reference's behaviour), give up with exit code 3
+    double stall_report_s = 60, receipt_timeout_s = 0;
     std::map<int, double> samples;  // client id -> n_k
 };
 
@@ -58,7 +63,7 @@ void usage() {
     std::cerr << "usage: fa_aggregator -i ID -d DATA_OWNERS -c COMPUTE_NODES [--mode fedavg|literal] [--gpus G]\n"
                  "       [--rounds R] [--port-base P] [--discover] [--link-mbps M] [--samples id:n,...]\n"
                  "       [--divisor K] [--last-layers L] [--no-pinned] [--layout range|rs] [--rs-chunks C]\n"
-                 "       [--eager]\n";
+                 "       [--eager] [--stall-report S] [--receipt-timeout S]\n";
 }
 
 bool parse_args(int argc, char** argv, Options* o) {
@@ -83,6 +88,8 @@ bool parse_args(int argc, char** argv, Options* o) {
         else if (a == "--no-pinned") o->pinned = false;
         else if (a == "--eager") o->eager = true;
         else if (a == "--rs-chunks") o->rs_chunks = std::atoi(val("--rs-chunks"));
+        else if (a == "--stall-report") o->stall_report_s = std::atof(val("--stall-report"));
+        else if (a == "--receipt-timeout") o->receipt_timeout_s = std::atof(val("--receipt-timeout"));
         else if (a == "--layout") {
             std::string l = val("--layout");
             if (l == "rs") o->rs = true;
@@ -109,7 +116,7 @@ bool parse_args(int argc, char** argv, Options* o) {
             return false;
         }
     }
-    return o->data_owners >= 1;
+    return o->data_owners >= 1 && o->stall_report_s > 0 && o->receipt_timeout_s >= 0;
 }
 
 // parts[1].layers.size() for the aggregator's ModelPart(start, -1) (systemAPI.cpp:19):
@@ -158,6 +165,7 @@ public:
             for (int i = 0; i < o.data_owners - 1; ++i) order.push_back(i + o.compute_nodes + 1);
         }
         for (int k = 0; k < (int)order.size(); ++k) slots_.insert({order[k], k});
+        expected_ = order;
         claimed_.assign(o.data_owners, 0);
     }
     ~Aggregator() { fa_destroy(ctx_); }
@@ -205,6 +213,7 @@ public:
             FA_CHECK(fa_submit(ctx_, r.model_part, slot, flat.data(), weight_of(r.client_id)));
         }
         b.bytes_in += r.blob_len;
+        b.arrived.insert(r.client_id);
         b.last = r;  // template of the reply: the last receipt (its buffers travel back, as in the reference)
         st_.absorb_s += secs_since(t0);
     }
@@ -250,6 +259,7 @@ public:
             }
         }
         b.held.clear();
+        b.arrived.clear();
         b.bytes_in = 0;
         st_.finalize_s += t_fin;
         st_.frame_s += secs_since(t0) - t_fin;
@@ -263,6 +273,20 @@ public:
     }
 
     size_t bytes_in(int mp) { return buckets_[mp].bytes_in; }
+
+    // The data owners whose receipt of bucket mp has not arrived this round ("mp 2: 4 7 9").
+    std::string missing(const std::vector<int>& mps) {
+        std::ostringstream os;
+        for (int mp : mps) {
+            const auto& got = buckets_[mp].arrived;
+            std::ostringstream ids;
+            int n = 0;
+            for (int c : expected_)
+                if (!got.count(c)) ids << (n++ ? " " : "") << c;
+            if (n) os << (os.tellp() > 0 ? "; " : "") << "part " << mp << ": " << n << " owner(s) [" << ids.str() << "]";
+        }
+        return os.str();
+    }
 
     // The reductions of a phase's buckets as one batched launch (fa_reduce_parts: the last-part layers of
     // phase 2, aggregator.cpp:108-150, are one segment table); the following reduce() calls then only
@@ -291,6 +315,7 @@ private:
         size_t numel = 0, bytes_in = 0;
         Receipt last;
         std::vector<std::shared_ptr<const Bytes>> held;  // pinned frames DMA'd from, until finalize
+        std::set<int> arrived;  // client ids received this round
     };
 
     int slot_of(int client) {
@@ -323,8 +348,32 @@ private:
     std::map<int, Bucket> buckets_;
     std::map<int, int> slots_;  // client id -> slot
     std::vector<char> claimed_;  // slot -> an arrived client holds it
+    std::vector<int> expected_;  // the data owners' ids in slot order
     Stats st_;
 };
+
+// The next receipt, with the failure detection the reference lacks (its receive loop blocks forever on a
+// data owner that died, network_layer.cpp:654-665): every stall_report_s of silence names the owners still
+// missing in this phase; after receipt_timeout_s of silence (if set) the aggregator exits with code 3.
+Receipt wait_receipt(NetLayer& net, const Options& o, Aggregator& agg, const std::vector<int>& mps, int round,
+                     int phase) {
+    Receipt r;
+    double silent = 0;
+    for (;;) {
+        double step = o.stall_report_s;
+        if (o.receipt_timeout_s > 0) step = std::min(step, o.receipt_timeout_s - silent);
+        if (net.try_next_receipt(&r, std::max(1, (int)(step * 1000)))) return r;
+        silent += step;
+        const bool give_up = o.receipt_timeout_s > 0 && silent >= o.receipt_timeout_s - 1e-9;
+        std::cerr << "[aggregator] round " << round << " phase " << phase << ": no receipt for " << silent
+                  << " s; missing " << agg.missing(mps) << (give_up ? "; giving up (--receipt-timeout)" : "")
+                  << "\n";
+        if (give_up) {
+            net.stop();
+            std::exit(3);
+        }
+    }
+}
 
 }  // namespace
 
@@ -369,7 +418,7 @@ int main(int argc, char** argv) {
         std::vector<Receipt> early;  // phase-2 receipts that overtook phase 1 (not in the reference's FIFO)
         int received = 0;
         while (received < o.data_owners) {
-            Receipt r = net.next_receipt();
+            Receipt r = wait_receipt(net, o, agg, {1}, round, 1);
             if (r.model_part != 1) {
                 early.push_back(std::move(r));
                 continue;
@@ -393,8 +442,10 @@ int main(int argc, char** argv) {
             agg.absorb(r);
             ++got;
         }
+        std::vector<int> mps;
+        for (int mp = 2; mp <= L + 1; ++mp) mps.push_back(mp);
         while (got < want) {
-            Receipt r = net.next_receipt();
+            Receipt r = wait_receipt(net, o, agg, mps, round, 2);
             if (r.model_part < 2 || r.model_part > L + 1) {
                 std::cerr << "[aggregator] unexpected model_part " << r.model_part << " in phase 2\n";
                 continue;
@@ -407,8 +458,6 @@ int main(int argc, char** argv) {
         for (int mp = 2; mp <= L + 1; ++mp) in2 += agg.bytes_in(mp);
         auto t3 = std::chrono::steady_clock::now();
         std::vector<std::shared_ptr<const Bytes>> replies;
-        std::vector<int> mps;
-        for (int mp = 2; mp <= L + 1; ++mp) mps.push_back(mp);
         agg.reduce_all(mps);
         for (int mp : mps) replies.push_back(agg.reduce(mp));
         const double red2 = secs_since(t3);

@@ -119,3 +119,33 @@ def test_multi_mb_parts_concurrent_owners(torch_gpu, tmp_path, pinned, sequentia
     finally:
         if agg.poll() is None:
             agg.kill()
+
+
+@pytest.mark.parametrize("drop_phase", [1, 2])
+def test_missing_owner_is_reported_and_times_out(torch_gpu, drop_phase):
+    """Failure detection: one data owner never sends its phase-1 (or phase-2) receipts.  The
+    reference's aggregator blocks forever (its receive loop, network_layer.cpp:654-665); fa_aggregator names
+    the missing owner after --stall-report seconds of silence and exits with code 3 after --receipt-timeout."""
+    D, base = 3, pick_base()  # owner ids 0, 2, 3 (aggregator.cpp:103-105 with C = 1); owner k = 1 is id 2
+    agg = subprocess.Popen([AGG, "-i", "-1", "-d", str(D), "-c", "1", "--rounds", "1", "--port-base", str(base),
+                            "--stall-report", "1", "--receipt-timeout", "3"],
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        time.sleep(0.5)
+        r = subprocess.run([OWNERS, "--blobs", os.path.join(GOLDEN, "lenet5_c1"), "--parts", "1,2,3", "-d", str(D),
+                            "-c", "1", "--port-base", str(base), "--model-name", "2", "--start", "6", "--end", "1",
+                            "--drop-owner", "1", "--drop-phase", str(drop_phase), "--reply-timeout", "8"],
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 1  # the owners never get their replies
+        out, err = agg.communicate(timeout=60)
+        assert agg.returncode == 3, err[-2000:]
+        stalls = [l for l in err.splitlines() if "no receipt for" in l]
+        assert len(stalls) >= 2 and "giving up" in stalls[-1]
+        if drop_phase == 1:
+            assert "phase 1" in stalls[0] and "part 1: 1 owner(s) [2]" in stalls[0]
+        else:
+            assert "phase 2" in stalls[0] and "part 2: 1 owner(s) [2]; part 3: 1 owner(s) [2]" in stalls[0]
+            assert sum(l.startswith("{") for l in out.splitlines()) == 0  # no round completed
+    finally:
+        if agg.poll() is None:
+            agg.kill()

@@ -8,6 +8,7 @@
 //
 //   fa_fake_owners --blobs DIR --parts 1,2,3 -d D -c C [--rounds R] [--mode fedavg|literal]
 //                  [--port-base P] [--model-name N --model-type T --start S --end E] [--seed X]
+//                  [--drop-owner K [--drop-phase P]] [--reply-timeout S]
 //                  [--sequential]   (owners send at once, one connection each, unless --sequential
 //                                    or --mode literal, whose result depends on the arrival order)
 // Prints one JSON line: {"ok": bool, "rounds": R, "checked_elems": ..., "round_ms": [...]}.
@@ -65,6 +66,8 @@ int main(int argc, char** argv) {
     uint64_t seed = 0x5EED;
     float divisor = 1000.0f;
     bool concurrent = true;
+    int drop_owner = -1, drop_phase = 1;  // failure injection: owner K never sends its phase-P receipts
+    long reply_timeout_ms = 600000;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
         const char* v = i + 1 < argc ? argv[i + 1] : "";
@@ -82,6 +85,9 @@ int main(int argc, char** argv) {
         else if (a == "--seed") seed = std::strtoull(v, nullptr, 0), ++i;
         else if (a == "--divisor") divisor = (float)std::atof(v), ++i;
         else if (a == "--sequential") concurrent = false;
+        else if (a == "--drop-owner") drop_owner = std::atoi(v), ++i;
+        else if (a == "--drop-phase") drop_phase = std::atoi(v), ++i;
+        else if (a == "--reply-timeout") reply_timeout_ms = (long)(std::atof(v) * 1000), ++i;
         else {
             std::cerr << "unknown argument " << a << "\n";
             return 2;
@@ -148,7 +154,7 @@ int main(int argc, char** argv) {
     size_t checked = 0;
     std::vector<long> round_ms;
     auto collect = [&](int want, std::vector<Receipt>* got) {
-        const long t_end = now_ms() + 600000;
+        const long t_end = now_ms() + reply_timeout_ms;
         while ((int)got->size() < want && now_ms() < t_end) {
             for (auto& kv : listeners) {
                 Receipt r;
@@ -203,6 +209,7 @@ int main(int argc, char** argv) {
             for (int k = 0; k < D; ++k)
                 for (auto& p : parts) {
                     if ((phase == 1) != (p.mp == 1)) continue;
+                    if (k == drop_owner && phase == drop_phase) continue;  // this owner "died"
                     by_owner[k].push_back(frames[p.mp][k]);
                     ++sent;
                 }

@@ -31,12 +31,12 @@ for s in $STEPS; do
         rc=$?; cat "$OUT/bench.json"; tail -3 "$OUT/bench.err"; ok_or_fail $rc bench ;;
     prof)
         timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-            python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-secondary > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
+            python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-secondary --no-live-pmc > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
         rc=$?; tail -3 "$OUT/prof.err"; ok_or_fail $rc prof ;;
     pmc)
         for c in FETCH_SIZE WRITE_SIZE; do
             timeout -k 10 600 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$OUT/pmc_$c" -o run -- \
-                python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-secondary > "$OUT/pmc_$c.json" 2> "$OUT/pmc_$c.err"
+                python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-secondary --no-live-pmc > "$OUT/pmc_$c.json" 2> "$OUT/pmc_$c.err"
             rc=$?; tail -2 "$OUT/pmc_$c.err"; ok_or_fail $rc pmc_$c
         done ;;
     pmcw)  # the same passes for the secondary workloads whose traffic bench.py reports
@@ -44,7 +44,7 @@ for s in $STEPS; do
         rc=$?; ok_or_fail $rc pmcw ;;
     layouts)
         for L in rs chain; do
-            timeout -k 10 300 python bench.py --layout $L --steps 10 --no-cpu-baseline --no-secondary > "$OUT/bench_$L.json" 2> "$OUT/bench_$L.err"
+            timeout -k 10 300 python bench.py --layout $L --steps 10 --no-cpu-baseline --no-secondary --no-live-pmc > "$OUT/bench_$L.json" 2> "$OUT/bench_$L.err"
             rc=$?; cat "$OUT/bench_$L.json"; tail -2 "$OUT/bench_$L.err"; ok_or_fail $rc layout_$L
         done ;;
     h2d)
@@ -106,7 +106,7 @@ for s in $STEPS; do
         done ;;
     bench3)  # three bench runs (fresh process each): the spread of pool placement
         for i in 1 2 3; do
-            timeout -k 10 300 python bench.py --no-cpu-baseline --no-secondary > "$OUT/bench3_$i.json" 2> "$OUT/bench3_$i.err"
+            timeout -k 10 300 python bench.py --no-cpu-baseline --no-secondary --no-live-pmc > "$OUT/bench3_$i.json" 2> "$OUT/bench3_$i.err"
             rc=$?; cat "$OUT/bench3_$i.json"; ok_or_fail $rc bench3_$i
         done ;;
     *)
