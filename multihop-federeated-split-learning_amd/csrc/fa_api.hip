@@ -1532,6 +1532,12 @@ int fa_phased_timeouts(int device, uint64_t* count) {
     return FA_OK;
 }
 
+// Diagnostic, not part of the ABI in fa.h: the per-workgroup timeline of the last phased launch on `device`
+// when the process runs with FA_TIMELINE=1 (tools/timeline.py).
+extern "C" int fa_diag_phased_timeline(int device, unsigned long long* out, int cap) {
+    return out && cap > 0 ? fa::phased_timeline(device, out, cap) : -1;
+}
+
 int fa_fill_uniform(void* d_dst, size_t n, fa_dtype dt, uint64_t seed, uint32_t client, uint64_t idx0,
                     void* hip_stream) {
     g_err.clear();

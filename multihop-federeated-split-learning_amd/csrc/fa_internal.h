@@ -54,6 +54,9 @@ hipError_t launch_chain(const ClientTable& t, int nc, fa_dtype in, fa_dtype out,
                         int64_t head, int64_t nvec, int64_t n, bool vector_ok, const Tuning& tu, hipStream_t s);
 // Meetings of the phased kernel on device `dev` that gave up waiting (the grid was not co-resident).
 hipError_t phased_timeouts(int dev, uint64_t* count);
+// FA_TIMELINE=1 diagnostic: copies the last phased launch's per-workgroup timeline (8 words each) on device
+// dev into out; returns the words copied (0: no timeline, -1: HIP error).
+int phased_timeline(int dev, unsigned long long* out, int cap);
 // Elements per GPU from which the phased walk applies (0: not in use); see fa_kernels.hip.
 int64_t phased_min_elems(fa_dtype in, const Tuning& tu);
 hipError_t launch_literal(const void* x, fa_dtype in, void* dst, fa_dtype out, float divisor, int64_t head,

@@ -352,7 +352,9 @@ __device__ __forceinline__ void put(const ClientTable& t, int nc, void* out, int
 template <typename IN, typename OUT, bool INIT, int REGS, bool SYNC, int TH>
 __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, int nc, const float* init,
                                                                        void* out, int64_t head, int64_t nvec, int64_t n,
-                                                                       unsigned* sync, int slack, int rl_last) {
+                                                                       unsigned* sync, int slack, int rl_last,
+                                                                       int skew, int skew_last,
+                                                                       unsigned long long* tl) {
     constexpr int V = In<IN>::kVec, T = TH, RL = Phased<IN, REGS, TH>::RL, RR = Phased<IN, REGS, TH>::RR;
     constexpr int U = TH > 256 ? 8 : 16;  // loads in flight per wave (2 waves per SIMD at 512 threads)
     __shared__ float buf[RL * T * V];
@@ -360,46 +362,27 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
     // latency hides under the phase's loads
     unsigned long long ticket = 0;
     int wait_budget = 1 << 16;  // thread 0: spins per meeting; 0 after one ran out (the grid is not co-resident)
+    // diagnostic timeline (FA_TIMELINE, fa_diag_phased_timeline): per workgroup, 8 slots of the 100 MHz
+    // wall clock -- start, phase-0 arrival / departure at the meeting, last arrival / departure, end
+    unsigned long long* my_tl = tl ? tl + (size_t)blockIdx.x * 8 : nullptr;
+    if (my_tl && threadIdx.x == 0) my_tl[0] = (unsigned long long)wall_clock64();
     if (threadIdx.x == 0)
         ticket = __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(sync), 1ull, __ATOMIC_RELAXED,
                                         __HIP_MEMORY_SCOPE_AGENT);
     if constexpr (SYNC) sync_scalar_edges<IN, INIT>(t, nc, init, head, head + nvec * V, n);
     else chain_scalar_edges<IN, OUT, INIT>(t, nc, init, out, head, head + nvec * V, n);
     const int64_t G = gridDim.x;
-    const int64_t per_phase = G * T * (RL + RR);
+    // skew: the workgroups of the odd XCDs (blockIdx odd; blocks are dealt round-robin over the 8 XCDs)
+    // take `skew` fewer LDS rows than the even ones in every full phase, and 2 skew_last fewer in the last
+    // (rl_last - skew_last against rl_last + skew_last) -- those XCDs read 5-10% slower (tools/timeline.py)
+    const int64_t per_phase = G * T * (RL + RR) - (G / 2) * T * skew;
     const int phases = (int)((nvec + per_phase - 1) / per_phase);
-    for (int p = 0; p < phases; ++p) {
-        // LDS vectors per lane in this phase: RL in full phases; the last phase is balanced by the host
-        // (every lane the same share, registers first: phased_rl_last)
-        const int rl = p == phases - 1 ? rl_last : RL;
-        const int64_t base = (int64_t)p * per_phase + (int64_t)blockIdx.x * T + threadIdx.x;
-#pragma unroll 1
-        for (int i = 0; i < rl; ++i) {
-            const int64_t v = base + (int64_t)i * G * T;
-            if (v < nvec) {
-                float acc[V];
-                chain_vec<IN, U, true, INIT>(t, nc, init, head + v * V, acc);
-#pragma unroll
-                for (int j = 0; j < V; ++j) buf[(i * T + threadIdx.x) * V + j] = acc[j];
-            }
-        }
-        // register part: this wave's contiguous chunk after the phase's LDS part
-        const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-        const int64_t c0 = (int64_t)p * per_phase + G * T * rl + ((int64_t)blockIdx.x * (T / 64) + wave) * RR * 64;
-        float keep[RR][V];
-        const bool staged = stage_regs<IN, INIT, RR, U>(t, nc, init, head, c0, nvec, keep);
-        if (!staged) {  // the chunk that holds the end of the bucket (or lies past it): no staging
-            for (int r = 0; r < RR; ++r) {
-                const int64_t v = c0 + r * 64 + (threadIdx.x & 63);
-                if (v < nvec) {
-                    float acc[V];
-                    chain_vec<IN, U, true, INIT>(t, nc, init, head + v * V, acc);
-                    put<OUT, V, SYNC>(t, nc, out, head + v * V, acc);
-                }
-            }
-        }
+    const bool odd = blockIdx.x & 1;
+    // the meeting before phase p's writes: every workgroup's reads of the phase are done (all but `slack`)
+    auto meet = [&](int p) {
         __syncthreads();
         if (threadIdx.x == 0) {
+            const unsigned long long t_arrive = my_tl ? (unsigned long long)wall_clock64() : 0;
             unsigned* arrive = sync + 4 + (unsigned)((ticket / (unsigned long long)G) % kSyncRing);
             __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const unsigned target = (unsigned)(G * (p + 1) - slack);
@@ -413,11 +396,62 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
                 __hip_atomic_fetch_add(sync + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 wait_budget = 0;
             }
+            if (my_tl) {
+                const unsigned long long t_leave = (unsigned long long)wall_clock64();
+                if (p == 0) my_tl[1] = t_arrive, my_tl[2] = t_leave;
+                my_tl[3] = t_arrive, my_tl[4] = t_leave, my_tl[6] = (unsigned long long)(p + 1);
+            }
         }
         __syncthreads();
+    };
+    for (int p = 0; p < phases; ++p) {
+        // LDS vectors per lane in this phase: r_all rows every workgroup takes, then r_even more that only
+        // the even XCDs' take.  Full phases: RL - skew and skew; the last phase is balanced by the host
+        // (rl_last per lane on average, registers first: phased_rl_last)
+        const bool last = p == phases - 1;
+        const int r_all = last ? rl_last - skew_last : RL - skew;
+        const int r_even = last ? 2 * skew_last : skew;
+        const int rl = r_all + (odd ? 0 : r_even);
+        // LDS row i: block (i G + b) of T vectors for i < r_all, block (r_all G + (i - r_all) G/2 + b/2) after
+        const int64_t p0 = (int64_t)p * per_phase + threadIdx.x;
+        const int64_t lds_rows = (int64_t)r_all * G + (int64_t)r_even * (G / 2);
+        auto row_vec = [&](int i) {
+            return i < r_all ? p0 + ((int64_t)i * G + blockIdx.x) * T
+                             : p0 + ((int64_t)r_all * G + (int64_t)(i - r_all) * (G / 2) + blockIdx.x / 2) * T;
+        };
 #pragma unroll 1
         for (int i = 0; i < rl; ++i) {
-            const int64_t v = base + (int64_t)i * G * T;
+            const int64_t v = row_vec(i);
+            if (v < nvec) {
+                float acc[V];
+                chain_vec<IN, U, true, INIT>(t, nc, init, head + v * V, acc);
+#pragma unroll
+                for (int j = 0; j < V; ++j) buf[(i * T + threadIdx.x) * V + j] = acc[j];
+            }
+        }
+        if (my_tl && p == 0) {
+            __syncthreads();
+            if (threadIdx.x == 0) my_tl[7] = (unsigned long long)wall_clock64();
+        }
+        // register part: this wave's contiguous chunk after the phase's LDS part
+        const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+        const int64_t c0 = (int64_t)p * per_phase + lds_rows * T + ((int64_t)blockIdx.x * (T / 64) + wave) * RR * 64;
+        float keep[RR][V];
+        const bool staged = stage_regs<IN, INIT, RR, U>(t, nc, init, head, c0, nvec, keep);
+        if (!staged) {  // the chunk that holds the end of the bucket (or lies past it): no staging
+            for (int r = 0; r < RR; ++r) {
+                const int64_t v = c0 + r * 64 + (threadIdx.x & 63);
+                if (v < nvec) {
+                    float acc[V];
+                    chain_vec<IN, U, true, INIT>(t, nc, init, head + v * V, acc);
+                    put<OUT, V, SYNC>(t, nc, out, head + v * V, acc);
+                }
+            }
+        }
+        meet(p);
+#pragma unroll 1
+        for (int i = 0; i < rl; ++i) {
+            const int64_t v = row_vec(i);
             if (v < nvec) put<OUT, V, SYNC>(t, nc, out, head + v * V, &buf[(i * T + threadIdx.x) * V]);
         }
         if (staged) {
@@ -425,6 +459,11 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
 #pragma unroll
             for (int r = 0; r < RR; ++r) put<OUT, V, SYNC>(t, nc, out, head + (c + r * 64) * V, keep[r]);
         }
+    }
+    if (my_tl) {  // end: this workgroup's stores have completed
+        __threadfence();
+        __syncthreads();
+        if (threadIdx.x == 0) my_tl[5] = (unsigned long long)wall_clock64();
     }
     if (threadIdx.x == 0) {
         const unsigned e = (unsigned)((ticket / (unsigned long long)G) % kSyncRing);
@@ -716,6 +755,7 @@ struct PhasedDevice {
     std::once_flag once;
     int cus = 0;
     unsigned* sync = nullptr;  // kSyncSlots slots, kSyncStride words apart
+    unsigned long long* tl = nullptr;  // FA_TIMELINE=1: the last phased launch's per-workgroup timeline
 };
 PhasedDevice g_phased[kMaxDevices];
 
@@ -735,33 +775,53 @@ PhasedDevice* phased_device() {
         }
         d.cus = cus;
         d.sync = p;
+        const char* e = std::getenv("FA_TIMELINE");
+        if (e && std::atoi(e) > 0 && hipMalloc((void**)&d.tl, sizeof(unsigned long long) * 8 * cus) == hipSuccess)
+            (void)hipMemset(d.tl, 0, sizeof(unsigned long long) * 8 * cus);
     });
     (void)hipGetLastError();
     return d.sync ? &d : nullptr;
 }
 
-// LDS vectors per lane in the last phase of a bucket of nvec vectors (fedavg_phased_kernel's rl_last):
-// the last phase's remainder is spread evenly over all `lanes` of the grid.  Up to RL vectors per lane it
-// goes to LDS alone; more fill every wave's register chunk (RR) and LDS takes the rest, so no lane holds
-// more than one vector above the average (filling LDS first and then whole register chunks left half the
-// waves of a partial phase idle while the others did RL + RR).
-inline int phased_rl_last(int64_t nvec, int64_t lanes, int RL, int RR) {
-    const int64_t per_phase = lanes * (RL + RR);
-    const int64_t rem = nvec % per_phase;
-    if (rem == 0) return RL;
+// LDS vectors per lane in the last phase (fedavg_phased_kernel's rl_last), whose `rem` vectors are spread
+// evenly over all `lanes` of the grid.  Up to RL vectors per lane go to LDS alone; more fill every wave's
+// register chunk (RR) and LDS takes the rest, so no lane holds more than one vector above the average
+// (filling LDS first and then whole register chunks left half the waves of a partial phase idle while the
+// others did RL + RR).
+inline int phased_rl_last(int64_t rem, int64_t lanes, int RL, int RR) {
+    if (rem >= lanes * (RL + RR)) return RL;
     const int64_t q = (rem + lanes - 1) / lanes;
     if (q <= RL) return (int)q;
     return (int)std::max<int64_t>(0, q - RR);
 }
 
+// LDS rows the odd XCDs' workgroups leave to the even ones in every full phase (fedavg_phased_kernel's
+// skew): RL / 10 in the f32 form -- 4 of its 40 (north star 1.259-1.261 against 1.271 ms, C4 5.25 against
+// 5.30, one rank's share at 2 GPUs 0.668-0.673 against 0.677-0.684; gpurun_out r02s25-s26); more loses
+// again.  None in the 512-thread bf16 form, whose 10 rows leave no step small enough (C3: 1 row 0.425-0.427
+// ms against 0.424, 4 rows 0.444-0.449; r02s26-s27).  FA_PHASED_SKEW overrides it (below RL / 2).
+int phased_skew(int RL) {
+    static const int v = [] {
+        const char* e = std::getenv("FA_PHASED_SKEW");
+        return e ? std::max(0, std::atoi(e)) : -1;
+    }();
+    return std::min(v >= 0 ? v : RL >= 20 ? RL / 10 : 0, RL / 2 - 1);
+}
+
 // Enqueue one phased launch on stream s, on the stream's counter slot.
 template <typename Kern>
-hipError_t phased_enqueue(PhasedDevice* d, Kern kern, int th, hipStream_t s, const ClientTable& t, int nc,
-                          const float* init, void* out, int64_t head, int64_t nvec, int64_t n, int rl_last) {
+hipError_t phased_enqueue(PhasedDevice* d, Kern kern, int th, int RL, int RR, hipStream_t s, const ClientTable& t,
+                          int nc, const float* init, void* out, int64_t head, int64_t nvec, int64_t n) {
     const unsigned slot = (unsigned)(((uintptr_t)s >> 4) % kSyncSlots);
     const int slack = d->cus / 32;  // the write part starts once all but ~3% of the workgroups have arrived
+    const int64_t lanes = (int64_t)d->cus * th;
+    const int skew = d->cus % 2 ? 0 : phased_skew(RL);
+    const int64_t per_phase = lanes * (RL + RR) - (int64_t)(d->cus / 2) * th * skew;
+    const int64_t phases = (nvec + per_phase - 1) / per_phase;
+    const int rl_last = phased_rl_last(nvec - (phases - 1) * per_phase, lanes, RL, RR);
+    const int skew_last = std::min({(skew + 1) / 2, rl_last, RL - rl_last});
     hipLaunchKernelGGL(kern, dim3((unsigned)d->cus), dim3(th), 0, s, t, nc, init, out, head, nvec, n,
-                       d->sync + slot * kSyncStride, slack, rl_last);
+                       d->sync + slot * kSyncStride, slack, rl_last, skew, skew_last, d->tl);
     return hipGetLastError();
 }
 
@@ -795,8 +855,7 @@ hipError_t launch_phased_r(const ClientTable& t, int nc, const float* init, void
     static std::atomic<int> occ[2] = {-1, -1};  // per INIT variant
     auto kern = init ? fedavg_phased_kernel<IN, OUT, true, REGS, false, TH> : fedavg_phased_kernel<IN, OUT, false, REGS, false, TH>;
     if (!phased_fits(occ[init ? 1 : 0], kern, TH)) return hipErrorNotSupported;
-    return phased_enqueue(d, kern, TH, s, t, nc, init, out, head, nvec, n,
-                          phased_rl_last(nvec, (int64_t)d->cus * TH, RL, RR));
+    return phased_enqueue(d, kern, TH, RL, RR, s, t, nc, init, out, head, nvec, n);
 }
 
 // Clients from which a bucket smaller than one phase takes a phase sized to it (launch_phased); fewer
@@ -901,6 +960,15 @@ hipError_t phased_timeouts(int dev, uint64_t* count) {
     return hipSuccess;
 }
 
+int phased_timeline(int dev, unsigned long long* out, int cap) {
+    if (dev < 0 || dev >= kMaxDevices || !g_phased[dev].tl) return 0;
+    const int n = std::min(cap, g_phased[dev].cus * 8);
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(out, g_phased[dev].tl, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    return n;
+}
+
 hipError_t launch_chain(const ClientTable& t, int nc, fa_dtype in, fa_dtype outdt, const float* init, void* out,
                         int64_t head, int64_t nvec, int64_t n, bool vector_ok, const Tuning& tu, hipStream_t s) {
     if (in == FA_F32 && outdt == FA_F32)
@@ -963,8 +1031,8 @@ hipError_t launch_sync_phased_r(const ClientTable& t, int nc, int64_t head, int6
     static std::atomic<int> occ{-1};
     auto kern = fedavg_phased_kernel<T, T, false, REGS, true, TH>;
     if (!phased_fits(occ, kern, TH)) return hipErrorNotSupported;
-    return phased_enqueue(d, kern, TH, s, t, nc, (const float*)nullptr, (void*)nullptr, head, nvec, n,
-                          phased_rl_last(nvec, (int64_t)d->cus * TH, Phased<T, REGS, TH>::RL, Phased<T, REGS, TH>::RR));
+    return phased_enqueue(d, kern, TH, Phased<T, REGS, TH>::RL, Phased<T, REGS, TH>::RR, s, t, nc,
+                          (const float*)nullptr, (void*)nullptr, head, nvec, n);
 }
 
 template <typename T>

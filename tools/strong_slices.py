@@ -22,6 +22,8 @@ def main():
     import bench
     import torch
     fa = bench.load_pkg()
+    if os.environ.get("FA_BENCH_WALK"):  # A/B of fa_tuning.walk (process default, before any context)
+        fa.set_tuning(walk=int(os.environ["FA_BENCH_WALK"]))
     fa.lib()
     stream = torch.cuda.Stream()
     D, n = 32, 64 << 20
