@@ -201,8 +201,9 @@ def live_traffic(workload, timeout=150):
                         per[(r["Kernel_Name"], r.get("Grid_Size") or r.get("Grid_Size_X"))].append(float(r["Counter_Value"]))
             if not per:
                 return None, "live PMC pass %s: no %s records" % (counter, counter)
-            if kernel is None:  # the dominant kernel = the most fetched bytes (the reductions, not the fills)
-                kernel = max(per.items(), key=lambda kv: sum(kv[1]))[0]
+            if kernel is None:  # the dominant kernel = the most fetched bytes among the reductions
+                red = {k: v for k, v in per.items() if "fill_kernel" not in k[0] and "read_probe" not in k[0]}
+                kernel = max((red or per).items(), key=lambda kv: sum(kv[1]))[0]
             v = per.get(kernel)
             if not v:
                 return None, "live PMC pass %s: dominant kernel missing" % counter
@@ -336,6 +337,27 @@ class SyncSetup(Setup):
 
     def algo_bytes(self):
         return 2 * self.D * self.n * self.s_in
+
+
+def read_stream_peak(fa, torch, setup, stream, reps=7):
+    """Measured read-STREAM peak on this run's own client slots: a read-only launch over
+    the D buckets -- from one phase up the phased kernel itself with its output stream switched off
+    (fa_diag_read_stream) -- median of `reps` HIP-event timings on the launch stream.  GB/s of bytes
+    read; frac_of_read_stream = achieved / this, i.e. what the output stream costs on top of the reads."""
+    if setup.in_dt != fa.F32:
+        return None
+    n = setup.n - setup.n % 4
+    ptrs = setup.clients(0)
+    ms = []
+    for i in range(reps + 2):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        fa.diag_read_stream(ptrs, n, stream=stream)
+        b.record(stream)
+        b.synchronize()
+        if i >= 2:
+            ms.append(a.elapsed_time(b))
+    return round(setup.D * n * 4 / (statistics.median(ms) * 1e-3) / 1e9, 1)
 
 
 def timed_loop(torch, setup, steps, warmup, stream, dist, barrier):
@@ -593,6 +615,8 @@ def main():
 
     kavg = statistics.mean(kern_ms)
     achieved = setup.algo_bytes() / (kavg * 1e-3) / 1e9
+    read_peak = read_stream_peak(fa, torch, setup, stream) if args.layout == "range" and not under_profiler() \
+        else None
     committed = traffic_from_profile(args.workload, world, strong and args.layout == "range")
     traffic, traffic_src = live if live[0] is not None else committed
     line = {
@@ -625,7 +649,9 @@ def main():
                      "kernel_ms_median": round(statistics.median(kern_ms), 4),
                      "kernel": "rank %d's launch (%s)" % (rank, "its range of every bucket" if args.layout == "range"
                                                          else "its clients' local reduction"),
-                     "phased_meeting_timeouts": timeouts},
+                     "phased_meeting_timeouts": timeouts,
+                     "read_stream_peak": read_peak, "frac_of_read_stream":
+                         round(achieved / read_peak, 4) if read_peak else None},
         "cpu_baseline": cpu,
     }
     if world > 1:

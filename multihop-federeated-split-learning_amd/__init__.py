@@ -86,6 +86,7 @@ def lib():
         "fa_phased_timeouts": (I, [I, ctypes.POINTER(U64)]),
         "fa_reduce_device": (I, [P, I, P, P, I, S, I, P, I, I, P, P]),
         "fa_fill_uniform": (I, [P, S, I, U64, U32, U64, P]),
+        "fa_diag_read_stream": (I, [P, I, S, P]),  # diagnostics (outside fa.h)
         "fa_set_tuning": (I, [ctypes.POINTER(_Tuning)]),
         "fa_get_tuning": (I, [ctypes.POINTER(_Tuning)]),
     }
@@ -159,6 +160,13 @@ def sync_device(clients, weights, n, dtype, stream=None, gpu=0, ctx=None):
 
 def fill_uniform(dst, n, dtype, seed, client, idx0=0, stream=None):
     check(lib().fa_fill_uniform(_addr(dst), n, dtype, seed, client, idx0, _stream(stream)))
+
+
+def diag_read_stream(buffers, n, stream=None):
+    """fa_diag_read_stream (diagnostic, outside fa.h): one read-only launch over the fp32 device buffers
+    (n elements each, n % 4 == 0, 16-byte aligned) on `stream`; time it with events on that stream."""
+    arr = (ctypes.c_void_p * len(buffers))(*[_addr(b) for b in buffers])
+    check(lib().fa_diag_read_stream(arr, len(buffers), n, _stream(stream)))
 
 
 def _tuning_dict(t):

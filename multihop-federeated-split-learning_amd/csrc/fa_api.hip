@@ -1532,6 +1532,30 @@ int fa_phased_timeouts(int device, uint64_t* count) {
     return FA_OK;
 }
 
+// Diagnostic, not part of the ABI in fa.h: one read-stream probe launch over nc device buffers of n fp32
+// elements each (16-byte aligned, n a multiple of 4, nc <= 128) on `hip_stream`, enqueued; bench.py times
+// it with events on that stream (roofline.read_stream_peak).
+extern "C" int fa_diag_read_stream(const void* const* d_bufs, int nc, size_t n, void* hip_stream) {
+    g_err.clear();
+    if (!d_bufs || nc < 1 || nc > fa::kMaxClients || n % 4) return fail(FA_ERR_ARG, "bad read-stream arguments");
+    fa::ClientTable t{};
+    for (int k = 0; k < nc; ++k) {
+        if (!d_bufs[k] || (uintptr_t)d_bufs[k] % 16) return fail(FA_ERR_ARG, "buffer %d null or misaligned", k);
+        t.src[k] = d_bufs[k];
+    }
+    static float* sinks[64] = {};  // per device
+    static std::mutex mu;
+    int dev = 0;
+    FA_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return fail(FA_ERR_ARG, "device %d", dev);
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!sinks[dev]) FA_HIP(hipMalloc((void**)&sinks[dev], 256));
+    }
+    FA_HIP(fa::launch_read_probe(t, nc, (int64_t)(n / 4), sinks[dev], static_cast<hipStream_t>(hip_stream)));
+    return FA_OK;
+}
+
 // Diagnostic, not part of the ABI in fa.h: the per-workgroup timeline of the last phased launch on `device`
 // when the process runs with FA_TIMELINE=1 (tools/timeline.py).
 extern "C" int fa_diag_phased_timeline(int device, unsigned long long* out, int cap) {

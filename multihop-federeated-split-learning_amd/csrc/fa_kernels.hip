@@ -342,6 +342,7 @@ __device__ __forceinline__ void sync_scalar_edges(const ClientTable& t, int nc, 
 // every client slot in place.
 template <typename OUT, int V, bool SYNC>
 __device__ __forceinline__ void put(const ClientTable& t, int nc, void* out, int64_t e, const float* acc) {
+    if (!SYNC && !out) return;  // the read-stream probe (launch_read_probe): the same reads, no output stream
     if constexpr (SYNC) {
         for (int k = 0; k < nc; ++k) Out<OUT>::template store<V, kStSc1>(const_cast<void*>(t.src[k]), e, acc);
     } else {
@@ -1131,6 +1132,38 @@ bool phased_takes(fa_dtype in, int64_t nvec, int nc, const Tuning& tu) {
     PhasedDevice* d = phased_device();
     const int64_t lanes = (int64_t)d->cus * (in == FA_F32 ? 256 : 512);
     return (nvec + lanes - 1) / lanes >= (in == FA_F32 ? 8 : 4);
+}
+
+// Read-stream probe (SURVEY.md 8d "also report a measured read-STREAM peak").  From one phase up it is the
+// phased kernel itself with no output (launch_read_probe): the same reads, LDS staging and meetings,
+// no writes -- the best read rate measured on this chip for these buffers (simple grid-stride read
+// kernels reach ~6.95 TB/s, this ~7.2).  Below one phase, this kernel: every lane reads one 16-byte
+// vector of each of nc buffers per step with U loads in flight, over a grid of 8 workgroups per CU
+// walking the XCD eighths; the sum is stored only if it equals a value uniform[-1,1) inputs never
+// produce, so nothing is written and nothing is elided.
+__global__ __launch_bounds__(256) void read_probe_kernel(const ClientTable t, int nc, int64_t nvec, float* sink) {
+    const int64_t nb8 = gridDim.x >> 3;
+    const int64_t per = (nvec + nb8 * 8 * 256 - 1) / (nb8 * 8 * 256);  // vectors per lane
+    const int64_t slot = (int64_t)(blockIdx.x & 7) * nb8 + (blockIdx.x >> 3);
+    float acc = 0.0f;
+    for (int64_t i = 0; i < per; ++i) {
+        const int64_t v = (slot * per + i) * 256 + threadIdx.x;
+        if (v >= nvec) break;
+        float a[4];
+        chain_vec<float, 16, true, false>(t, nc, nullptr, v * 4, a);
+        acc += a[0] + a[1] + a[2] + a[3];
+    }
+    if (acc == 1.0e30f) sink[0] = acc;
+}
+
+hipError_t launch_read_probe(const ClientTable& t, int nc, int64_t nvec, float* sink, hipStream_t s) {
+    // from one phase up: the phased kernel itself with no output (its reads, LDS and meetings, no writes)
+    const hipError_t e = launch_phased_r<float, float, 192, 256>(t, nc, nullptr, nullptr, 0, nvec, nvec * 4, s);
+    if (e != hipErrorNotSupported) return e;
+    PhasedDevice* d = phased_device();
+    const int g = (d ? d->cus : 256) * 8;
+    hipLaunchKernelGGL(read_probe_kernel, dim3((unsigned)g), dim3(256), 0, s, t, nc, nvec, sink);
+    return hipGetLastError();
 }
 
 hipError_t launch_fill(void* dst, int64_t n, fa_dtype dt, uint64_t seed, uint32_t client, uint64_t idx0,
