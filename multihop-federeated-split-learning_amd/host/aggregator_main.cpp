@@ -469,9 +469,10 @@ int main(int argc, char** argv) {
         printf("{\"round\":%d,\"phase1\":{\"receive_s\":%.6f,\"reduce_s\":%.6f,\"bytes_in\":%zu,"
                "\"absorb_s\":%.6f,\"finalize_s\":%.6f,\"frame_s\":%.6f},"
                "\"phase2\":{\"receive_s\":%.6f,\"reduce_s\":%.6f,\"bytes_in\":%zu,\"layers\":%d,"
-               "\"absorb_s\":%.6f,\"finalize_s\":%.6f,\"frame_s\":%.6f,\"send_s\":%.6f}}\n",
+               "\"absorb_s\":%.6f,\"finalize_s\":%.6f,\"frame_s\":%.6f,\"send_s\":%.6f},"
+               "\"send_failures\":%llu}\n",
                round, recv1, red1, in1, s1.absorb_s, s1.finalize_s, s1.frame_s, recv2, red2, in2, L, s2.absorb_s,
-               s2.finalize_s, s2.frame_s, send2);
+               s2.finalize_s, s2.frame_s, send2, (unsigned long long)net.send_failures());
         fflush(stdout);
     }
     net.stop();

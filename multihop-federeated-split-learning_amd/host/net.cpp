@@ -9,6 +9,7 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <cerrno>
 #include <chrono>
 #include <cstring>
 #include <iostream>
@@ -80,6 +81,15 @@ bool send_all(int fd, const void* p, size_t n) {
         n -= (size_t)k;
     }
     return true;
+}
+
+// A kept connection whose peer has closed it (FIN or reset already seen): writing would succeed into the
+// socket buffer and lose the frame, so the sender reconnects instead.  The receivers never send data back,
+// so anything readable on a sender's socket means end of stream or an error.
+static bool peer_closed(int fd) {
+    char c;
+    const ssize_t k = ::recv(fd, &c, 1, MSG_PEEK | MSG_DONTWAIT);
+    return k == 0 || (k < 0 && errno != EAGAIN && errno != EWOULDBLOCK);
 }
 
 static bool recv_all(int fd, void* p, size_t n) {
@@ -315,7 +325,14 @@ void NetLayer::sender_loop(int i) {
         }
         int fd = -1;
         auto it = me.open.find(o.dest);
-        if (it != me.open.end()) fd = it->second;
+        if (it != me.open.end()) {
+            fd = it->second;
+            if (peer_closed(fd)) {
+                close(fd);
+                me.open.erase(it);
+                fd = -1;
+            }
+        }
         std::string host;
         int port;
         {
@@ -323,10 +340,22 @@ void NetLayer::sender_loop(int i) {
             host = routes_.host_for(o.dest);
             port = routes_.port_for(o.dest);
         }
+        const bool reused = fd >= 0;
         if (fd < 0) fd = connect_to(host, port, 100, 200);
+        bool sent = fd >= 0 && send_all(fd, o.bytes->data(), o.bytes->size());
+        if (!sent && reused) {
+            // the kept connection broke (the peer restarted or closed it): one fresh connection, the whole
+            // frame again -- the receiver drops the partial frame with the dead connection
+            close(fd);
+            me.open.erase(o.dest);
+            fd = connect_to(host, port, 100, 200);
+            sent = fd >= 0 && send_all(fd, o.bytes->data(), o.bytes->size());
+        }
         if (fd < 0) {
+            ++send_failures_;
             std::cerr << "[net] cannot reach node " << o.dest << " at " << host << ":" << port << "\n";
-        } else if (!send_all(fd, o.bytes->data(), o.bytes->size())) {
+        } else if (!sent) {
+            ++send_failures_;
             std::cerr << "[net] send to node " << o.dest << " failed\n";
             close(fd);
             me.open.erase(o.dest);

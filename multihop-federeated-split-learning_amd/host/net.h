@@ -91,6 +91,9 @@ public:
 
     RoutingTable& routes() { return routes_; }
     uint64_t bytes_received() const { return bytes_rx_; }
+    // Frames that could not be delivered (no connection after the retries, or a send that failed again on
+    // a fresh connection); the reference ignores send errors (network_layer.cpp:19-24).
+    uint64_t send_failures() const { return send_failures_; }
 
 private:
     struct Out {
@@ -130,6 +133,7 @@ private:
     double link_mbps_ = 0;
     std::atomic<bool> running_{false};
     std::atomic<uint64_t> bytes_rx_{0};
+    std::atomic<uint64_t> send_failures_{0};
     std::thread rx_;
     std::mutex m_rx_;
     std::condition_variable cv_rx_;

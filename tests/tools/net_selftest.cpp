@@ -11,11 +11,13 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <iostream>
+#include <memory>
 #include <sstream>
 #include <thread>
 #include <vector>
@@ -137,6 +139,32 @@ int main(int argc, char** argv) {
         }
         d->stop();
     }
+    // a kept connection whose receiver went away: the next frame goes over a fresh connection to the
+    // receiver that took its place (the reference keeps writing into the dead socket)
+    uint64_t send_failures = 0;
+    {
+        auto d7 = std::make_unique<NetLayer>(7, routes);
+        if (!d7->start()) ok = false;
+        agg.send(7, a, true);
+        agg.flush();
+        Receipt r1;
+        if (!d7->try_next_receipt(&r1, 20000)) ok = false;
+        d7->stop();
+        d7.reset();
+        std::this_thread::sleep_for(std::chrono::milliseconds(50));
+        auto d7b = std::make_unique<NetLayer>(7, routes);
+        if (!d7b->start()) ok = false;
+        agg.send(7, b, true);
+        agg.flush();
+        Receipt r2;
+        if (!(d7b->try_next_receipt(&r2, 20000) && r2.model_part == 3 && r2.blob_len == 1000)) {
+            std::cerr << "kept connection: the frame after the receiver restarted was lost\n";
+            ok = false;
+        }
+        d7b->stop();
+        send_failures = agg.send_failures();
+        if (send_failures) ok = false;
+    }
     agg.stop();
 
     // archive split copy: layout_into + values + seal_params == with_params_into
@@ -178,7 +206,8 @@ int main(int argc, char** argv) {
         checked_archive = ar.size();
     }
     printf("{\"ok\": %s, \"rounds\": %d, \"senders\": %d, \"pool_allocations\": %zu, \"live_after\": %zu, "
-           "\"archive_bytes\": %zu}\n",
-           ok ? "true" : "false", rounds, D, allocs, (size_t)live_allocs, checked_archive);
+           "\"archive_bytes\": %zu, \"send_failures\": %llu}\n",
+           ok ? "true" : "false", rounds, D, allocs, (size_t)live_allocs, checked_archive,
+           (unsigned long long)send_failures);
     return ok ? 0 : 1;
 }
