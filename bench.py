@@ -538,6 +538,10 @@ def main():
         ("ns_w%d" % world if strong and args.layout == "range" and args.workload == "northstar"
          and "ns_w%d" % world in WORKLOADS else None)
     live = (None, None)
+    if world > 1 and pmc_workload:
+        import torch  # counting devices does not initialise the GPU on this image
+        if torch.cuda.device_count() < world:  # rehearsal: the ranks' kernels are not the per-rank launch shape
+            pmc_workload = None
     if rank == 0 and pmc_workload and not args.no_live_pmc and not under_profiler():
         live = live_traffic(pmc_workload)
         if live[0] is None:
