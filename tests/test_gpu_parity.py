@@ -783,3 +783,21 @@ def test_phased_graph_replays(fa, O, torch_gpu):
         assert torch.equal(out.view(torch.int32), ref.view(torch.int32))
     t1 = eager_ms()
     assert t1 < 1.5 * t0 + 0.05, (t0, t1)
+
+
+@pytest.mark.parametrize("n,D", [(1_000_000, 8), (int(PHASE_ELEMS * 88 / 72 * 1.5), 6)])
+def test_read_stream_probe_reads_only(fa, O, torch_gpu, n, D):
+    """fa_diag_read_stream (bench's roofline.read_stream_peak): the simple probe below one phase, the phased
+    kernel with its output stream switched off above; it writes nothing -- every client buffer keeps its
+    bits and the kernel's output pointer stays null (put() returns before any store)."""
+    torch = torch_gpu
+    clients = [filled(fa, torch, n, False, 55, k) for k in range(D)]
+    before = [c.clone() for c in clients]
+    s = torch.cuda.Stream()
+    for _ in range(2):
+        fa.diag_read_stream(clients, n, stream=s)
+    s.synchronize()
+    for a, b in zip(clients, before):
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+    with pytest.raises(fa.FaError):
+        fa.diag_read_stream(clients, n + 1, stream=s)  # not a multiple of 4
