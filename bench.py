@@ -515,6 +515,8 @@ def main():
     ap.add_argument("--ctx-multi", default="", choices=["", "range", "rs"],
                     help="one process over every visible GPU through the C ABI: FA_SHARD_RANGE or FA_SHARD_CLIENT_RS "
                          "(RCCL reduce-scatter); prints one JSON object (a secondary of the N = 1 run)")
+    ap.add_argument("--ctx-gpus", type=int, default=0,
+                    help="with --ctx-multi: use the first K visible GPUs (default all)")
     ap.add_argument("--h2d", action="store_true",
                     help="with --ctx-multi: host-inclusive rounds (fa_submit_pinned of every client from host "
                          "memory, overlapped per GPU, + fa_finalize into host memory)")
@@ -730,11 +732,13 @@ def ctx_multi(args):
     fa = load_pkg()
     fa.lib()
     G = torch.cuda.device_count()
+    if args.ctx_gpus > 0:
+        G = min(G, args.ctx_gpus)
     D, n, in_dt, _, desc = WORKLOADS[args.workload]
     idt = fa.F32 if in_dt == "f32" else fa.BF16
     s_in = 4 if in_dt == "f32" else 2
     rs = args.ctx_multi == "rs"
-    agg = fa.Aggregator(G, rs=rs)
+    agg = fa.Aggregator(devices=list(range(G)), rs=rs)
     agg.define(1, n, idt, fa.F32, D, fa.FEDAVG)
     for g in range(G):
         with torch.cuda.device(g):
@@ -783,15 +787,19 @@ def ctx_multi_secondaries(n_dev, timeout=240):
     """On a node with several visible GPUs, the N = 1 run also times the in-process multi-GPU layouts over
     all of them (child processes, time-limited: a stalled collective cannot take the main line with it)."""
     res = {}
-    for layout, workload, h2d in (("range", "northstar", False), ("rs", "northstar", False), ("rs", "c4", False),
-                                  ("range", "c5", True)):
-        # the last: BASELINE C5, 128 x 1 GiB buckets arriving from host memory, H2D overlapped over every GPU's link
-        key = "ctx_%s_%s%s_%dgpu" % (layout, workload, "_h2d" if h2d else "", n_dev)
+    # BASELINE C4 is quoted on 4 GPUs (RCCL reduce-scatter), C5 on 8 (128 x 1 GiB buckets arriving from host
+    # memory, H2D overlapped over every GPU's link); the north star on all of them
+    for layout, workload, h2d, gpus in (("range", "northstar", False, n_dev), ("rs", "northstar", False, n_dev),
+                                        ("rs", "c4", False, min(4, n_dev)), ("rs", "c4", False, n_dev),
+                                        ("range", "c5", True, min(8, n_dev))):
+        key = "ctx_%s_%s%s_%dgpu" % (layout, workload, "_h2d" if h2d else "", gpus)
+        if key in res:
+            continue
         try:
             r = subprocess.run([sys.executable, os.path.abspath(__file__), "--ctx-multi", layout, "--workload",
-                                workload] + (["--h2d", "--steps", "3", "--warmup", "1"] if h2d else
-                                             ["--steps", "10", "--warmup", "2"]), capture_output=True, text=True,
-                               timeout=timeout)
+                                workload, "--ctx-gpus", str(gpus)] + (["--h2d", "--steps", "3", "--warmup", "1"] if h2d
+                                                                      else ["--steps", "10", "--warmup", "2"]),
+                               capture_output=True, text=True, timeout=timeout)
             res[key] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
                 {"error": "rc %d: %s" % (r.returncode, r.stderr[-300:])}
         except Exception as e:  # noqa: BLE001 -- reported, never fatal
