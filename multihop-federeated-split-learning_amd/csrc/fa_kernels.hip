@@ -354,7 +354,7 @@ template <typename IN, typename OUT, bool INIT, int REGS, bool SYNC, int TH>
 __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, int nc, const float* init,
                                                                        void* out, int64_t head, int64_t nvec, int64_t n,
                                                                        unsigned* sync, int slack, int rl_last,
-                                                                       int skew, int skew_last,
+                                                                       int skew, int skew_last, int last_meet,
                                                                        unsigned long long* tl) {
     constexpr int V = In<IN>::kVec, T = TH, RL = Phased<IN, REGS, TH>::RL, RR = Phased<IN, REGS, TH>::RR;
     constexpr int U = TH > 256 ? 8 : 16;  // loads in flight per wave (2 waves per SIMD at 512 threads)
@@ -449,7 +449,8 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
                 }
             }
         }
-        meet(p);
+        if (!last || last_meet) meet(p);
+        else __syncthreads();
 #pragma unroll 1
         for (int i = 0; i < rl; ++i) {
             const int64_t v = row_vec(i);
@@ -821,8 +822,16 @@ hipError_t phased_enqueue(PhasedDevice* d, Kern kern, int th, int RL, int RR, hi
     const int64_t phases = (nvec + per_phase - 1) / per_phase;
     const int rl_last = phased_rl_last(nvec - (phases - 1) * per_phase, lanes, RL, RR);
     const int skew_last = std::min({(skew + 1) / 2, rl_last, RL - rl_last});
+    // The last phase writes without the meeting: each workgroup as soon as it has read its share, beside
+    // the slower workgroups' last reads (one rank's share at 2 / 4 / 8 GPUs 0.664 / 0.344 / 0.173 ms
+    // against 0.670 / 0.346 / 0.176 with the meeting, north star, C3 and C4 unchanged; gpurun_out r02s36).
+    // FA_PHASED_LAST_MEET=1 restores it.
+    static const int last_meet = [] {
+        const char* e = std::getenv("FA_PHASED_LAST_MEET");
+        return e ? std::atoi(e) : 0;
+    }();
     hipLaunchKernelGGL(kern, dim3((unsigned)d->cus), dim3(th), 0, s, t, nc, init, out, head, nvec, n,
-                       d->sync + slot * kSyncStride, slack, rl_last, skew, skew_last, d->tl);
+                       d->sync + slot * kSyncStride, slack, rl_last, skew, skew_last, last_meet, d->tl);
     return hipGetLastError();
 }
 
