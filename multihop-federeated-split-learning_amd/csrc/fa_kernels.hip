@@ -817,7 +817,9 @@ hipError_t phased_enqueue(PhasedDevice* d, Kern kern, int th, int RL, int RR, hi
     const unsigned slot = (unsigned)(((uintptr_t)s >> 4) % kSyncSlots);
     const int slack = d->cus / 32;  // the write part starts once all but ~3% of the workgroups have arrived
     const int64_t lanes = (int64_t)d->cus * th;
-    const int skew = d->cus % 2 ? 0 : phased_skew(RL);
+    // the skew follows the whole chip's round-robin of workgroups over its 8 XCDs (blockIdx parity = XCD
+    // parity); a partition of the chip (fewer CUs per device) keeps the plain layout
+    const int skew = d->cus >= 256 && d->cus % 16 == 0 ? phased_skew(RL) : 0;
     const int64_t per_phase = lanes * (RL + RR) - (int64_t)(d->cus / 2) * th * skew;
     const int64_t phases = (nvec + per_phase - 1) / per_phase;
     const int rl_last = phased_rl_last(nvec - (phases - 1) * per_phase, lanes, RL, RR);
