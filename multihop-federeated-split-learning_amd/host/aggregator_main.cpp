@@ -56,6 +56,7 @@ struct Options {
     // failure detection: after stall_report_s without a receipt, name the data owners still missing;
     // after receipt_timeout_s (0 = wait forever, the reference's behaviour), give up with exit code 3
     double stall_report_s = 60, receipt_timeout_s = 0;
+    int rx_concurrency = 0;  // large receipts received at once (NetLayer::set_rx_concurrency; 0 = no limit)
     std::map<int, double> samples;  // client id -> n_k
 };
 
@@ -63,7 +64,7 @@ void usage() {
     std::cerr << "usage: fa_aggregator -i ID -d DATA_OWNERS -c COMPUTE_NODES [--mode fedavg|literal] [--gpus G]\n"
                  "       [--rounds R] [--port-base P] [--discover] [--link-mbps M] [--samples id:n,...]\n"
                  "       [--divisor K] [--last-layers L] [--no-pinned] [--layout range|rs] [--rs-chunks C]\n"
-                 "       [--eager] [--stall-report S] [--receipt-timeout S]\n";
+                 "       [--eager] [--stall-report S] [--receipt-timeout S] [--rx-concurrency K]\n";
 }
 
 bool parse_args(int argc, char** argv, Options* o) {
@@ -90,6 +91,7 @@ bool parse_args(int argc, char** argv, Options* o) {
         else if (a == "--rs-chunks") o->rs_chunks = std::atoi(val("--rs-chunks"));
         else if (a == "--stall-report") o->stall_report_s = std::atof(val("--stall-report"));
         else if (a == "--receipt-timeout") o->receipt_timeout_s = std::atof(val("--receipt-timeout"));
+        else if (a == "--rx-concurrency") o->rx_concurrency = std::atoi(val("--rx-concurrency"));
         else if (a == "--layout") {
             std::string l = val("--layout");
             if (l == "rs") o->rs = true;
@@ -395,6 +397,7 @@ int main(int argc, char** argv) {
     }
     NetLayer net(o.id, RoutingTable(o.port_base));
     net.set_link_mbps(o.link_mbps);
+    net.set_rx_concurrency(o.rx_concurrency);
     std::string err;
     if (o.discover && !net.find_init(600, &err)) {
         std::cerr << "[aggregator] discovery failed: " << err << "\n";

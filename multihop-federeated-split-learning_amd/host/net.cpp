@@ -169,6 +169,10 @@ void NetLayer::stop() {
         std::lock_guard<std::mutex> lk(m_tx_);
     }
     cv_tx_.notify_all();
+    {
+        std::lock_guard<std::mutex> lk(m_gate_);
+    }
+    cv_gate_.notify_all();  // readers waiting for a receive turn
     // wake the receiver's poll/accept, and close the socket only after it has left: closing under it
     // raced its reads of listen_fd_ (TSan, tests/test_host_sanitizers.py) and could hand it a reused fd
     if (listen_fd_ >= 0) shutdown(listen_fd_, SHUT_RDWR);
@@ -278,13 +282,68 @@ void NetLayer::receiver_loop() {
     reap(true);
 }
 
+bool NetLayer::gate_enter(uint64_t seq) {
+    std::unique_lock<std::mutex> lk(m_gate_);
+    gate_wait_.insert(seq);
+    cv_gate_.wait(lk, [&] { return !running_ || (gate_active_ < gate_limit_ && *gate_wait_.begin() == seq); });
+    gate_wait_.erase(seq);
+    if (!running_) {
+        cv_gate_.notify_all();
+        return false;
+    }
+    ++gate_active_;
+    cv_gate_.notify_all();  // the next position may be admitted too
+    return true;
+}
+
+void NetLayer::gate_leave() {
+    {
+        std::lock_guard<std::mutex> lk(m_gate_);
+        --gate_active_;
+    }
+    cv_gate_.notify_all();
+}
+
+// recv_frame with the receive gate (set_rx_concurrency): the length first, then -- for a large frame,
+// once its turn has come -- the body.  A turn is given up when the sender stalls.
+std::shared_ptr<Bytes> NetLayer::recv_frame_gated(int fd, uint64_t seq) {
+    int32_t len = 0;
+    if (!recv_all(fd, &len, 4) || len <= 0) return nullptr;
+    bool gated = gate_limit_ > 0 && (size_t)len >= kGateBytes;
+    if (gated && !gate_enter(seq)) return nullptr;
+    auto b = new_frame_buffer((size_t)len);
+    char* c = reinterpret_cast<char*>(b->data());
+    size_t n = (size_t)len;
+    auto last = std::chrono::steady_clock::now();
+    while (n > 0) {
+        pollfd p{fd, POLLIN, 0};
+        const int r = poll(&p, 1, 200);
+        if (r < 0 && errno != EINTR) break;
+        if (r <= 0) {
+            if (!running_) break;
+            if (gated && std::chrono::steady_clock::now() - last > std::chrono::milliseconds(kGateStallMs)) {
+                gate_leave();  // the owner stalled: let the others through
+                gated = false;
+            }
+            continue;
+        }
+        const ssize_t k = ::recv(fd, c, n, 0);
+        if (k <= 0) break;
+        c += k;
+        n -= (size_t)k;
+        last = std::chrono::steady_clock::now();
+    }
+    if (gated) gate_leave();
+    return n == 0 ? b : nullptr;
+}
+
 // One connection: one frame (the reference's default, save_connection 0), or frames until EOF when
 // the sender keeps the connection open (save_connection 1).
 void NetLayer::reader_loop(Conn* c) {
     const int fd = c->fd;
     uint64_t seq = c->seq0;
     for (;;) {
-        auto text = recv_frame(fd);
+        auto text = gate_limit_ > 0 ? recv_frame_gated(fd, seq) : recv_frame(fd);
         if (!text) {
             publish(seq, Item{});  // release the FIFO position
             break;

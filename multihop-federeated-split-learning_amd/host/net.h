@@ -32,6 +32,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -80,6 +81,14 @@ public:
 
     // Link emulation: receipts are held until t_start + bytes*8/(mbps*1e6) s (0 = off).
     void set_link_mbps(double mbps) { link_mbps_ = mbps; }
+    // Receive at most k frames of >= kGateBytes at a time, granted in FIFO order (0 = no limit).  Owners
+    // that send at once share the link and, unlimited, all finish together at the end of the phase -- so
+    // every receipt's H2D copy would start then.  Gated, receipts complete one after another and their
+    // copies overlap the rest of the phase.  A gated receive that makes no progress for kGateStallMs gives
+    // its turn up (a stalled owner does not hold the others back).
+    void set_rx_concurrency(int k) { gate_limit_ = k; }
+    static constexpr size_t kGateBytes = 8u << 20;
+    static constexpr int kGateStallMs = 2000;
 
     Receipt next_receipt();      // blocking FIFO pop (check_new_task for a data owner, :392-409)
     Message next_refactor();     // blocking (check_new_refactor_task, :481-493)
@@ -125,6 +134,9 @@ private:
     void reader_loop(Conn* c);
     void sender_loop(int i);
     Item parse_frame(std::shared_ptr<Bytes> text, bool* keep);
+    std::shared_ptr<Bytes> recv_frame_gated(int fd, uint64_t seq);
+    bool gate_enter(uint64_t seq);
+    void gate_leave();
 
     int my_id_;
     RoutingTable routes_;
@@ -132,6 +144,11 @@ private:
     int port_ = -1, listen_fd_ = -1;
     double link_mbps_ = 0;
     std::atomic<bool> running_{false};
+    int gate_limit_ = 0;
+    std::mutex m_gate_;
+    std::condition_variable cv_gate_;
+    int gate_active_ = 0;            // under m_gate_
+    std::set<uint64_t> gate_wait_;   // under m_gate_: FIFO positions waiting for a turn
     std::atomic<uint64_t> bytes_rx_{0};
     std::atomic<uint64_t> send_failures_{0};
     std::thread rx_;

@@ -167,6 +167,53 @@ int main(int argc, char** argv) {
     }
     agg.stop();
 
+    // receive gate: 6 owners sending 9 MiB frames at once, at most 2 received at a time, granted in
+    // accept order; every frame arrives whole and the FIFO order is the accept order
+    {
+        RoutingTable groutes(base + 100);
+        NetLayer gagg(-1, groutes);
+        gagg.set_rx_concurrency(2);
+        if (!gagg.start()) {
+            std::cerr << "gate: bind failed\n";
+            ok = false;
+        } else {
+            const size_t big = 9u << 20;
+            std::vector<std::shared_ptr<Bytes>> gf;
+            for (int k = 0; k < D; ++k) gf.push_back(make_frame(200 + k, 2, big, (uint8_t)(77 + k)));
+            std::vector<std::thread> th;
+            for (int k = 0; k < D; ++k)
+                th.emplace_back([&, k] {
+                    const int fd = connect_to("127.0.0.1", groutes.port_for(-1), 50, 100);
+                    if (fd < 0 || !send_all(fd, gf[k]->data(), gf[k]->size())) ok = false;
+                    if (fd >= 0) close(fd);
+                });
+            std::vector<char> seen(D, 0);
+            for (int i = 0; i < D; ++i) {
+                Receipt rc;
+                if (!gagg.try_next_receipt(&rc, 20000)) {
+                    std::cerr << "gate: receipt " << i << " missing\n";
+                    ok = false;
+                    break;
+                }
+                const int k = rc.client_id - 200;
+                if (k < 0 || k >= D || seen[k] || rc.blob_len != big) {
+                    ok = false;
+                    continue;
+                }
+                seen[k] = 1;
+                const char* v = (const char*)rc.blob();
+                for (size_t j = 0; j < big; j += 65537)
+                    if (v[j] != (char)((uint8_t)(77 + k) + j * 7)) {
+                        std::cerr << "gate: payload mismatch client " << k << "\n";
+                        ok = false;
+                        break;
+                    }
+            }
+            for (auto& t : th) t.join();
+            gagg.stop();
+        }
+    }
+
     // archive split copy: layout_into + values + seal_params == with_params_into
     size_t checked_archive = 0;
     if (argc > 1) {
