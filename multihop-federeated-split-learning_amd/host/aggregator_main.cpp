@@ -56,7 +56,10 @@ struct Options {
     // failure detection: after stall_report_s without a receipt, name the data owners still missing;
     // after receipt_timeout_s (0 = wait forever, the reference's behaviour), give up with exit code 3
     double stall_report_s = 60, receipt_timeout_s = 0;
-    int rx_concurrency = 0;  // large receipts received at once (NetLayer::set_rx_concurrency; 0 = no limit)
+    // large receipts received at once (NetLayer::set_rx_concurrency; 0 = no limit).  C4 at D = 64 over
+    // loopback (gpurun_out r02s40), owner-view round: unlimited 3.15-3.32 s, 4 at a time 2.05-2.48 s,
+    // 16 at a time 2.15-2.31 s -- the phase end drops from 0.48-0.51 s to 0.04-0.17 s
+    int rx_concurrency = 8;
     std::map<int, double> samples;  // client id -> n_k
 };
 
