@@ -78,8 +78,8 @@ def _large_parts(d):
     import torch.nn as nn
     torch.manual_seed(1)
     parts = {1: nn.Sequential(nn.Conv2d(3, 64, 3), nn.ReLU(), nn.Conv2d(64, 64, 3)),
-             2: nn.Sequential(nn.Linear(1024, 1536), nn.ReLU()),
-             3: nn.Sequential(nn.Linear(1536, 1000), nn.ReLU(), nn.Linear(1000, 10))}
+             2: nn.Sequential(nn.Linear(1024, 2304), nn.ReLU()),  # 9.4 MB: above the receive gate's 8 MiB
+             3: nn.Sequential(nn.Linear(2304, 1000), nn.ReLU(), nn.Linear(1000, 10))}
     for mp, m in parts.items():
         torch.jit.save(torch.jit.script(m), os.path.join(d, "mp%d_client0.pt" % mp))
     return {mp: sum(p.numel() for p in m.parameters()) for mp, m in parts.items()}
@@ -90,6 +90,8 @@ def _large_parts(d):
     (True, True, ["--eager"]),                          # chains advance as the in-order receipts land
     (True, False, ["--eager"]),
     (True, False, ["--layout", "rs", "--rs-chunks", "3"]),  # RCCL reduce-scatter layout (one GPU: a copy)
+    (True, False, ["--rx-concurrency", "2"]),           # 6 owners at once, 2 large receipts received at a time
+    (False, False, ["--rx-concurrency", "0"]),          # no receive gate
 ])
 def test_multi_mb_parts_concurrent_owners(torch_gpu, tmp_path, pinned, sequential, extra):
     """D=6 owners sending at once (or one after another) multi-MB parts: pinned zero-copy ingest
