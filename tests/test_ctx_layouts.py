@@ -69,17 +69,19 @@ def test_rs_layout_literal_and_errors(fa, O, torch_gpu):
             agg.sync_states(1)
 
 
-@pytest.mark.parametrize("G,D,chunks", [(2, 7, 8), (4, 7, 3), (3, 2, 5), (4, 9, 1)])
-def test_rs_layout_multi_gpu_tolerance(fa, O, torch_gpu, G, D, chunks):
+@pytest.mark.parametrize("G,D,chunks,bf16", [(2, 7, 8, False), (4, 7, 3, False), (3, 2, 5, False), (4, 9, 1, False),
+                                             (2, 5, 4, True), (3, 6, 2, True)])
+def test_rs_layout_multi_gpu_tolerance(fa, O, torch_gpu, G, D, chunks, bf16):
     """G shards: clients dealt to the GPUs (a GPU may hold none: D < G), every GPU's shard holds its
     cyclic blocks; the whole result within 1e-6 of sum_k |w_k x_k| of the oracle's ordered chain (the
-    exchange adds per-GPU partials); the device-resident round on the same slots agrees bit for bit."""
+    exchange adds per-GPU partials; bf16 inputs exchange fp32 partials too); the device-resident round
+    on the same slots agrees bit for bit."""
     n = 1_234_567
     w = O.weights(D)
-    xs = host_clients(O, 71, D, n)
+    xs = host_clients(O, 71, D, n, bf16)
     with rs_ctx(fa, G) as agg:
         agg.set_tuning(rs_chunks=chunks)
-        agg.define(1, n, fa.F32, fa.F32, D, fa.FEDAVG)
+        agg.define(1, n, fa.BF16 if bf16 else fa.F32, fa.F32, D, fa.FEDAVG)
         for k in range(D):
             agg.submit(1, k, xs[k], w[k])
         got = agg.finalize(1)
@@ -87,7 +89,8 @@ def test_rs_layout_multi_gpu_tolerance(fa, O, torch_gpu, G, D, chunks):
             agg.reduce(1, w)
         assert_bits(agg.copy_output(1), got)
     ref = O.fedavg(xs, w)
-    absw = sum(abs(np.float64(wk)) * np.abs(x.astype(np.float64)) for wk, x in zip(w, xs))
+    vals = [O.bf16_to_f32(x) if bf16 else x for x in xs]
+    absw = sum(abs(np.float64(wk)) * np.abs(x.astype(np.float64)) for wk, x in zip(w, vals))
     err = np.abs(got.astype(np.float64) - ref) / (1e-6 * absw + 1e-30)
     assert np.all(err <= 1.0), float(err.max())
 
