@@ -60,6 +60,7 @@ struct Options {
     // loopback (gpurun_out r02s40), owner-view round: unlimited 3.15-3.32 s, 4 at a time 2.05-2.48 s,
     // 16 at a time 2.15-2.31 s -- the phase end drops from 0.48-0.51 s to 0.04-0.17 s
     int rx_concurrency = 8;
+    int senders = 8;  // fan-out sender threads (each destination keeps to one, in order)
     std::map<int, double> samples;  // client id -> n_k
 };
 
@@ -67,7 +68,8 @@ void usage() {
     std::cerr << "usage: fa_aggregator -i ID -d DATA_OWNERS -c COMPUTE_NODES [--mode fedavg|literal] [--gpus G]\n"
                  "       [--rounds R] [--port-base P] [--discover] [--link-mbps M] [--samples id:n,...]\n"
                  "       [--divisor K] [--last-layers L] [--no-pinned] [--layout range|rs] [--rs-chunks C]\n"
-                 "       [--eager] [--stall-report S] [--receipt-timeout S] [--rx-concurrency K]\n";
+                 "       [--eager] [--stall-report S] [--receipt-timeout S] [--rx-concurrency K]\n"
+                 "       [--senders S]\n";
 }
 
 bool parse_args(int argc, char** argv, Options* o) {
@@ -95,6 +97,7 @@ bool parse_args(int argc, char** argv, Options* o) {
         else if (a == "--stall-report") o->stall_report_s = std::atof(val("--stall-report"));
         else if (a == "--receipt-timeout") o->receipt_timeout_s = std::atof(val("--receipt-timeout"));
         else if (a == "--rx-concurrency") o->rx_concurrency = std::atoi(val("--rx-concurrency"));
+        else if (a == "--senders") o->senders = std::atoi(val("--senders"));
         else if (a == "--layout") {
             std::string l = val("--layout");
             if (l == "rs") o->rs = true;
@@ -398,7 +401,7 @@ int main(int argc, char** argv) {
             [](char* p) { fa_host_free(p); }, true);
         set_frame_allocator([pool](size_t n) { return pool->get(n); });
     }
-    NetLayer net(o.id, RoutingTable(o.port_base));
+    NetLayer net(o.id, RoutingTable(o.port_base), o.senders);
     net.set_link_mbps(o.link_mbps);
     net.set_rx_concurrency(o.rx_concurrency);
     std::string err;
