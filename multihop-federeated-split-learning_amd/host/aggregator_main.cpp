@@ -188,16 +188,24 @@ public:
             std::exit(1);
         }
         Bucket& b = buckets_[r.model_part];
+        const int es = ar.param_elem_size();  // the bucket dtype: fp32 (the reference) or bf16 (config C3)
         if (!b.defined) {
-            if (!ar.params_are_float()) {
-                std::cerr << "[aggregator] bucket " << r.model_part << " has non-fp32 parameters\n";
+            if (es == 0) {
+                std::cerr << "[aggregator] bucket " << r.model_part << ": parameters not all fp32 or all bf16\n";
+                std::exit(1);
+            }
+            if (es == 2 && o_.rs) {
+                std::cerr << "[aggregator] --layout rs exchanges fp32 partials into an fp32 result: bucket "
+                          << r.model_part << " has bf16 parameters (use the range layout)\n";
                 std::exit(1);
             }
             b.numel = (size_t)ar.param_numel();
-            FA_CHECK(fa_bucket_define(ctx_, r.model_part, b.numel, FA_F32, FA_F32, o_.data_owners, o_.mode));
+            b.elem = es;
+            const fa_dtype dt = es == 4 ? FA_F32 : FA_BF16;
+            FA_CHECK(fa_bucket_define(ctx_, r.model_part, b.numel, dt, dt, o_.data_owners, o_.mode));
             b.defined = true;
-        } else if ((size_t)ar.param_numel() != b.numel) {
-            std::cerr << "[aggregator] bucket " << r.model_part << " changed size\n";
+        } else if ((size_t)ar.param_numel() != b.numel || es != b.elem) {
+            std::cerr << "[aggregator] bucket " << r.model_part << " changed size or dtype\n";
             std::exit(1);
         }
         const int slot = slot_of(r.client_id);
@@ -213,8 +221,8 @@ public:
                                           weight_of(r.client_id)));
             }
         } else {  // strided parameters: flatten first
-            std::vector<float> flat(b.numel);
-            if (!ar.gather_params(flat.data(), &err)) {
+            std::vector<uint8_t> flat(b.numel * (size_t)b.elem);
+            if (!ar.gather_param_bytes(flat.data(), &err)) {
                 std::cerr << "[aggregator] " << err << "\n";
                 std::exit(1);
             }
@@ -258,10 +266,10 @@ public:
             ar.seal_params((uint8_t*)values);
         } else {  // strided parameters: through a flat copy
             const auto t1 = std::chrono::steady_clock::now();
-            std::vector<float> out(b.numel);
+            std::vector<uint8_t> out(b.numel * (size_t)b.elem);
             FA_CHECK(fa_finalize(ctx_, mp, out.data()));
             t_fin = secs_since(t1);
-            if (!ar.with_params_into(out.data(), (uint8_t*)values, &err)) {
+            if (!ar.with_param_bytes_into(out.data(), (uint8_t*)values, &err)) {
                 std::cerr << "[aggregator] reply for part " << mp << ": " << err << "\n";
                 std::exit(1);
             }
@@ -321,6 +329,7 @@ private:
     struct Bucket {
         bool defined = false;
         size_t numel = 0, bytes_in = 0;
+        int elem = 4;  // bytes per parameter element: 4 fp32, 2 bf16
         Receipt last;
         std::vector<std::shared_ptr<const Bytes>> held;  // pinned frames DMA'd from, until finalize
         std::set<int> arrived;  // client ids received this round

@@ -592,38 +592,62 @@ bool TorchArchive::params_are_float() const {
     return true;
 }
 
+int TorchArchive::param_elem_size() const {
+    if (params_.empty()) return 4;
+    const std::string& st = params_[0].storage_type;
+    if (st != "FloatStorage" && st != "BFloat16Storage") return 0;
+    for (auto& t : params_)
+        if (t.storage_type != st) return 0;
+    return st == "FloatStorage" ? 4 : 2;
+}
+
 bool TorchArchive::param_segments(std::vector<const void*>* ptrs, std::vector<size_t>* bytes) const {
     ptrs->clear();
     bytes->clear();
+    const int es = param_elem_size();
+    if (!es) return false;
     for (auto& t : params_) {
-        if (!t.contiguous || t.storage_type != "FloatStorage") return false;
+        if (!t.contiguous) return false;
         if (t.numel == 0) continue;
         ptrs->push_back(t.data);
-        bytes->push_back((size_t)t.numel * 4);
+        bytes->push_back((size_t)t.numel * (size_t)es);
+    }
+    return true;
+}
+
+// Element-size-agnostic walk of one (possibly strided) parameter in row-major index order:
+// fn(e, off) for element e at element offset `off` from the parameter's first element.
+template <class Fn>
+static void walk_param(const TensorView& t, Fn fn) {
+    std::vector<int64_t> idx(t.sizes.size(), 0);
+    for (int64_t e = 0; e < t.numel; ++e) {
+        int64_t off = 0;
+        for (size_t d = 0; d < idx.size(); ++d) off += idx[d] * t.strides[d];
+        fn(e, off);
+        for (size_t d = idx.size(); d-- > 0;) {
+            if (++idx[d] < t.sizes[d]) break;
+            idx[d] = 0;
+        }
+    }
+}
+
+bool TorchArchive::gather_param_bytes(uint8_t* dst, std::string* err) const {
+    const int es = param_elem_size();
+    if (!es) return fail(err, "parameters are not all fp32 or all bf16");
+    for (auto& t : params_) {
+        if (t.contiguous) {
+            std::memcpy(dst, t.data, (size_t)t.numel * (size_t)es);
+        } else {
+            walk_param(t, [&](int64_t e, int64_t off) { std::memcpy(dst + e * es, t.data + off * es, (size_t)es); });
+        }
+        dst += (size_t)t.numel * (size_t)es;
     }
     return true;
 }
 
 bool TorchArchive::gather_params(float* dst, std::string* err) const {
-    for (auto& t : params_) {
-        if (t.storage_type != "FloatStorage") return fail(err, "parameter " + t.name + " is not fp32");
-        if (t.contiguous) {
-            std::memcpy(dst, t.data, (size_t)t.numel * 4);
-        } else {  // strided: walk the index space in row-major order
-            std::vector<int64_t> idx(t.sizes.size(), 0);
-            for (int64_t e = 0; e < t.numel; ++e) {
-                int64_t off = 0;
-                for (size_t d = 0; d < idx.size(); ++d) off += idx[d] * t.strides[d];
-                std::memcpy(dst + e, t.data + off * 4, 4);
-                for (size_t d = idx.size(); d-- > 0;) {
-                    if (++idx[d] < t.sizes[d]) break;
-                    idx[d] = 0;
-                }
-            }
-        }
-        dst += t.numel;
-    }
-    return true;
+    if (param_elem_size() != 4) return fail(err, "parameters are not all fp32");
+    return gather_param_bytes(reinterpret_cast<uint8_t*>(dst), err);
 }
 
 bool TorchArchive::with_params(const float* src, std::string* out, std::string* err) const {
@@ -669,33 +693,30 @@ uint32_t crc32_parallel(const uint8_t* p, size_t n) {
 }  // namespace
 
 bool TorchArchive::with_params_into(const float* src, uint8_t* o, std::string* err) const {
+    if (param_elem_size() != 4) return fail(err, "parameters are not all fp32");
+    return with_param_bytes_into(reinterpret_cast<const uint8_t*>(src), o, err);
+}
+
+bool TorchArchive::with_param_bytes_into(const uint8_t* src, uint8_t* o, std::string* err) const {
+    const int es = param_elem_size();
+    if (!es) return fail(err, "parameters are not all fp32 or all bf16");
     std::vector<void*> dsts;
     std::vector<size_t> bytes;
-    if (layout_into(o, &dsts, &bytes, nullptr)) {  // contiguous fp32 parameters: copy the gaps, then the values
+    if (layout_into(o, &dsts, &bytes, nullptr)) {  // contiguous parameters: copy the gaps, then the values
         for (size_t k = 0; k < dsts.size(); ++k) {
             uint8_t* d = (uint8_t*)dsts[k];
-            const uint8_t* s0 = (const uint8_t*)src;
+            const uint8_t* s0 = src;
             parallel_ranges(bytes[k], 16u << 20, [&](size_t lo, size_t hi) { std::memcpy(d + lo, s0 + lo, hi - lo); });
-            src += bytes[k] / 4;
+            src += bytes[k];
         }
         seal_params(o);
         return true;
     }
     parallel_ranges(size_, 16u << 20, [&](size_t lo, size_t hi) { std::memcpy(o + lo, base_ + lo, hi - lo); });
     for (auto& t : params_) {
-        if (t.storage_type != "FloatStorage") return fail(err, "parameter " + t.name + " is not fp32");
         uint8_t* d = o + (t.data - base_);
-        std::vector<int64_t> idx(t.sizes.size(), 0);
-        for (int64_t e = 0; e < t.numel; ++e) {
-            int64_t off = 0;
-            for (size_t k = 0; k < idx.size(); ++k) off += idx[k] * t.strides[k];
-            std::memcpy(d + off * 4, src + e, 4);
-            for (size_t k = idx.size(); k-- > 0;) {
-                if (++idx[k] < t.sizes[k]) break;
-                idx[k] = 0;
-            }
-        }
-        src += t.numel;
+        walk_param(t, [&](int64_t e, int64_t off) { std::memcpy(d + off * es, src + e * es, (size_t)es); });
+        src += (size_t)t.numel * (size_t)es;
     }
     seal_params(o);
     return true;
@@ -704,10 +725,11 @@ bool TorchArchive::with_params_into(const float* src, uint8_t* o, std::string* e
 bool TorchArchive::layout_into(uint8_t* o, std::vector<void*>* dsts, std::vector<size_t>* bytes,
                                std::string* err) const {
     std::vector<std::pair<size_t, size_t>> holes;  // [lo, hi) of each parameter's values
+    const int es = param_elem_size();
+    if (!es) return fail(err, "parameters are not all fp32 or all bf16");
     for (auto& t : params_) {
-        if (t.storage_type != "FloatStorage") return fail(err, "parameter " + t.name + " is not fp32");
         if (!t.contiguous) return fail(err, "parameter " + t.name + " is strided");
-        holes.push_back({(size_t)(t.data - base_), (size_t)(t.data - base_) + (size_t)t.numel * 4});
+        holes.push_back({(size_t)(t.data - base_), (size_t)(t.data - base_) + (size_t)t.numel * (size_t)es});
     }
     std::vector<std::pair<size_t, size_t>> sorted = holes;
     std::sort(sorted.begin(), sorted.end());

@@ -54,12 +54,19 @@ public:
     const std::vector<TensorView>& buffers() const { return buffers_; } // named_buffers(true) order
     int64_t param_numel() const;
     bool params_are_float() const;
+    // Bytes per parameter element when every parameter is fp32 (4) or every one is bf16 (2); 0 when
+    // they are mixed or of another type (the bucket dtype of a receipt).
+    int param_elem_size() const;
 
-    // Contiguous pieces of the parameter bucket, in order (one per contiguous fp32 param):
-    // a gather list for fa_submit_gather.  Returns false if some param is not contiguous fp32.
+    // Contiguous pieces of the parameter bucket, in order (one per contiguous param, fp32 or bf16
+    // throughout): a gather list for fa_submit_gather.  False if some param is strided or the types mix.
     bool param_segments(std::vector<const void*>* ptrs, std::vector<size_t>* bytes) const;
     // Strided-safe copy of all parameters (as fp32) into dst[param_numel()].
     bool gather_params(float* dst, std::string* err) const;
+    // The same for either bucket dtype: param_numel() * param_elem_size() bytes, in their own type.
+    bool gather_param_bytes(uint8_t* dst, std::string* err) const;
+    // with_params_into for either bucket dtype: src holds the values in the parameters' own type.
+    bool with_param_bytes_into(const uint8_t* src, uint8_t* dst, std::string* err) const;
     // A copy of the archive bytes with every parameter replaced by src (fp32, named order) and
     // the CRC-32 of every rewritten record updated in its data descriptor and central directory.
     bool with_params(const float* src, std::string* out, std::string* err) const;
@@ -68,7 +75,8 @@ public:
     // The same in two steps, for a producer that writes the values itself (e.g. a D2H copy straight
     // into the outgoing frame): layout_into copies everything but the parameter values into dst and
     // returns where each parameter's values go (named_parameters order; false when a parameter is
-    // strided or not fp32); seal_params then recomputes the CRC-32 of the parameter records.
+    // strided or the parameters are not all fp32 or all bf16); seal_params then recomputes the CRC-32
+    // of the parameter records.
     bool layout_into(uint8_t* dst, std::vector<void*>* param_dsts, std::vector<size_t>* param_bytes,
                      std::string* err) const;
     void seal_params(uint8_t* dst) const;

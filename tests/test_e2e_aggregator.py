@@ -71,9 +71,10 @@ def test_lenet_rounds_over_tcp(torch_gpu, mode, D, rounds):
             agg.kill()
 
 
-def _large_parts(d):
+def _large_parts(d, bf16=False):
     """Model-part archives of a few MB (torch.jit.save: the same zip/pickle layout as torch::save), big
-    enough that the aggregator receives them into its pooled pinned buffers and replies from them."""
+    enough that the aggregator receives them into its pooled pinned buffers and replies from them;
+    bf16 parameters (BFloat16Storage records) with bf16=True."""
     import torch
     import torch.nn as nn
     torch.manual_seed(1)
@@ -81,6 +82,8 @@ def _large_parts(d):
              2: nn.Sequential(nn.Linear(1024, 2304), nn.ReLU()),  # 9.4 MB: above the receive gate's 8 MiB
              3: nn.Sequential(nn.Linear(2304, 1000), nn.ReLU(), nn.Linear(1000, 10))}
     for mp, m in parts.items():
+        if bf16:
+            m = m.to(torch.bfloat16)
         torch.jit.save(torch.jit.script(m), os.path.join(d, "mp%d_client0.pt" % mp))
     return {mp: sum(p.numel() for p in m.parameters()) for mp, m in parts.items()}
 
@@ -148,6 +151,52 @@ def test_missing_owner_is_reported_and_times_out(torch_gpu, drop_phase):
         else:
             assert "phase 2" in stalls[0] and "part 2: 1 owner(s) [2]; part 3: 1 owner(s) [2]" in stalls[0]
             assert sum(l.startswith("{") for l in out.splitlines()) == 0  # no round completed
+    finally:
+        if agg.poll() is None:
+            agg.kill()
+
+
+@pytest.mark.parametrize("extra", [[], ["--eager"], ["--mode", "literal"]])
+def test_bf16_parts_over_tcp(torch_gpu, tmp_path, extra):
+    """BASELINE config C3's dtype through the drop-in process: owners send bf16 model parts
+    (BFloat16Storage records); the aggregator reduces them in bf16 buckets (fp32 chain, one rounding)
+    and replies in bf16, bit-exact against the oracle's bf16 FedAvg (or the literal last/500 in bf16)."""
+    sizes = _large_parts(str(tmp_path), bf16=True)
+    D, rounds = 5, 2
+    base = pick_base()
+    literal = "literal" in extra
+    agg = subprocess.Popen([AGG, "-i", "-1", "-d", str(D), "-c", "1", "--rounds", str(rounds), "--port-base",
+                            str(base)] + extra, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        time.sleep(0.5)
+        r = subprocess.run([OWNERS, "--blobs", str(tmp_path), "--parts", "1,2,3", "-d", str(D), "-c", "1",
+                            "--rounds", str(rounds), "--port-base", str(base), "--model-name", "1", "--start", "9",
+                            "--end", "3"] + (["--mode", "literal"] if literal else []),
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res = json.loads(r.stdout.strip().splitlines()[-1])
+        assert res["ok"] and res["checked_elems"] == rounds * D * sum(sizes.values())
+        out, err = agg.communicate(timeout=60)
+        assert agg.returncode == 0, err[-2000:]
+    finally:
+        if agg.poll() is None:
+            agg.kill()
+
+
+def test_bf16_parts_rejected_by_rs_layout(torch_gpu, tmp_path):
+    """The rs layout exchanges fp32 partials into an fp32 result, which cannot become a bf16 reply: the
+    aggregator says so and exits instead of replying in another dtype."""
+    _large_parts(str(tmp_path), bf16=True)
+    base = pick_base()
+    agg = subprocess.Popen([AGG, "-i", "-1", "-d", "2", "-c", "1", "--rounds", "1", "--port-base", str(base),
+                            "--layout", "rs"], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        time.sleep(0.5)
+        subprocess.run([OWNERS, "--blobs", str(tmp_path), "--parts", "1,2,3", "-d", "2", "-c", "1", "--port-base",
+                        str(base), "--model-name", "1", "--start", "9", "--end", "3", "--reply-timeout", "5"],
+                       capture_output=True, text=True, timeout=120)
+        out, err = agg.communicate(timeout=60)
+        assert agg.returncode == 1 and "bf16" in err
     finally:
         if agg.poll() is None:
             agg.kill()

@@ -56,6 +56,7 @@ struct Part {
     std::string blob;
     TorchArchive ar;
     size_t n = 0;
+    int es = 4;  // parameter element bytes: 4 fp32, 2 bf16 (the template's dtype)
 };
 
 }  // namespace
@@ -113,6 +114,11 @@ int main(int argc, char** argv) {
             return 1;
         }
         p.n = (size_t)p.ar.param_numel();
+        p.es = p.ar.param_elem_size();
+        if (!p.es) {
+            std::cerr << "template mp" << p.mp << ": parameters not all fp32 or all bf16\n";
+            return 1;
+        }
     }
     // data owner ids: the init node 0 and the ids the aggregator replies to (aggregator.cpp:103-105)
     std::vector<int> ids = {0};
@@ -164,24 +170,28 @@ int main(int argc, char** argv) {
         return (int)got->size() == want;
     };
     const int threads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    auto fill = [&](uint64_t sd, uint32_t k, size_t n, float* x) {  // the oracle's generator, in chunks
+    auto fill = [&](uint64_t sd, uint32_t k, size_t n, int es, uint8_t* x) {  // the oracle's generator, in chunks
         std::vector<std::thread> th;
         const size_t per = (n + threads - 1) / threads;
         for (int t = 0; t < threads; ++t) {
             const size_t lo = std::min(n, t * per), hi = std::min(n, lo + per);
-            if (lo < hi) th.emplace_back([=] { fa_oracle_fill_f32(sd, k, lo, hi - lo, x + lo); });
+            if (lo < hi)
+                th.emplace_back([=] {
+                    if (es == 4) fa_oracle_fill_f32(sd, k, lo, hi - lo, reinterpret_cast<float*>(x) + lo);
+                    else fa_oracle_fill_bf16(sd, k, lo, hi - lo, reinterpret_cast<uint16_t*>(x) + lo);
+                });
         }
         for (auto& t : th) t.join();
     };
     for (int round = 0; round < rounds; ++round) {
         // The data owners' side of a round (their training) is not timed: values and frames are made
         // first, then the clock runs from the first phase-1 send to the last phase-2 reply.
-        std::map<int, std::vector<std::vector<float>>> values;  // mp -> per client
+        std::map<int, std::vector<std::vector<uint8_t>>> values;  // mp -> per client (the parameters' own dtype)
         std::map<int, std::vector<std::shared_ptr<const Bytes>>> frames;
         for (auto& p : parts) {
             for (int k = 0; k < D; ++k) {
-                std::vector<float> x(p.n);
-                fill(seed ^ ((uint64_t)round << 48) ^ ((uint64_t)p.mp << 32), (uint32_t)k, p.n, x.data());
+                std::vector<uint8_t> x(p.n * (size_t)p.es);
+                fill(seed ^ ((uint64_t)round << 48) ^ ((uint64_t)p.mp << 32), (uint32_t)k, p.n, p.es, x.data());
                 Message m;  // Task(myID, aggregation_, -1), data_owner.cpp:225-231
                 m.type = OPERATION;
                 m.client_id = ids[k];
@@ -192,7 +202,7 @@ int main(int argc, char** argv) {
                 char* vals = nullptr;
                 auto f = operation_frame(m, p.ar.size(), &vals);
                 std::string err;
-                if (!p.ar.with_params_into(x.data(), (uint8_t*)vals, &err)) {
+                if (!p.ar.with_param_bytes_into(x.data(), (uint8_t*)vals, &err)) {
                     std::cerr << err << "\n";
                     return 1;
                 }
@@ -254,21 +264,30 @@ int main(int argc, char** argv) {
                 ok = false;
                 continue;
             }
-            std::vector<float> got(p->n), want(p->n);
-            ar.gather_params(got.data(), &err);
+            const size_t es = (size_t)p->es;
+            std::vector<uint8_t> got(p->n * es), want(p->n * es);
+            if (ar.param_elem_size() != p->es || !ar.gather_param_bytes(got.data(), &err)) {
+                std::cerr << "reply for part " << p->mp << " changed dtype: " << err << "\n";
+                ok = false;
+                continue;
+            }
             const auto& xs = values[p->mp];
             if (mode == "literal") {
-                fa_oracle_literal_f32(xs[D - 1].data(), p->n, divisor, want.data());
-            } else {
+                if (es == 4) fa_oracle_literal_f32((const float*)xs[D - 1].data(), p->n, divisor, (float*)want.data());
+                else fa_oracle_literal_bf16((const uint16_t*)xs[D - 1].data(), p->n, divisor, want.data(), 1);
+            } else if (es == 4) {
                 std::vector<const float*> ptrs;
-                for (auto& x : xs) ptrs.push_back(x.data());
-                fa_oracle_fedavg_f32(ptrs.data(), w.data(), D, p->n, nullptr, want.data(), threads);
+                for (auto& x : xs) ptrs.push_back((const float*)x.data());
+                fa_oracle_fedavg_f32(ptrs.data(), w.data(), D, p->n, nullptr, (float*)want.data(), threads);
+            } else {  // bf16 buckets: the fp32 chain, rounded once to bf16 (RNE)
+                std::vector<const uint16_t*> ptrs;
+                for (auto& x : xs) ptrs.push_back((const uint16_t*)x.data());
+                fa_oracle_fedavg_bf16(ptrs.data(), w.data(), D, p->n, nullptr, want.data(), 1, threads);
             }
-            if (std::memcmp(got.data(), want.data(), p->n * 4) != 0) {
+            if (std::memcmp(got.data(), want.data(), p->n * es) != 0) {
                 size_t bad = 0;
-                while (bad < p->n && std::memcmp(&got[bad], &want[bad], 4) == 0) ++bad;
-                std::cerr << "part " << p->mp << " mismatch at " << bad << ": " << got[bad] << " vs " << want[bad]
-                          << "\n";
+                while (bad < p->n && std::memcmp(&got[bad * es], &want[bad * es], es) == 0) ++bad;
+                std::cerr << "part " << p->mp << " mismatch at element " << bad << " (" << es << "-byte elements)\n";
                 ok = false;
             }
             checked += p->n;
