@@ -101,7 +101,7 @@ def main():
             out[key] = {k: med([key, k]) for k in recs[0][key]}
         out["read0_median_per_xcd_us"] = {x: med(["read0_median_per_xcd_us", x]) for x in range(8)}
         out["lds0_median_per_xcd_us"] = {x: med(["lds0_median_per_xcd_us", x]) for x in range(8)}
-        out["swizzle"] = os.environ.get("FA_PHASED_SWIZZLE", "0")
+        out["skew"] = os.environ.get("FA_PHASED_SKEW", "default")
         print(json.dumps(out), flush=True)
         s.close()
 
