@@ -801,3 +801,36 @@ def test_read_stream_probe_reads_only(fa, O, torch_gpu, n, D):
         assert torch.equal(a.view(torch.int32), b.view(torch.int32))
     with pytest.raises(fa.FaError):
         fa.diag_read_stream(clients, n + 1, stream=s)  # not a multiple of 4
+
+
+def test_context_misuse(fa, O, torch_gpu):
+    """Misuse of a context is an error code, never a wrong result: gather pieces that do not add up to
+    the bucket, a slot out of range, a finalize into pieces of the wrong total; redefining a bucket
+    replaces it (new size, new client count) and the next round is bit-exact; a receipt submitted
+    twice counts once (the later one replaces it, as a retransmitted owner would)."""
+    n, D = 10_007, 3
+    w = O.weights(D)
+    xs = host_clients(O, 81, D, n, False)
+    with fa.Aggregator(1) as agg:
+        agg.define(1, n, fa.F32, fa.F32, D, fa.FEDAVG)
+        with pytest.raises(fa.FaError) as e:
+            agg.submit_gather(1, 0, [xs[0][:100], xs[0][100:-1]], w[0])  # one element short
+        assert e.value.code == fa.ERR_ARG
+        with pytest.raises(fa.FaError):
+            agg.submit(1, -1, xs[0], w[0])
+        junk = np.full(n, 7.0, np.float32)
+        agg.submit(1, 1, junk, 0.25)      # replaced below
+        for k in range(D):
+            agg.submit(1, k, xs[k], w[k])
+        with pytest.raises(fa.FaError) as e:
+            agg.finalize_gather(1, [np.empty(n - 1, np.float32)])
+        assert e.value.code == fa.ERR_ARG
+        assert_bits(agg.finalize(1), O.fedavg(xs, w))
+        # redefine: more elements and clients, then a full round
+        n2, D2 = 20_011, 5
+        w2 = O.weights(D2)
+        xs2 = host_clients(O, 82, D2, n2, False)
+        agg.define(1, n2, fa.F32, fa.F32, D2, fa.FEDAVG)
+        for k in range(D2):
+            agg.submit(1, k, xs2[k], w2[k])
+        assert_bits(agg.finalize(1), O.fedavg(xs2, w2))
