@@ -127,3 +127,16 @@ def test_no_device_fails_loudly(fa):
     with pytest.raises(fa.FaError) as e:
         fa.Aggregator(1)
     assert e.value.code in (fa.ERR_NODEV, fa.ERR_ARG)
+
+
+def test_native_bench_built_and_checks_arguments():
+    """bin/fa_bench (the C++-only round timer) is built with the library; bad arguments exit with 2
+    before any device work (so this runs without a GPU)."""
+    import os
+    import subprocess
+    from conftest import PKG_DIR
+    exe = os.path.join(PKG_DIR, "bin", "fa_bench")
+    assert os.access(exe, os.X_OK)
+    for bad in (["--workload", "nope"], ["--steps", "0"], ["--layout", "ring"], ["--frobnicate"]):
+        r = subprocess.run([exe] + bad, capture_output=True, text=True, timeout=60)
+        assert r.returncode == 2, (bad, r.stderr)
