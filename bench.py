@@ -34,6 +34,7 @@ import json
 import os
 import statistics
 import shutil
+import signal
 import subprocess
 import sys
 import tempfile
@@ -184,8 +185,19 @@ def live_traffic(workload, timeout=150):
             for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
                 env.pop(k, None)
             try:
-                subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env, timeout=timeout,
-                               check=True, cwd=ROOT)
+                # its own process group, so a pass that times out is killed whole (the profiler and the
+                # bench under it), not just the profiler's front end
+                proc = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env, cwd=ROOT,
+                                        start_new_session=True)
+                try:
+                    _, err = proc.communicate(timeout=timeout)
+                except subprocess.TimeoutExpired:
+                    os.killpg(proc.pid, signal.SIGKILL)
+                    proc.communicate()
+                    return None, "live PMC pass %s timed out after %d s" % (counter, timeout)
+                if proc.returncode != 0:
+                    return None, "live PMC pass %s failed (rc %d): %s" % (counter, proc.returncode,
+                                                                         (err or b"")[-200:].decode(errors="replace"))
             except (subprocess.SubprocessError, OSError) as e:
                 return None, "live PMC pass %s failed: %s" % (counter, repr(e)[:200])
             path = os.path.join(d, "run_counter_collection.csv")
