@@ -62,3 +62,33 @@ def test_live_traffic_reports_a_missing_profiler(monkeypatch, tmp_path):
 def test_bench_skips_live_pmc_under_a_profiler(monkeypatch):
     monkeypatch.setenv("ROCPROF_COUNTERS", "FETCH_SIZE")
     assert bench.under_profiler()
+
+
+HANG = r'''#!/usr/bin/env python3
+import os, subprocess, sys, time
+# a profiler whose child hangs: both must die when the pass times out
+child = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(600)"])
+open(os.environ["FAKE_ROCPROF_PIDS"], "w").write("%d %d" % (os.getpid(), child.pid))
+time.sleep(600)
+'''
+
+
+def test_live_traffic_timeout_kills_the_whole_pass(tmp_path, monkeypatch):
+    fake = tmp_path / "rocprofv3"
+    fake.write_text(HANG)
+    fake.chmod(fake.stat().st_mode | stat.S_IEXEC)
+    pids = tmp_path / "pids"
+    monkeypatch.setenv("PATH", str(tmp_path) + os.pathsep + os.environ["PATH"])
+    monkeypatch.setenv("FAKE_ROCPROF_PIDS", str(pids))
+    traffic, reason = bench.live_traffic("northstar", timeout=3)
+    assert traffic is None and "timed out" in reason
+    import time
+    for pid in map(int, pids.read_text().split()):
+        for _ in range(50):  # reaped by now, or about to be
+            try:
+                os.kill(pid, 0)
+            except ProcessLookupError:
+                break
+            time.sleep(0.1)
+        else:
+            raise AssertionError("process %d of the timed-out pass survived" % pid)
