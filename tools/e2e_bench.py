@@ -10,6 +10,10 @@ Beside it, oracle/_ref/ref_harness times the reference-literal receive loop
 (torch::load + (p+p)/1000 + copy_, aggregator.cpp:63-88) on the VGG FC part.
 
   python tools/e2e_bench.py [D] [rounds] [aggregator args...]   (e.g. --layout rs, --eager)
+
+E2E_MODEL=c3 uses BASELINE C3's bucket sizes instead (ResNet-101 split "10,19": 2 594 688 / 29 511 680 /
+5 130 parameters) in bf16 -- Linear layers with exactly those parameter counts; the aggregator only
+sees flat parameter buckets, so their shapes do not matter.
 """
 import json
 import os
@@ -42,6 +46,21 @@ def vgg_c4_parts(d):
     return sizes
 
 
+def c3_bf16_parts(d):
+    import torch
+    import torch.nn as nn
+    torch.manual_seed(0)
+    parts = {1: nn.Sequential(nn.Linear(347, 7456)),    # 2 594 688 parameters
+             2: nn.Sequential(nn.Linear(4095, 7205)),   # 29 511 680
+             3: nn.Sequential(nn.Linear(512, 10))}      # 5 130 (the ResNet fc)
+    sizes = {}
+    for mp, m in parts.items():
+        m = m.to(torch.bfloat16)
+        torch.jit.save(torch.jit.script(m), os.path.join(d, "mp%d_client0.pt" % mp))
+        sizes[mp] = sum(p.numel() for p in m.parameters())
+    return sizes
+
+
 def heartbeat(every=20):
     """A progress line on stderr every `every` s: large rounds (D = 64 VGG owners, 30 GB of receipts per
     round over loopback) run for minutes with nothing else to print."""
@@ -60,10 +79,12 @@ def main():
     D = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 2
     extra = sys.argv[3:]
-    out = {"workload": "VGG-19 C4 model parts (split 3,19), %d data owners, loopback TCP" % D,
+    c3 = os.environ.get("E2E_MODEL") == "c3"
+    out = {"workload": ("ResNet-101 C3 bucket sizes (split 10,19), bf16" if c3 else
+                        "VGG-19 C4 model parts (split 3,19)") + ", %d data owners, loopback TCP" % D,
            "aggregator_args": extra}
     with tempfile.TemporaryDirectory() as d:
-        sizes = vgg_c4_parts(d)
+        sizes = c3_bf16_parts(d) if c3 else vgg_c4_parts(d)
         out["params_per_part"] = sizes
         base = random.randrange(10000, 32000, 100)  # below the ephemeral port range
         agg = subprocess.Popen([AGG, "-i", "-1", "-d", str(D), "-c", "1", "--rounds", str(rounds), "--port-base",
@@ -71,7 +92,9 @@ def main():
         time.sleep(0.5)
         t0 = time.perf_counter()
         r = subprocess.run([OWNERS, "--blobs", d, "--parts", "1,2,3", "-d", str(D), "-c", "1", "--rounds",
-                            str(rounds), "--port-base", str(base), "--model-name", "0", "--start", "20", "--end", "3"],
+                            str(rounds), "--port-base", str(base)] +
+                           (["--model-name", "1", "--start", "19", "--end", "10"] if c3 else
+                            ["--model-name", "0", "--start", "20", "--end", "3"]),
                            capture_output=True, text=True, timeout=900)
         wall = time.perf_counter() - t0
         a_out, a_err = agg.communicate(timeout=120)
