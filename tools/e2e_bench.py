@@ -12,8 +12,9 @@ Beside it, oracle/_ref/ref_harness times the reference-literal receive loop
   python tools/e2e_bench.py [D] [rounds] [aggregator args...]   (e.g. --layout rs, --eager)
 
 E2E_MODEL=c3 uses BASELINE C3's bucket sizes instead (ResNet-101 split "10,19": 2 594 688 / 29 511 680 /
-5 130 parameters) in bf16 -- Linear layers with exactly those parameter counts; the aggregator only
-sees flat parameter buckets, so their shapes do not matter.
+5 130 parameters) in bf16, E2E_MODEL=c2 C2's (ResNet-18 split "3,8": 83 584 / 9 442 304 / 5 130) in fp32
+-- Linear layers with exactly those parameter counts; the aggregator only sees flat parameter buckets,
+so their shapes do not matter.
 """
 import json
 import os
@@ -46,16 +47,22 @@ def vgg_c4_parts(d):
     return sizes
 
 
-def c3_bf16_parts(d):
+def resnet_parts(d, c3):
     import torch
     import torch.nn as nn
     torch.manual_seed(0)
-    parts = {1: nn.Sequential(nn.Linear(347, 7456)),    # 2 594 688 parameters
-             2: nn.Sequential(nn.Linear(4095, 7205)),   # 29 511 680
-             3: nn.Sequential(nn.Linear(512, 10))}      # 5 130 (the ResNet fc)
+    if c3:
+        parts = {1: nn.Sequential(nn.Linear(347, 7456)),    # 2 594 688 parameters
+                 2: nn.Sequential(nn.Linear(4095, 7205)),   # 29 511 680
+                 3: nn.Sequential(nn.Linear(512, 10))}      # 5 130 (the ResNet fc)
+    else:
+        parts = {1: nn.Sequential(nn.Linear(31, 2612)),     # 83 584
+                 2: nn.Sequential(nn.Linear(9220, 1024)),   # 9 442 304
+                 3: nn.Sequential(nn.Linear(512, 10))}      # 5 130
     sizes = {}
     for mp, m in parts.items():
-        m = m.to(torch.bfloat16)
+        if c3:
+            m = m.to(torch.bfloat16)
         torch.jit.save(torch.jit.script(m), os.path.join(d, "mp%d_client0.pt" % mp))
         sizes[mp] = sum(p.numel() for p in m.parameters())
     return sizes
@@ -79,12 +86,14 @@ def main():
     D = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 2
     extra = sys.argv[3:]
-    c3 = os.environ.get("E2E_MODEL") == "c3"
-    out = {"workload": ("ResNet-101 C3 bucket sizes (split 10,19), bf16" if c3 else
-                        "VGG-19 C4 model parts (split 3,19)") + ", %d data owners, loopback TCP" % D,
+    model = os.environ.get("E2E_MODEL", "c4")
+    resnet = model in ("c2", "c3")
+    out = {"workload": {"c2": "ResNet-18 C2 bucket sizes (split 3,8), fp32",
+                        "c3": "ResNet-101 C3 bucket sizes (split 10,19), bf16"}.get(
+                            model, "VGG-19 C4 model parts (split 3,19)") + ", %d data owners, loopback TCP" % D,
            "aggregator_args": extra}
     with tempfile.TemporaryDirectory() as d:
-        sizes = c3_bf16_parts(d) if c3 else vgg_c4_parts(d)
+        sizes = resnet_parts(d, model == "c3") if resnet else vgg_c4_parts(d)
         out["params_per_part"] = sizes
         base = random.randrange(10000, 32000, 100)  # below the ephemeral port range
         agg = subprocess.Popen([AGG, "-i", "-1", "-d", str(D), "-c", "1", "--rounds", str(rounds), "--port-base",
@@ -93,7 +102,7 @@ def main():
         t0 = time.perf_counter()
         r = subprocess.run([OWNERS, "--blobs", d, "--parts", "1,2,3", "-d", str(D), "-c", "1", "--rounds",
                             str(rounds), "--port-base", str(base)] +
-                           (["--model-name", "1", "--start", "19", "--end", "10"] if c3 else
+                           (["--model-name", "1", "--start", "19", "--end", "10"] if resnet else
                             ["--model-name", "0", "--start", "20", "--end", "3"]),
                            capture_output=True, text=True, timeout=900)
         wall = time.perf_counter() - t0
