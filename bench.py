@@ -795,7 +795,7 @@ def ctx_multi(args):
     print(json.dumps(out), flush=True)
 
 
-def ctx_multi_secondaries(n_dev, timeout=240):
+def ctx_multi_secondaries(n_dev, timeout=150):
     """On a node with several visible GPUs, the N = 1 run also times the in-process multi-GPU layouts over
     all of them (child processes, time-limited: a stalled collective cannot take the main line with it)."""
     res = {}

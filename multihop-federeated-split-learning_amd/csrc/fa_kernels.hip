@@ -832,6 +832,8 @@ hipError_t phased_enqueue(PhasedDevice* d, Kern kern, int th, int RL, int RR, hi
         const char* e = std::getenv("FA_PHASED_LAST_MEET");
         return e ? std::atoi(e) : 0;
     }();
+    // FA_TIMELINE: a launch without meetings leaves their stamps alone, so clear the previous launch's
+    if (d->tl) (void)hipMemsetAsync(d->tl, 0, sizeof(unsigned long long) * 8 * d->cus, s);
     hipLaunchKernelGGL(kern, dim3((unsigned)d->cus), dim3(th), 0, s, t, nc, init, out, head, nvec, n,
                        d->sync + slot * kSyncStride, slack, rl_last, skew, skew_last, last_meet, d->tl);
     return hipGetLastError();

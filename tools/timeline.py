@@ -28,6 +28,16 @@ def summarize(tl, G):
     start = [r[0] for r in rows]
     t0 = min(start)
     us = lambda x: round(x * TICK_US, 2)  # noqa: E731
+    whole = [r[5] - r[0] for r in rows]  # start to stores completed, per workgroup
+    base = {
+        "meetings": int(rows[0][6]),
+        "span_us": us(max(r[5] for r in rows) - t0),
+        "start_spread_us": us(max(start) - t0),
+        "workgroup_us": {"min": us(min(whole)), "median": us(statistics.median(whole)), "max": us(max(whole))},
+        "end_spread_us": us(max(r[5] for r in rows) - min(r[5] for r in rows)),
+    }
+    if base["meetings"] == 0:  # a launch without meetings (one sized phase): the meeting stamps stay 0
+        return base
     read0 = [r[1] - r[0] for r in rows]
     lds0 = [r[7] - r[0] for r in rows]  # phase 0's LDS part; the register part follows until r[1]
     wait0 = [r[2] - r[1] for r in rows]
@@ -37,10 +47,7 @@ def summarize(tl, G):
     for x in range(8):
         per_xcd[x] = us(statistics.median([read0[b] for b in range(x, G, 8)]))
         lds_xcd[x] = us(statistics.median([lds0[b] for b in range(x, G, 8)]))
-    return {
-        "meetings": int(rows[0][6]),
-        "span_us": us(max(r[5] for r in rows) - t0),
-        "start_spread_us": us(max(start) - t0),
+    return dict(base, **{
         "read0_us": {"min": us(min(read0)), "median": us(statistics.median(read0)), "max": us(max(read0))},
         "read0_median_per_xcd_us": per_xcd,
         "lds0_median_per_xcd_us": lds_xcd,
@@ -48,8 +55,7 @@ def summarize(tl, G):
         "last_arrival_spread_us": us(max(arrive_last) - min(arrive_last)),
         "write_after_last_meeting_us": {"min": us(min(write)), "median": us(statistics.median(write)),
                                          "max": us(max(write))},
-        "end_spread_us": us(max(r[5] for r in rows) - min(r[5] for r in rows)),
-    }
+    })
 
 
 def main():
@@ -96,11 +102,14 @@ def main():
         out = {"workload": name, "launches": launches, "event_ms_median": round(statistics.median(ms), 4),
                "algorithmic_bytes": s.algo_bytes(), "meetings": recs[0]["meetings"]}
         for key in ("span_us", "start_spread_us", "last_arrival_spread_us", "end_spread_us"):
-            out[key] = med([key])
-        for key in ("read0_us", "wait0_us", "write_after_last_meeting_us"):
-            out[key] = {k: med([key, k]) for k in recs[0][key]}
-        out["read0_median_per_xcd_us"] = {x: med(["read0_median_per_xcd_us", x]) for x in range(8)}
-        out["lds0_median_per_xcd_us"] = {x: med(["lds0_median_per_xcd_us", x]) for x in range(8)}
+            if key in recs[0]:
+                out[key] = med([key])
+        for key in ("workgroup_us", "read0_us", "wait0_us", "write_after_last_meeting_us"):
+            if key in recs[0]:
+                out[key] = {k: med([key, k]) for k in recs[0][key]}
+        if out["meetings"]:
+            out["read0_median_per_xcd_us"] = {x: med(["read0_median_per_xcd_us", x]) for x in range(8)}
+            out["lds0_median_per_xcd_us"] = {x: med(["lds0_median_per_xcd_us", x]) for x in range(8)}
         out["skew"] = os.environ.get("FA_PHASED_SKEW", "default")
         print(json.dumps(out), flush=True)
         s.close()
