@@ -73,7 +73,7 @@ def test_states_reject_mixed_architectures():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("D,bf16", [(1, False), (5, False), (3, True), (13, False), (13, True), (64, False), (70, False), (70, True), (130, False), (130, True)])
+@pytest.mark.parametrize("D,bf16", [(1, False), (2, True), (5, False), (3, True), (8, False), (8, True), (9, False), (13, False), (13, True), (64, False), (70, False), (70, True), (130, False), (130, True)])
 def test_sync_device_bitexact(fa, O, torch_gpu, D, bf16):
     torch = torch_gpu
     n = 100_003
