@@ -899,7 +899,7 @@ int reduce_parts_impl(fa_ctx* ctx, int n_parts, const int* ids, const float* con
         bool batch = !p.rs && p.mode == FA_FEDAVG && p.D <= fa::kMaxClients;
         for (int g = 0; batch && g < ctx->G; ++g) {
             DeviceGuard dg(ctx->gpu[(size_t)g].dev);
-            batch = !fa::phased_takes(p.in, (int64_t)(p.cnt[(size_t)g] * dsize(p.in) / 16), p.D, tu);
+            batch = !fa::phased_takes(p.in, p.out, (int64_t)(p.cnt[(size_t)g] * dsize(p.in) / 16), p.D, tu);
         }
         if (batch) groups[{(int)p.in, (int)p.out}].push_back(i);
         else single.push_back(i);

@@ -58,7 +58,7 @@ hipError_t phased_timeouts(int dev, uint64_t* count);
 // dev into out; returns the words copied (0: no timeline, -1: HIP error).
 int phased_timeline(int dev, unsigned long long* out, int cap);
 // Elements per GPU from which the phased walk applies (0: not in use); see fa_kernels.hip.
-int64_t phased_min_elems(fa_dtype in, const Tuning& tu);
+int64_t phased_min_elems(fa_dtype in, fa_dtype out, const Tuning& tu);
 hipError_t launch_literal(const void* x, fa_dtype in, void* dst, fa_dtype out, float divisor, int64_t head,
                           int64_t nvec, int64_t n, bool vector_ok, const Tuning& tu, hipStream_t s);
 // In-place state sync: every slot t.src[0..nc) := the chain over them (continuing `init` if given).
@@ -73,7 +73,7 @@ hipError_t launch_segments(const SegDesc* d_segs, int nseg, int64_t blocks, fa_d
 // The same with the table in the kernel arguments (a.nseg <= kSegArgMax, sum of nc <= kSegArgClients).
 hipError_t launch_segargs(const SegArgs& a, fa_dtype in, fa_dtype out, int max_nc, const Tuning& tu, hipStream_t s);
 // Whether launch_chain takes the phased kernel for a bucket of nvec vectors and nc clients.
-bool phased_takes(fa_dtype in, int64_t nvec, int nc, const Tuning& tu);
+bool phased_takes(fa_dtype in, fa_dtype out, int64_t nvec, int nc, const Tuning& tu);
 hipError_t launch_fill(void* dst, int64_t n, fa_dtype dt, uint64_t seed, uint32_t client, uint64_t idx0,
                        hipStream_t s);
 // Read-stream probe over nc f32 buffers of nvec 16-byte vectors (16-byte aligned); nothing is written.

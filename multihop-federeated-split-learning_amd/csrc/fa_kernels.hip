@@ -263,10 +263,17 @@ __global__ __launch_bounds__(256) void fedavg_chain_kernel(const ClientTable t, 
 constexpr int kPhasedThreads = 256;
 constexpr int kSyncRing = 8;
 
-template <typename IN, int REGS, int TH = kPhasedThreads>
+// An LDS row holds a lane's finished vector (the whole chain is done before it is stored), so it is kept in
+// the OUTPUT dtype: rounded once to bf16 there exactly as the global store would, same bits, and a bf16
+// output fits twice the rows (the 512-thread bf16 form: 20 instead of 10, a phase of 33.5 M elements
+// instead of 23.1 M).
+template <typename OUT> using LdsT = typename std::conditional<std::is_same<OUT, uint16_t>::value, uint16_t, float>::type;
+
+template <typename IN, int REGS, int TH = kPhasedThreads, typename OUT = float>
 struct Phased {  // vectors per lane per phase: LDS (160 KiB per workgroup) + registers
     static constexpr int V = In<IN>::kVec;
-    static constexpr int RL = 160 * 1024 / (TH * V * 4);  // 256 threads: f32 in 40, bf16 in 20
+    // 256 threads: f32 -> f32 40; 512 threads: bf16 -> bf16 20, bf16 -> f32 10
+    static constexpr int RL = 160 * 1024 / (TH * V * (int)sizeof(LdsT<OUT>));
     static constexpr int RR = REGS / V;  // REGS 128: 32 / 16 vectors (arch VGPRs); 192: 48 / 24 (+ AGPRs)
 };
 
@@ -350,15 +357,42 @@ __device__ __forceinline__ void put(const ClientTable& t, int nc, void* out, int
     }
 }
 
+// LDS rows of a bf16 output: the finished vector as bf16 bits (pack_bf16), stored as they are.
+template <int V>
+__device__ __forceinline__ void pack_bf16(uint16_t* row, const float* acc) {
+    if constexpr (V == 8) {
+        *reinterpret_cast<u32x4*>(row) =
+            u32x4{f32_to_bf16(acc[0]) | (f32_to_bf16(acc[1]) << 16), f32_to_bf16(acc[2]) | (f32_to_bf16(acc[3]) << 16),
+                  f32_to_bf16(acc[4]) | (f32_to_bf16(acc[5]) << 16), f32_to_bf16(acc[6]) | (f32_to_bf16(acc[7]) << 16)};
+    } else {
+        *reinterpret_cast<u32x2*>(row) =
+            u32x2{f32_to_bf16(acc[0]) | (f32_to_bf16(acc[1]) << 16), f32_to_bf16(acc[2]) | (f32_to_bf16(acc[3]) << 16)};
+    }
+}
+template <int V, bool SYNC>
+__device__ __forceinline__ void put_bf16_bits(const ClientTable& t, int nc, void* out, int64_t e, const uint16_t* row) {
+    auto one = [&](void* base) {
+        uint16_t* p = reinterpret_cast<uint16_t*>(base) + e;
+        if constexpr (V == 8) st16<kStSc1>(p, *reinterpret_cast<const u32x4*>(row));
+        else st8<kStSc1>(p, *reinterpret_cast<const u32x2*>(row));
+    };
+    if constexpr (SYNC) {
+        for (int k = 0; k < nc; ++k) one(const_cast<void*>(t.src[k]));
+    } else {
+        one(out);
+    }
+}
+
 template <typename IN, typename OUT, bool INIT, int REGS, bool SYNC, int TH>
 __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, int nc, const float* init,
                                                                        void* out, int64_t head, int64_t nvec, int64_t n,
                                                                        unsigned* sync, int slack, int rl_last,
                                                                        int skew, int skew_last, int last_meet,
                                                                        unsigned long long* tl) {
-    constexpr int V = In<IN>::kVec, T = TH, RL = Phased<IN, REGS, TH>::RL, RR = Phased<IN, REGS, TH>::RR;
+    constexpr int V = In<IN>::kVec, T = TH, RL = Phased<IN, REGS, TH, OUT>::RL, RR = Phased<IN, REGS, TH, OUT>::RR;
     constexpr int U = TH > 256 ? 8 : 16;  // loads in flight per wave (2 waves per SIMD at 512 threads)
-    __shared__ float buf[RL * T * V];
+    constexpr bool kPacked = std::is_same<LdsT<OUT>, uint16_t>::value;  // LDS rows hold bf16 output bits
+    __shared__ LdsT<OUT> buf[RL * T * V];
     // thread 0 takes the ticket; its value is first needed at the phase-0 meeting, so the atomic's
     // latency hides under the phase's loads
     unsigned long long ticket = 0;
@@ -426,8 +460,12 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
             if (v < nvec) {
                 float acc[V];
                 chain_vec<IN, U, true, INIT>(t, nc, init, head + v * V, acc);
+                if constexpr (kPacked) {
+                    pack_bf16<V>(reinterpret_cast<uint16_t*>(&buf[(i * T + threadIdx.x) * V]), acc);
+                } else {
 #pragma unroll
-                for (int j = 0; j < V; ++j) buf[(i * T + threadIdx.x) * V + j] = acc[j];
+                    for (int j = 0; j < V; ++j) buf[(i * T + threadIdx.x) * V + j] = acc[j];
+                }
             }
         }
         if (my_tl && p == 0) {
@@ -454,7 +492,13 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
 #pragma unroll 1
         for (int i = 0; i < rl; ++i) {
             const int64_t v = row_vec(i);
-            if (v < nvec) put<OUT, V, SYNC>(t, nc, out, head + v * V, &buf[(i * T + threadIdx.x) * V]);
+            if (v < nvec) {
+                if constexpr (kPacked)
+                    put_bf16_bits<V, SYNC>(t, nc, out, head + v * V,
+                                           reinterpret_cast<const uint16_t*>(&buf[(i * T + threadIdx.x) * V]));
+                else
+                    put<OUT, V, SYNC>(t, nc, out, head + v * V, reinterpret_cast<const float*>(&buf[(i * T + threadIdx.x) * V]));
+            }
         }
         if (staged) {
             const int64_t c = c0 + (threadIdx.x & 63);
@@ -800,14 +844,14 @@ inline int phased_rl_last(int64_t rem, int64_t lanes, int RL, int RR) {
 // LDS rows the odd XCDs' workgroups leave to the even ones in every full phase (fedavg_phased_kernel's
 // skew): RL / 10 in the f32 form -- 4 of its 40 (north star 1.259-1.261 against 1.271 ms, C4 5.25 against
 // 5.30, one rank's share at 2 GPUs 0.668-0.673 against 0.677-0.684; gpurun_out r02s25-s26); more loses
-// again.  None in the 512-thread bf16 form, whose 10 rows leave no step small enough (C3: 1 row 0.425-0.427
-// ms against 0.424, 4 rows 0.444-0.449; r02s26-s27).  FA_PHASED_SKEW overrides it (below RL / 2).
+// again.  None in the 512-thread bf16 form: with fp32 rows (10) no step was small enough (C3: 1 row
+// 0.425-0.427 ms against 0.424, 4 rows 0.444-0.449; r02s26-s27), and its bf16 rows (20) keep none either.  FA_PHASED_SKEW overrides it (below RL / 2).
 int phased_skew(int RL) {
     static const int v = [] {
         const char* e = std::getenv("FA_PHASED_SKEW");
         return e ? std::max(0, std::atoi(e)) : -1;
     }();
-    return std::min(v >= 0 ? v : RL >= 20 ? RL / 10 : 0, RL / 2 - 1);
+    return std::min(v >= 0 ? v : RL >= 40 ? RL / 10 : 0, RL / 2 - 1);  // the bf16 form (20 rows): none
 }
 
 // Enqueue one phased launch on stream s, on the stream's counter slot.
@@ -858,7 +902,7 @@ hipError_t launch_phased_r(const ClientTable& t, int nc, const float* init, void
                            int64_t n, hipStream_t s, bool sized = false) {
     PhasedDevice* d = phased_device();
     if (!d) return hipErrorNotSupported;
-    constexpr int RL = Phased<IN, REGS, TH>::RL, RR = Phased<IN, REGS, TH>::RR;
+    constexpr int RL = Phased<IN, REGS, TH, OUT>::RL, RR = Phased<IN, REGS, TH, OUT>::RR;
     const int64_t per_phase = (int64_t)d->cus * TH * (RL + RR);
     // experiment knob (tools/): FA_PHASED_MIN_VECS lowers the smallest bucket the phased kernel takes
     static const int64_t min_env = [] {
@@ -910,14 +954,14 @@ hipError_t launch_phased_sized(const ClientTable& t, int nc, const float* init, 
 
 // Smallest bucket (elements of dtype `in` per GPU) that the phased walk of `tu` takes on the current
 // device, or 0 when the phased kernel is not in use.
-int64_t phased_min_elems_impl(fa_dtype in, const Tuning& tu) {
+int64_t phased_min_elems_impl(fa_dtype in, fa_dtype out, const Tuning& tu) {
     if (tu.walk < 3 || tu.walk > 5) return 0;
     PhasedDevice* d = phased_device();
     if (!d) return 0;
     const bool big = tu.walk == 5 || (tu.walk == 4 && in == FA_BF16);  // the 512-thread form
     const int regs = big ? 96 : tu.walk == 4 ? 192 : 128, th = big ? 512 : kPhasedThreads;
     const int V = in == FA_F32 ? 4 : 8;
-    const int rl = 160 * 1024 / (th * V * 4), rr = regs / V;
+    const int rl = 160 * 1024 / (th * V * (out == FA_BF16 ? 2 : 4)), rr = regs / V;  // Phased<>::RL
     return (int64_t)d->cus * th * (rl + rr) * V;
 }
 
@@ -962,7 +1006,7 @@ hipError_t launch_chain_t(const ClientTable& t, int nc, const float* init, void*
 
 }  // namespace
 
-int64_t phased_min_elems(fa_dtype in, const Tuning& tu) { return phased_min_elems_impl(in, tu); }
+int64_t phased_min_elems(fa_dtype in, fa_dtype out, const Tuning& tu) { return phased_min_elems_impl(in, out, tu); }
 
 hipError_t phased_timeouts(int dev, uint64_t* count) {
     *count = 0;
@@ -1040,12 +1084,13 @@ template <typename T, int REGS, int TH>
 hipError_t launch_sync_phased_r(const ClientTable& t, int nc, int64_t head, int64_t nvec, int64_t n, hipStream_t s) {
     PhasedDevice* d = phased_device();
     if (!d) return hipErrorNotSupported;
-    const int64_t per_phase = (int64_t)d->cus * TH * (Phased<T, REGS, TH>::RL + Phased<T, REGS, TH>::RR);
+    constexpr int RL = Phased<T, REGS, TH, T>::RL, RR = Phased<T, REGS, TH, T>::RR;
+    const int64_t per_phase = (int64_t)d->cus * TH * (RL + RR);
     if (nvec < per_phase) return hipErrorNotSupported;
     static std::atomic<int> occ{-1};
     auto kern = fedavg_phased_kernel<T, T, false, REGS, true, TH>;
     if (!phased_fits(occ, kern, TH)) return hipErrorNotSupported;
-    return phased_enqueue(d, kern, TH, Phased<T, REGS, TH>::RL, Phased<T, REGS, TH>::RR, s, t, nc,
+    return phased_enqueue(d, kern, TH, RL, RR, s, t, nc,
                           (const float*)nullptr, (void*)nullptr, head, nvec, n);
 }
 
@@ -1136,9 +1181,9 @@ hipError_t launch_segments(const SegDesc* d_segs, int nseg, int64_t blocks, fa_d
     return launch_segments_t<uint16_t, uint16_t>(d_segs, nseg, blocks, max_nc, tu.block, s);
 }
 
-bool phased_takes(fa_dtype in, int64_t nvec, int nc, const Tuning& tu) {
+bool phased_takes(fa_dtype in, fa_dtype out, int64_t nvec, int nc, const Tuning& tu) {
     if (tu.walk < 3 || tu.walk > 5) return false;
-    const int64_t full = phased_min_elems_impl(in, tu) / (in == FA_F32 ? 4 : 8);
+    const int64_t full = phased_min_elems_impl(in, out, tu) / (in == FA_F32 ? 4 : 8);
     if (full <= 0) return false;
     if (nvec >= full) return true;
     if (tu.walk != 4 || nc < sized_min_clients()) return false;

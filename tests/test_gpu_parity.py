@@ -106,6 +106,7 @@ PHASE_ELEMS = 256 * 256 * 72 * 4  # one phase of walk 4 on a 256-CU MI355X (f32 
     (False, False, 130, 1.05, 0, False),  # two passes: the second continues the chain (INIT)
     (False, False, 6, 1.4, 0, True),     # d_init given by the caller
     (False, False, 7, 1.25, 2, False),   # just over one phase of walk 5
+    (True, True, 32, 2.5, 0, False),     # bf16 -> bf16: two phases of bf16 LDS rows (33.5 M elements each)
 ])
 def test_phased_walk_same_bits(fa, O, torch_gpu, in_bf16, out_bf16, D, phases, offset, use_init):
     """The phased kernel (walk 4: persistent grid, reads and writes separated in time) against the
@@ -153,15 +154,18 @@ def test_phased_walk_same_bits(fa, O, torch_gpu, in_bf16, out_bf16, D, phases, o
 LANES_F32, LANES_BF16 = 256 * 256, 256 * 512  # phased grid lanes (256 CUs): f32 256-thread, bf16 512-thread
 
 
-@pytest.mark.parametrize("in_bf16,D,q,frac", [
+@pytest.mark.parametrize("in_bf16,D,q,frac,out_bf16", [
     # buckets below one phase, D >= 16: one phase sized to the bucket, q vectors per lane
-    (False, 16, 9, 0.3), (False, 16, 20, 0.9), (False, 20, 26, 0.5), (False, 16, 40, 0.1), (False, 32, 64, 0.0),
-    (False, 17, 87, 0.7),
-    (True, 16, 5, 0.5), (True, 16, 9, 0.2), (True, 18, 20, 0.9),
+    (False, 16, 9, 0.3, False), (False, 16, 20, 0.9, False), (False, 20, 26, 0.5, False),
+    (False, 16, 40, 0.1, False), (False, 32, 64, 0.0, False), (False, 17, 87, 0.7, False),
+    (True, 16, 5, 0.5, False), (True, 16, 9, 0.2, False), (True, 18, 20, 0.9, False),
     # several phases whose last one is balanced: q_last in (RL, RR) -> registers only, > RR -> both
-    (False, 32, 88 + 44, 0.5), (False, 16, 88 * 2 + 70, 0.3), (True, 16, 22 + 15, 0.4),
+    (False, 32, 88 + 44, 0.5, False), (False, 16, 88 * 2 + 70, 0.3, False), (True, 16, 22 + 15, 0.4, False),
+    # bf16 outputs: LDS rows hold bf16 (bf16 -> bf16: RL 20 + RR 12 per phase; f32 -> bf16: RL 80 + RR 48)
+    (True, 16, 30, 0.3, True), (True, 32, 32 + 20, 0.4, True), (True, 16, 11, 0.6, True),
+    (False, 16, 100, 0.5, True), (False, 16, 128 + 30, 0.2, True),
 ])
-def test_sized_phase_same_bits(fa, O, torch_gpu, in_bf16, D, q, frac):
+def test_sized_phase_same_bits(fa, O, torch_gpu, in_bf16, D, q, frac, out_bf16):
     """Phases sized to the bucket (launch_phased_sized) and the balanced last phase (phased_rl_last)
     against the one-shot walk on the same device inputs, whole buckets bit for bit, plus sampled
     elements against the oracle.  n = q vectors per lane minus a fraction of one lane-vector row, so
@@ -177,17 +181,24 @@ def test_sized_phase_same_bits(fa, O, torch_gpu, in_bf16, D, q, frac):
     try:
         for walk in (2, 5):
             fa.set_tuning(walk=walk)
-            out = dev_buf(torch, n, False)
-            fa.reduce_device(clients, w, n, fa.BF16 if in_bf16 else fa.F32, out, fa.F32, fa.FEDAVG)
+            out = dev_buf(torch, n, out_bf16)
+            fa.reduce_device(clients, w, n, fa.BF16 if in_bf16 else fa.F32, out, fa.BF16 if out_bf16 else fa.F32,
+                             fa.FEDAVG)
             torch.cuda.synchronize()
             outs[walk] = out
     finally:
         fa.set_tuning(walk=before["walk"])
-    assert torch.equal(outs[2].view(torch.int32), outs[5].view(torch.int32))
+    dt = torch.int16 if out_bf16 else torch.int32
+    assert torch.equal(outs[2].view(dt), outs[5].view(dt))
     if not in_bf16:
         rng = np.random.default_rng(q)
         idx = np.unique(np.concatenate([[0, n - 1], rng.integers(0, n, 512)]))
-        assert_bits(outs[5][torch.as_tensor(idx, device="cuda")].cpu().numpy(), O.fedavg_at(seed, w, idx))
+        ref = O.fedavg_at(seed, w, idx)
+        got = outs[5][torch.as_tensor(idx, device="cuda")].cpu().numpy()
+        if out_bf16:
+            assert_bits(got.view(np.uint16), O.f32_to_bf16(ref))
+        else:
+            assert_bits(got, ref)
     del clients
 
 

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B of two builds of the package on one bench workload (GPU box tool).
 
-  python tools/ab_lib.py PKG_DIR [workload=northstar] [launches=30]      (workload "sync:<w>": state sync)
+  python tools/ab_lib.py PKG_DIR [workload=northstar] [launches=30]      (workload "sync:<w>": state sync; round_c2/c3/c4: one round)
 
 PKG_DIR holds an ``__init__.py`` and ``lib/libfa.so`` (e.g. a build of an earlier commit); the
 workload's buckets are set up through that build's own context and timed with HIP events on
@@ -30,8 +30,11 @@ def main():
     fa.lib()
     import bench  # noqa: E402  (finds the package above in sys.modules)
     sync = workload.startswith("sync:")  # compute-node state sync (fa_sync_part) on a workload's shape
-    D, n, i, o, _ = bench.WORKLOADS[workload[5:] if sync else workload]
-    s = (bench.SyncSetup if sync else bench.Setup)(fa, torch, D, n, i, o, 0, 0)
+    if workload in bench.ROUNDS:  # one aggregator round on its own buckets (bench.RoundSetup)
+        s = bench.RoundSetup(fa, torch, workload, 0)
+    else:
+        D, n, i, o, _ = bench.WORKLOADS[workload[5:] if sync else workload]
+        s = (bench.SyncSetup if sync else bench.Setup)(fa, torch, D, n, i, o, 0, 0)
     stream = torch.cuda.Stream()
     evs = []
     for k in range(launches):
