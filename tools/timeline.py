@@ -35,6 +35,7 @@ def summarize(tl, G):
         "start_spread_us": us(max(start) - t0),
         "workgroup_us": {"min": us(min(whole)), "median": us(statistics.median(whole)), "max": us(max(whole))},
         "end_spread_us": us(max(r[5] for r in rows) - min(r[5] for r in rows)),
+        "workgroup_median_per_xcd_us": {x: us(statistics.median(whole[x::8])) for x in range(8)},
     }
     if base["meetings"] == 0:  # a launch without meetings (one sized phase): the meeting stamps stay 0
         return base
@@ -77,7 +78,7 @@ def main():
         D, n, in_dt, out_dt, _ = bench.WORKLOADS[name]
         s = bench.Setup(fa, torch, D, n, in_dt, out_dt, 0, 0)
         torch.cuda.synchronize()
-        recs, ms = [], []
+        recs, ms, raws = [], [], []
         for i in range(launches + 2):
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(stream)
@@ -90,6 +91,8 @@ def main():
             if i >= 2:
                 recs.append(summarize(list(buf), G))
                 ms.append(a.elapsed_time(b))
+                if os.environ.get("TL_DUMP") == "1":  # raw per-workgroup times (us), launch by launch
+                    raws.append([round((buf[g * 8 + 5] - buf[g * 8]) * TICK_US, 1) for g in range(G)])
 
         def med(path):
             vals = []
@@ -107,10 +110,13 @@ def main():
         for key in ("workgroup_us", "read0_us", "wait0_us", "write_after_last_meeting_us"):
             if key in recs[0]:
                 out[key] = {k: med([key, k]) for k in recs[0][key]}
+        out["workgroup_median_per_xcd_us"] = {x: med(["workgroup_median_per_xcd_us", x]) for x in range(8)}
         if out["meetings"]:
             out["read0_median_per_xcd_us"] = {x: med(["read0_median_per_xcd_us", x]) for x in range(8)}
             out["lds0_median_per_xcd_us"] = {x: med(["lds0_median_per_xcd_us", x]) for x in range(8)}
         out["skew"] = os.environ.get("FA_PHASED_SKEW", "default")
+        if raws:
+            out["workgroup_us_per_launch"] = raws
         print(json.dumps(out), flush=True)
         s.close()
 
