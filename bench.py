@@ -372,24 +372,37 @@ def read_stream_peak(fa, torch, setup, stream, reps=7):
     return round(setup.D * n * 4 / (statistics.median(ms) * 1e-3) / 1e9, 1)
 
 
-def timed_loop(torch, setup, steps, warmup, stream, dist, barrier):
+def timed_loop(torch, setup, steps, warmup, stream, dist, barrier, per_launch=10):
+    """`steps` steps back to back, bracketed by barrier + synchronize: returns (wall seconds, region_ms, kern_ms).
+
+    The timed region holds nothing but the steps: one HIP event pair on the launch stream brackets all of
+    them (region_ms = their device time / steps -- the roofline's average launch duration), with no event
+    between steps (an event pair per step added 7-12 us of wall time per step, gpurun_out r02s71).
+    kern_ms: per-launch event pairs from a separate loop of `per_launch` steps after the timed region
+    (kernel_ms_min / _median)."""
     for i in range(warmup):
         setup.launch(i, stream)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    a.record(stream)
     for i in range(steps):
-        evs[i][0].record(stream)
         setup.launch(warmup + i, stream)
-        evs[i][1].record(stream)
+    b.record(stream)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    kern_ms = [a.elapsed_time(b) for a, b in evs]
-    return wall, kern_ms
+    region_ms = a.elapsed_time(b) / steps
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(per_launch)]
+    for i, (x, y) in enumerate(evs):
+        x.record(stream)
+        setup.launch(warmup + steps + i, stream)
+        y.record(stream)
+    torch.cuda.synchronize()
+    return wall, region_ms, [x.elapsed_time(y) for x, y in evs]
 
 
 def time_client_sharded(torch, dist, shard, setup, layout, n, world, device, stream, steps, warmup, chunks, barrier):
@@ -622,7 +635,7 @@ def main():
 
     # the dominant kernel alone (roofline), HIP events on its stream
     timeouts0 = fa.phased_timeouts(device)
-    wall_k, kern_ms = timed_loop(torch, setup, args.steps, args.warmup, stream, dist, barrier)
+    wall_k, kavg, kern_ms = timed_loop(torch, setup, args.steps, args.warmup, stream, dist, barrier)
     timeouts = fa.phased_timeouts(device) - timeouts0  # > 0: the persistent grid was not co-resident
     if args.layout == "range":
         wall = wall_k
@@ -631,7 +644,6 @@ def main():
                                    args.warmup, args.chunks, barrier)
     wall = max_over_ranks(wall)
 
-    kavg = statistics.mean(kern_ms)
     achieved = setup.algo_bytes() / (kavg * 1e-3) / 1e9
     read_peak = read_stream_peak(fa, torch, setup, stream) if args.layout == "range" and not under_profiler() \
         else None
@@ -663,8 +675,10 @@ def main():
                      "traffic_committed_profile": committed[0],
                      "traffic_live_error": live[1] if live[0] is None and live[1] else None,
                      "algorithmic_bytes_per_launch": setup.algo_bytes(),
-                     "kernel_ms_avg": round(kavg, 4), "kernel_ms_min": round(min(kern_ms), 4),
-                     "kernel_ms_median": round(statistics.median(kern_ms), 4),
+                     "kernel_ms_avg": round(kavg, 4),
+                     "kernel_ms_avg_source": "HIP events on the launch stream bracketing the %d timed steps" % args.steps,
+                     "kernel_ms_min": round(min(kern_ms), 4), "kernel_ms_median": round(statistics.median(kern_ms), 4),
+                     "kernel_ms_per_launch_events_avg": round(statistics.mean(kern_ms), 4),
                      "kernel": "rank %d's launch (%s)" % (rank, "its range of every bucket" if args.layout == "range"
                                                          else "its clients' local reduction"),
                      "phased_meeting_timeouts": timeouts,
@@ -707,7 +721,7 @@ def main():
                 if L == "weak_range":
                     s2 = Setup(fa, torch, D, n, in_dt, out_dt, rank * n, device)
                     torch.cuda.synchronize()
-                    w2, _ = timed_loop(torch, s2, steps2, 3, stream, dist, barrier)
+                    w2, _, _ = timed_loop(torch, s2, steps2, 3, stream, dist, barrier)
                     tb, desc2 = D * n * s_in * world, "weak scaling: every rank reduces its own %d-element slice " \
                                                        "of %d buckets, no collective" % (n, D)
                 else:
@@ -828,8 +842,7 @@ def single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier):
         sD, sn, si, so, sdesc = WORKLOADS[name]
         s = Setup(fa, torch, sD, sn, si, so, 0, device)
         torch.cuda.synchronize()
-        w2, km = timed_loop(torch, s, max(10, args.steps), 3, stream, dist, barrier)
-        ka = statistics.mean(km)
+        w2, ka, _ = timed_loop(torch, s, max(10, args.steps), 3, stream, dist, barrier)
         sec[name] = {"description": sdesc, "gib_s": round(s.input_bytes() * max(10, args.steps) / w2 / 2**30, 1),
                      "kernel_ms_avg": round(ka, 4),
                      "achieved_GBs": round(s.algo_bytes() / (ka * 1e-3) / 1e9, 1),
@@ -845,8 +858,7 @@ def single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier):
         for batched in (True, False):
             s = RoundSetup(fa, torch, name, device, batched=batched)
             torch.cuda.synchronize()
-            w2, km = timed_loop(torch, s, max(10, args.steps), 3, stream, dist, barrier)
-            ka = statistics.mean(km)
+            w2, ka, _ = timed_loop(torch, s, max(10, args.steps), 3, stream, dist, barrier)
             sec[name + ("" if batched else "_unbatched")] = {
                 "description": "one aggregator round: " + s.desc + ", buckets " + "/".join(map(str, s.sizes)) +
                                (" (phase 2 batched: fa_reduce_parts)" if batched else " (one launch per part)"),
@@ -857,8 +869,7 @@ def single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier):
 
     def one(key, s, desc):
         torch.cuda.synchronize()
-        _, km = timed_loop(torch, s, max(10, args.steps), 3, stream, dist, barrier)
-        ka = statistics.mean(km)
+        _, ka, _ = timed_loop(torch, s, max(10, args.steps), 3, stream, dist, barrier)
         sec[key] = {"description": desc, "kernel_ms_avg": round(ka, 4),
                     "achieved_GBs": round(s.algo_bytes() / (ka * 1e-3) / 1e9, 1),
                     "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

@@ -27,8 +27,7 @@ def main():
         for batched in (True, False):
             s = bench.RoundSetup(fa, torch, name, 0, batched=batched)
             torch.cuda.synchronize()
-            wall, km = bench.timed_loop(torch, s, steps, 5, stream, None, lambda: None)
-            ka = statistics.mean(km)
+            wall, ka, km = bench.timed_loop(torch, s, steps, 5, stream, None, lambda: None)
             print(json.dumps({"round": name, "batched": batched, "sizes": s.sizes, "D": s.D,
                               "round_ms_avg": round(ka, 4), "round_ms_min": round(min(km), 4),
                               "wall_ms": round(wall / steps * 1e3, 4),

@@ -30,8 +30,7 @@ def main():
     for W in ws:
         s = bench.Setup(fa, torch, D, n // W, "f32", "f32", 0, 0)
         torch.cuda.synchronize()
-        wall, km = bench.timed_loop(torch, s, steps, 5, stream, None, lambda: None)
-        ka = statistics.mean(km)
+        wall, ka, km = bench.timed_loop(torch, s, steps, 5, stream, None, lambda: None)
         print(json.dumps({"W": W, "elems": n // W, "sets": s.nsets, "kernel_ms_avg": round(ka, 4),
                           "kernel_ms_min": round(min(km), 4), "wall_ms": round(wall / steps * 1e3, 4),
                           "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / bench.HBM_PEAK_GBS, 4),
