@@ -57,18 +57,19 @@ def main():
         shutil.copy(os.path.join(src, "prof", "run_kernel_stats.csv"), os.path.join(prof, rnd + "_kernel_stats.csv"))
         g = per_kernel(kt)
         bj = os.path.join(src, "prof_bench.json")
-        steps = 0
+        steps = warmup = 0
         if os.path.exists(bj) and os.path.getsize(bj):
             line = json.loads(open(bj).read().strip().splitlines()[-1])
             summary["bench_under_profiler"] = line["roofline"]
-            steps = int(line["steps"])
-        # the bench's timed launches are the last `steps` of the dominant kernel (warm-ups come first)
+            steps, warmup = int(line["steps"]), int(line["warmup"])
+        # the dominant kernel's launches in bench order: warm-ups, the timed region's `steps`, then the
+        # separate per-launch-event loop (bench.timed_loop)
         summary["kernels"] = []
         for k, v in sorted(g.items(), key=lambda kv: -sum(kv[1])):
             rec = {"kernel": k[0], "grid": k[1], "calls": len(v), "avg_ns": round(sum(v) / len(v), 1), "min_ns": min(v)}
-            if steps and len(v) >= steps and not summary["kernels"]:
+            if steps and len(v) >= warmup + steps and not summary["kernels"]:
                 rec["timed_launches"] = steps
-                rec["timed_avg_ns"] = round(sum(v[-steps:]) / steps, 1)
+                rec["timed_avg_ns"] = round(sum(v[warmup:warmup + steps]) / steps, 1)
             summary["kernels"].append(rec)
 
     fetch = os.path.join(src, "pmc_FETCH_SIZE", "run_counter_collection.csv")
