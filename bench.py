@@ -546,6 +546,8 @@ def main():
                     help="with --ctx-multi: host-inclusive rounds (fa_submit_pinned of every client from host "
                          "memory, overlapped per GPU, + fa_finalize into host memory)")
     args = ap.parse_args()
+    if args.steps < 1 or args.warmup < 0:
+        ap.error("--steps must be >= 1 and --warmup >= 0")
     if args.ctx_multi:
         return ctx_multi(args)
 
