@@ -60,7 +60,8 @@ typedef enum {
  * into an fp32 partial, and an RCCL reduce-scatter over xGMI (one communicator per GPU, ncclCommInitAll in
  * this process) sums the partials piece by piece, overlapped with the reduction of the next piece
  * (fa_tuning.rs_chunks pieces; GPU g ends with block g of every piece, fa_rs_segments).  The summation
- * order changes: within 1e-6 of sum_k |w_k x_k| (bit-exact at n_gpus = 1).  Out dtype f32 only. */
+ * order changes: within 1e-6 of sum_k |w_k x_k| (bit-exact at n_gpus = 1).  A bf16 output is the fp32
+ * result rounded once to bf16 on each GPU after the exchange (so within one bf16 rounding of that). */
 #define FA_SHARD_CLIENT_RS 0x2
 /* Accumulate on arrival (range layout, FedAvg): as soon as receipts 0..k-1 of a round are all in, their
  * ordered chain is enqueued (continued in an fp32 accumulator), so the phase end only reduces the

@@ -252,6 +252,7 @@ struct Part {
     std::vector<char*> pool;       // per GPU: its client slots + the output (+ rs partial, eager acc)
     std::vector<size_t> stride;    // per GPU: bytes between consecutive slots
     std::vector<void*> dout;       // per GPU: the output (range: cnt elements of `out`; rs: its fp32 shard)
+    std::vector<void*> dout16;     // rs with a bf16 output: per GPU, its shard rounded to bf16 (the copy-out's source)
     std::vector<float*> partial;   // rs: per GPU, fp32 partial over its clients, npad elements
     std::vector<float*> acc;       // FA_ACCUMULATE_ON_ARRIVAL: per GPU, fp32 chain of the reduced prefix
     std::vector<hipEvent_t> done;  // per GPU: orders the copy-out after the reduction (see mark_done)
@@ -453,6 +454,7 @@ void free_part(fa_ctx* ctx, Part& p) {
     }
     p.pool.clear();
     p.dout.clear();
+    p.dout16.clear();
     p.done.clear();
 }
 
@@ -494,7 +496,7 @@ void set_rs_runs(Part& p, int G, int chunks) {
             if (hi > lo) rr.push_back(Run{off, lo, hi - lo});
             off += q;
         }
-        p.run_src[(size_t)g] = p.dout[(size_t)g];
+        p.run_src[(size_t)g] = p.out == FA_BF16 ? p.dout16[(size_t)g] : p.dout[(size_t)g];
     }
 }
 
@@ -577,7 +579,7 @@ int reduce_part(fa_ctx* ctx, Part& p, const float* w, hipStream_t s) {
         hipStream_t st = s ? s : r.compute;
         int rc = wait_copies(ctx, o, st);
         const void* last = slot_ptr(p, o, k);
-        if (rc || (rc = reduce_on(ctx, o, ctx->tuning.tu, &last, w, 1, p.n, p.in, p.partial[(size_t)o], FA_F32,
+        if (rc || (rc = reduce_on(ctx, o, ctx->tuning.tu, &last, w, 1, p.n, p.in, p.partial[(size_t)o], p.out,
                                   FA_LITERAL, p.divisor, nullptr, st)))
             return rc;
         if ((rc = mark_done(ctx, p, o, st))) return rc;
@@ -635,6 +637,17 @@ int reduce_part(fa_ctx* ctx, Part& p, const float* w, hipStream_t s) {
         }
         FA_NCCL(ncclGroupEnd());
         off += q;
+    }
+    if (p.out == FA_BF16) {  // the fp32 shard rounded once to bf16 (fma(x, 1, +0) = x: the sums are never -0)
+        const float one = 1.0f;
+        for (int g = 0; g < G; ++g) {
+            GpuRes& r = ctx->gpu[(size_t)g];
+            DeviceGuard dg(r.dev);
+            const void* shard = p.dout[(size_t)g];
+            int rc = reduce_on(ctx, g, ctx->tuning.tu, &shard, &one, 1, p.npad / (size_t)G, FA_F32,
+                               p.dout16[(size_t)g], FA_BF16, FA_FEDAVG, 1.0f, nullptr, r.comm);
+            if (rc) return rc;
+        }
     }
     for (int g = 0; g < G; ++g) {
         int rc = mark_done(ctx, p, g, ctx->gpu[(size_t)g].comm);
@@ -770,7 +783,7 @@ int submit_impl(fa_ctx* ctx, int part_id, int slot, const Gather& src, float wei
 // are issued before any is waited for, staged ones run on one host thread per GPU.
 int copy_output(fa_ctx* ctx, Part& p, const Gather& dst, bool pinned) {
     Trace tr("fa_copy_output n %d", (int)std::min<size_t>(p.n, 0x7fffffff));
-    const size_t so = p.rs ? 4 : dsize(p.out);
+    const size_t so = dsize(p.out);
     if (dst.total() != p.n * dsize(p.out))
         return fail(FA_ERR_ARG, "output of %zu bytes expected, destination holds %zu", p.n * dsize(p.out),
                     dst.total());
@@ -1211,7 +1224,6 @@ int fa_bucket_define(fa_ctx* ctx, int part_id, size_t n_elems, fa_dtype in, fa_d
     if (mode != FA_FEDAVG && mode != FA_LITERAL) return fail(FA_ERR_ARG, "bad mode");
     if (n_clients < 1) return fail(FA_ERR_ARG, "n_clients must be >= 1");
     const bool rs = (ctx->flags & FA_SHARD_CLIENT_RS) != 0;
-    if (rs && out != FA_F32) return fail(FA_ERR_ARG, "the rs layout reduce-scatters fp32 partials: out must be f32");
     auto it = ctx->parts.find(part_id);
     if (it != ctx->parts.end()) {
         free_part(ctx, it->second);
@@ -1253,6 +1265,7 @@ int fa_bucket_define(fa_ctx* ctx, int part_id, size_t n_elems, fa_dtype in, fa_d
     }
     p.pool.assign(G, nullptr);
     p.dout.assign(G, nullptr);
+    p.dout16.assign(G, nullptr);
     p.stride.assign(G, 0);
     p.partial.assign(G, nullptr);
     p.acc.assign(G, nullptr);
@@ -1269,11 +1282,12 @@ int fa_bucket_define(fa_ctx* ctx, int part_id, size_t n_elems, fa_dtype in, fa_d
         const size_t slot_elems = rs ? p.npad : p.cnt[g];
         const size_t held = (size_t)(p.c1[g] - p.c0[g]);
         p.stride[g] = slot_stride(slot_elems * dsize(in), ctx->tuning.slot_skew);
-        // one allocation: slots, then the output (range: cnt of `out`; rs: the fp32 shard), then the rs
-        // partial or the eager accumulator, each 4 KiB aligned
+        // one allocation: slots, then the output (range: cnt of `out`; rs: the fp32 shard, + its bf16
+        // rounding for a bf16 output), then the rs partial or the eager accumulator, each 4 KiB aligned
+        const size_t shard16_bytes = rs && out == FA_BF16 ? (p.npad / G * 2 + 4095) / 4096 * 4096 : 0;
         const size_t out_bytes = rs ? p.npad / G * 4 : p.cnt[g] * dsize(out);
         const size_t out_off = held * p.stride[g];
-        const size_t extra_off = out_off + (out_bytes + 4095) / 4096 * 4096;
+        const size_t extra_off = out_off + (out_bytes + 4095) / 4096 * 4096 + shard16_bytes;
         const size_t extra_bytes = rs ? p.npad * 4 : eager ? p.cnt[g] * 4 : 0;
         const size_t bytes = std::max<size_t>(1, extra_off + extra_bytes);
         if (hipMalloc((void**)&p.pool[g], bytes) != hipSuccess) {
@@ -1282,6 +1296,7 @@ int fa_bucket_define(fa_ctx* ctx, int part_id, size_t n_elems, fa_dtype in, fa_d
             return fail(FA_ERR_NOMEM, "device alloc of %zu B failed on GPU %zu", bytes, g);
         }
         p.dout[g] = p.pool[g] + out_off;
+        if (shard16_bytes) p.dout16[g] = p.pool[g] + out_off + (out_bytes + 4095) / 4096 * 4096;
         if (rs) {
             p.partial[g] = reinterpret_cast<float*>(p.pool[g] + extra_off);
             // the padding of every slot stays zero: the pieces past n reduce to 0

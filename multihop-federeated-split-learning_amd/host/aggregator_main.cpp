@@ -194,11 +194,6 @@ public:
                 std::cerr << "[aggregator] bucket " << r.model_part << ": parameters not all fp32 or all bf16\n";
                 std::exit(1);
             }
-            if (es == 2 && o_.rs) {
-                std::cerr << "[aggregator] --layout rs exchanges fp32 partials into an fp32 result: bucket "
-                          << r.model_part << " has bf16 parameters (use the range layout)\n";
-                std::exit(1);
-            }
             b.numel = (size_t)ar.param_numel();
             b.elem = es;
             const fa_dtype dt = es == 4 ? FA_F32 : FA_BF16;

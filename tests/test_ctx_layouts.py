@@ -36,52 +36,60 @@ def rs_ctx(fa, G):
 
 # ----------------------------------------------------------------- FA_SHARD_CLIENT_RS
 
-@pytest.mark.parametrize("n,D,chunks,bf16", [(1_000_003, 5, 1, False), (4_194_304, 8, 8, False),
-                                             (333_333, 3, 4, True), (63, 2, 3, False), (2_000_000, 130, 2, False)])
-def test_rs_layout_one_gpu_bitexact(fa, O, torch_gpu, n, D, chunks, bf16):
+@pytest.mark.parametrize("n,D,chunks,bf16,out_bf16", [
+    (1_000_003, 5, 1, False, False), (4_194_304, 8, 8, False, False), (333_333, 3, 4, True, False),
+    (63, 2, 3, False, False), (2_000_000, 130, 2, False, False),
+    (333_333, 3, 4, True, True), (1_000_003, 6, 3, False, True)])  # bf16 outputs: the shard rounded once
+def test_rs_layout_one_gpu_bitexact(fa, O, torch_gpu, n, D, chunks, bf16, out_bf16):
     """One GPU: the reduce-scatter over a one-rank communicator is a copy, so the pieces' chains are the
     single chain -- bit-exact, whatever the piece count; the slot padding stays out of the result."""
     w = O.weights(D)
     xs = host_clients(O, 60 + D, D, n, bf16)
+    ref = O.fedavg(xs, w, out_dtype="bf16") if bf16 and out_bf16 else \
+        O.f32_to_bf16(O.fedavg(xs, w)) if out_bf16 else O.fedavg(xs, w)  # f32 chain, rounded once
     with fa.Aggregator(1, rs=True) as agg:
         agg.set_tuning(rs_chunks=chunks)
         assert agg.get_tuning()["rs_chunks"] == chunks
-        agg.define(1, n, fa.BF16 if bf16 else fa.F32, fa.F32, D, fa.FEDAVG)
+        agg.define(1, n, fa.BF16 if bf16 else fa.F32, fa.BF16 if out_bf16 else fa.F32, D, fa.FEDAVG)
         for k in reversed(range(D)):
             agg.submit(1, k, xs[k], w[k])
-        assert_bits(agg.finalize(1), O.fedavg(xs, w))
+        assert_bits(agg.finalize(1), ref)
         # the device-resident round on the same slots
         agg.reduce(1, w)
-        assert_bits(agg.copy_output(1), O.fedavg(xs, w))
+        assert_bits(agg.copy_output(1), ref)
 
 
 def test_rs_layout_literal_and_errors(fa, O, torch_gpu):
     n, D = 100_001, 3
     xs = host_clients(O, 70, D, n)
     with fa.Aggregator(1, rs=True) as agg:
-        with pytest.raises(fa.FaError):
-            agg.define(1, n, fa.F32, fa.BF16, D, fa.FEDAVG)  # rs sums fp32 partials: f32 out only
         agg.define(1, n, fa.F32, fa.F32, D, fa.LITERAL)
         for k in [0, 2, 1]:
             agg.submit(1, k, xs[k])
         assert_bits(agg.finalize(1), O.literal(xs[1]))
+        agg.define(2, n, fa.F32, fa.BF16, D, fa.LITERAL)  # the last client's GPU writes bf16 directly
+        for k in [2, 0, 1]:
+            agg.submit(2, k, xs[k])
+        assert_bits(agg.finalize(2), O.f32_to_bf16(O.literal(xs[1])))  # fp32 literal, rounded once
         with pytest.raises(fa.FaError):
             agg.sync_states(1)
 
 
-@pytest.mark.parametrize("G,D,chunks,bf16", [(2, 7, 8, False), (4, 7, 3, False), (3, 2, 5, False), (4, 9, 1, False),
-                                             (2, 5, 4, True), (3, 6, 2, True)])
-def test_rs_layout_multi_gpu_tolerance(fa, O, torch_gpu, G, D, chunks, bf16):
+@pytest.mark.parametrize("G,D,chunks,bf16,out_bf16", [
+    (2, 7, 8, False, False), (4, 7, 3, False, False), (3, 2, 5, False, False), (4, 9, 1, False, False),
+    (2, 5, 4, True, False), (3, 6, 2, True, False), (3, 6, 2, True, True), (4, 7, 3, False, True)])
+def test_rs_layout_multi_gpu_tolerance(fa, O, torch_gpu, G, D, chunks, bf16, out_bf16):
     """G shards: clients dealt to the GPUs (a GPU may hold none: D < G), every GPU's shard holds its
     cyclic blocks; the whole result within 1e-6 of sum_k |w_k x_k| of the oracle's ordered chain (the
-    exchange adds per-GPU partials; bf16 inputs exchange fp32 partials too); the device-resident round
-    on the same slots agrees bit for bit."""
+    exchange adds per-GPU partials; bf16 inputs exchange fp32 partials too) -- for a bf16 output, plus
+    the one bf16 rounding of that sum (half a bf16 ulp, 2^-8 relative); the device-resident round on the
+    same slots agrees bit for bit."""
     n = 1_234_567
     w = O.weights(D)
     xs = host_clients(O, 71, D, n, bf16)
     with rs_ctx(fa, G) as agg:
         agg.set_tuning(rs_chunks=chunks)
-        agg.define(1, n, fa.BF16 if bf16 else fa.F32, fa.F32, D, fa.FEDAVG)
+        agg.define(1, n, fa.BF16 if bf16 else fa.F32, fa.BF16 if out_bf16 else fa.F32, D, fa.FEDAVG)
         for k in range(D):
             agg.submit(1, k, xs[k], w[k])
         got = agg.finalize(1)
@@ -91,7 +99,9 @@ def test_rs_layout_multi_gpu_tolerance(fa, O, torch_gpu, G, D, chunks, bf16):
     ref = O.fedavg(xs, w)
     vals = [O.bf16_to_f32(x) if bf16 else x for x in xs]
     absw = sum(abs(np.float64(wk)) * np.abs(x.astype(np.float64)) for wk, x in zip(w, vals))
-    err = np.abs(got.astype(np.float64) - ref) / (1e-6 * absw + 1e-30)
+    gotf = (O.bf16_to_f32(got) if out_bf16 else got).astype(np.float64)
+    bound = 1e-6 * absw + (2.0 ** -8 * np.abs(ref.astype(np.float64)) if out_bf16 else 0.0) + 1e-30
+    err = np.abs(gotf - ref) / bound
     assert np.all(err <= 1.0), float(err.max())
 
 
