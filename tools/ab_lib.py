@@ -2,6 +2,7 @@
 """A/B of two builds of the package on one bench workload (GPU box tool).
 
   python tools/ab_lib.py PKG_DIR [workload=northstar] [launches=30]      (workload "sync:<w>": state sync; round_c2/c3/c4: one round)
+  AB_TUNE="slot_skew=4096,..." sets the process tuning defaults (fa_set_tuning) before the context exists.
 
 PKG_DIR holds an ``__init__.py`` and ``lib/libfa.so`` (e.g. a build of an earlier commit); the
 workload's buckets are set up through that build's own context and timed with HIP events on
@@ -28,6 +29,9 @@ def main():
     sys.modules["mhfsl_amd"] = fa
     spec.loader.exec_module(fa)
     fa.lib()
+    tune = os.environ.get("AB_TUNE", "")  # e.g. "slot_skew=4096,rs_chunks=4": process tuning defaults
+    if tune:
+        fa.set_tuning(**{k: int(v) for k, v in (kv.split("=") for kv in tune.split(","))})
     import bench  # noqa: E402  (finds the package above in sys.modules)
     sync = workload.startswith("sync:")  # compute-node state sync (fa_sync_part) on a workload's shape
     if workload in bench.ROUNDS:  # one aggregator round on its own buckets (bench.RoundSetup)
