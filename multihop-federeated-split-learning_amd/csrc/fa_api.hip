@@ -40,6 +40,8 @@ namespace {
 
 thread_local std::string g_err;
 
+constexpr size_t kSkewAuto = SIZE_MAX;  // fa_tuning.slot_skew -2: chosen per bucket by slot_skew_for
+
 // Per-context tuning (fa_ctx_set_tuning); fa_set_tuning sets the process defaults that new contexts and
 // context-less fa_reduce_device calls start from.
 struct CtxTuning {
@@ -48,8 +50,8 @@ struct CtxTuning {
     // pools, profiles/r01_summary.json: sc1 stores 2.7% faster than nt, unroll 16 ~1% faster than 8,
     // block 128 2-3% faster than 256; the phased walk 1.269 ms on the north star in every pool).
     fa::Tuning tu{128, 0, 16, 1, 2, 4};
-    // Byte skew between consecutive client slots of one bucket (see slot_stride).
-    size_t slot_skew = 2048;
+    // Byte skew between consecutive client slots of one bucket (see slot_stride); kSkewAuto = by slot size.
+    size_t slot_skew = kSkewAuto;
     // FA_SHARD_CLIENT_RS: pieces per round (the reduce-scatter of piece c overlaps the reduce of c+1).
     int rs_chunks = 8;
 };
@@ -431,7 +433,16 @@ std::vector<std::pair<size_t, size_t>> rs_pieces(size_t npad, int G, int chunks)
 // 256-512 B skew -> 1.30-1.32 ms for 32 x 256 MiB vs 1.47-1.51 ms unskewed; re-laid out inside the
 // same six pools (round 1), 2048 B beat 512 B in every one (by 0.6-2.9%); 8 KiB + 512 and
 // 2 MiB + 512 are 7-12% slower.  Slots stay 16-byte aligned.
-size_t slot_stride(size_t bytes, size_t skew) { return (bytes + 4095) / 4096 * 4096 + skew; }
+// Re-measured on the phased kernel (tools/ab_lib.py AB_TUNE, three boxes, gpurun_out r02s79-s81): slots of
+// >= 64 MiB read faster at 512 B (one rank's share at 4 GPUs, 32 x 64 MiB: 0.320 vs 0.330-0.334 ms;
+// C4 0.7%, north star 0.4%, 2 ranks' share 0.6%), while 32 MiB slots (8 ranks' share) are 3-4% slower
+// at 512 and 9% slower at 1024 than at 2048, and C2's 48 MiB slots are equal.  The default (kSkewAuto)
+// therefore takes 512 B from 64 MiB up and 2048 B below.
+size_t slot_skew_for(size_t bytes, size_t skew) {
+    if (skew != kSkewAuto) return skew;
+    return bytes >= (size_t(64) << 20) ? 512 : 2048;
+}
+size_t slot_stride(size_t bytes, size_t skew) { return (bytes + 4095) / 4096 * 4096 + slot_skew_for(bytes, skew); }
 
 inline bool holds(const Part& p, int g, int k) { return k >= p.c0[(size_t)g] && k < p.c1[(size_t)g]; }
 inline char* slot_ptr(const Part& p, int g, int k) {
@@ -1036,8 +1047,9 @@ int tuning_from(const fa_tuning* t, CtxTuning* io) {
         nt.tu.store_policy = t->store_policy - 1;
     }
     if (t->slot_skew) {
-        if (t->slot_skew > 0 && t->slot_skew % 16) return fail(FA_ERR_ARG, "slot_skew must be a multiple of 16");
-        nt.slot_skew = t->slot_skew < 0 ? 0 : (size_t)t->slot_skew;
+        if (t->slot_skew < -2 || (t->slot_skew > 0 && t->slot_skew % 16))
+            return fail(FA_ERR_ARG, "slot_skew must be -2 (by slot size), -1 (none) or a multiple of 16");
+        nt.slot_skew = t->slot_skew == -2 ? kSkewAuto : t->slot_skew < 0 ? 0 : (size_t)t->slot_skew;
     }
     if (t->walk) {
         if (t->walk < 1 || t->walk > 6) return fail(FA_ERR_ARG, "walk must be 1..6");
@@ -1057,7 +1069,7 @@ void tuning_to(const CtxTuning& c, fa_tuning* t) {
     t->unroll = c.tu.unroll;
     t->load_policy = c.tu.load_nt ? 2 : 1;
     t->store_policy = c.tu.store_policy + 1;
-    t->slot_skew = (int)c.slot_skew;
+    t->slot_skew = c.slot_skew == kSkewAuto ? -2 : (int)c.slot_skew;
     t->walk = c.tu.walk + 1;
     t->rs_chunks = c.rs_chunks;
 }

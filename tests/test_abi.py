@@ -79,9 +79,12 @@ def test_tuning_roundtrip(fa):
     with pytest.raises(fa.FaError):
         fa.set_tuning(store_policy=5)
     assert fa.get_tuning()["store_policy"] == 4  # a rejected call changes nothing
+    assert before["slot_skew"] == -2  # default: by slot size
     fa.set_tuning(slot_skew=-1)
     assert fa.get_tuning()["slot_skew"] == 0
-    for bad in (dict(slot_skew=100), dict(walk=7), dict(rs_chunks=2000), dict(block=96)):
+    fa.set_tuning(slot_skew=-2)
+    assert fa.get_tuning()["slot_skew"] == -2
+    for bad in (dict(slot_skew=100), dict(slot_skew=-3), dict(walk=7), dict(rs_chunks=2000), dict(block=96)):
         with pytest.raises(fa.FaError):
             fa.set_tuning(**bad)
     fa.set_tuning(**{k: (v or -1) if k in ("max_blocks", "slot_skew") else v for k, v in before.items()})

@@ -492,7 +492,8 @@ def test_device_resident_part_round(fa, O, torch_gpu):
             ptrs.append(ptr)
             fa.fill_uniform(ptr, cnt, fa.F32, 50, k)
         gaps = {b - a for a, b in zip(ptrs, ptrs[1:])}
-        assert len(gaps) == 1 and gaps.pop() % 4096 == fa.get_tuning()["slot_skew"] % 4096
+        skew = fa.get_tuning()["slot_skew"]
+        assert len(gaps) == 1 and gaps.pop() % 4096 == (2048 if skew == -2 else skew % 4096)
         agg.reduce(3, w)
         assert_bits(agg.copy_output(3), O.fedavg(xs, w))
         # literal mode on the same layout: the last slot when nothing was submitted
@@ -503,7 +504,27 @@ def test_device_resident_part_round(fa, O, torch_gpu):
         assert_bits(agg.copy_output(4), O.literal(xs[-1]))
 
 
-@pytest.mark.parametrize("skew", [-1, 256, 512, 4096 + 512])
+def test_slot_skew_by_slot_size(fa, torch_gpu):
+    """The default skew (-2) is 2048 B below 64 MiB slots and 512 B from 64 MiB up (fa_api.hip
+    slot_skew_for); an explicit skew applies at every size."""
+    assert fa.get_tuning()["slot_skew"] == -2
+    with fa.Aggregator(1) as agg:
+        for part, n, want in ((1, (64 << 20) // 4 - 1024, 2048), (2, (64 << 20) // 4, 512), (3, (64 << 20) // 2, 512)):
+            dt = fa.BF16 if part == 3 else fa.F32
+            agg.define(part, n, dt, dt, 3, fa.FEDAVG)
+            p = [agg.slot(part, 0, k)[0] for k in range(3)]
+            assert p[1] - p[0] == p[2] - p[1] == (64 << 20) - (4096 if part == 1 else 0) + want
+    before = fa.get_tuning()
+    try:
+        fa.set_tuning(slot_skew=2048)
+        with fa.Aggregator(1) as agg:
+            agg.define(1, (64 << 20) // 4, fa.F32, fa.F32, 2, fa.FEDAVG)
+            assert agg.slot(1, 0, 1)[0] - agg.slot(1, 0, 0)[0] == (64 << 20) + 2048
+    finally:
+        fa.set_tuning(slot_skew=before["slot_skew"] or -1)
+
+
+@pytest.mark.parametrize("skew", [-1, -2, 256, 512, 4096 + 512])
 def test_slot_skew_does_not_change_bits(fa, O, torch_gpu, skew):
     before = fa.get_tuning()
     try:
