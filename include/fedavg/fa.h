@@ -215,7 +215,7 @@ typedef struct {
     int load_policy;  /* client loads: 1 default cache policy, 2 non-temporal */
     int store_policy; /* output stores: 1 plain, 2 nt, 3 sc1 (write-through), 4 sc0 sc1 */
     int slot_skew;    /* bytes between consecutive client slots beyond 4 KiB alignment (multiple of 16);
-                         -1 = none, -2 (default) = by slot size: 512 for slots of >= 64 MiB, else 2048;
+                         -1 = none, -2 (default) = by slot size: 512 for slots of >= 48 MiB, else 2048;
                          applies to buckets defined afterwards */
     int walk;         /* FedAvg grid walk over a bucket: 1 linear, 2 each XCD's workgroups own one contiguous
                          eighth, 3 the same with the odd eighths walked backwards (one-shot grid only),

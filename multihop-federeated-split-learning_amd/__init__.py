@@ -187,7 +187,7 @@ STORE_PLAIN, STORE_NT, STORE_SC1, STORE_SC01 = 1, 2, 3, 4
 
 def set_tuning(block=0, max_blocks=0, unroll=0, load_policy=0, store_policy=0, slot_skew=0, walk=0, rs_chunks=0):
     """fa_set_tuning (process defaults); every argument 0 = keep.  max_blocks -1 = one-shot grid,
-    slot_skew -1 = none, -2 = by slot size (the default: 512 B from 64 MiB slots up, else 2048)."""
+    slot_skew -1 = none, -2 = by slot size (the default: 512 B from 48 MiB slots up, else 2048)."""
     t = _Tuning(block, max_blocks, unroll, load_policy, store_policy, slot_skew, walk, rs_chunks)
     check(lib().fa_set_tuning(ctypes.byref(t)))
 

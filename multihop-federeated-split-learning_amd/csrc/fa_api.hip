@@ -433,14 +433,15 @@ std::vector<std::pair<size_t, size_t>> rs_pieces(size_t npad, int G, int chunks)
 // 256-512 B skew -> 1.30-1.32 ms for 32 x 256 MiB vs 1.47-1.51 ms unskewed; re-laid out inside the
 // same six pools (round 1), 2048 B beat 512 B in every one (by 0.6-2.9%); 8 KiB + 512 and
 // 2 MiB + 512 are 7-12% slower.  Slots stay 16-byte aligned.
-// Re-measured on the phased kernel (tools/ab_lib.py AB_TUNE, three boxes, gpurun_out r02s79-s81): slots of
-// >= 64 MiB read faster at 512 B (one rank's share at 4 GPUs, 32 x 64 MiB: 0.320 vs 0.330-0.334 ms;
-// C4 0.7%, north star 0.4%, 2 ranks' share 0.6%), while 32 MiB slots (8 ranks' share) are 3-4% slower
-// at 512 and 9% slower at 1024 than at 2048, and C2's 48 MiB slots are equal.  The default (kSkewAuto)
-// therefore takes 512 B from 64 MiB up and 2048 B below.
+// Re-measured on the phased kernel (tools/ab_lib.py AB_TUNE, fresh processes on several boxes, gpurun_out
+// r02s79-s92): slots of >= 56 MiB read faster at 512 B (one rank's share at 4 GPUs, 32 x 64 MiB: 0.320
+// vs 0.330-0.334 ms; C4 0.7%, north star 0.4%, 2 ranks' share 0.6%, the C3 round's 56 MiB bf16 slots
+// 0.8%), while 32 MiB slots (8 ranks' share) are 3-4% slower at 512 and 9% slower at 1024 than at 2048,
+// and C2's 47.9 MiB slots are equal.  The default (kSkewAuto) therefore takes 512 B from 48 MiB up and
+// 2048 B below.
 size_t slot_skew_for(size_t bytes, size_t skew) {
     if (skew != kSkewAuto) return skew;
-    return bytes >= (size_t(64) << 20) ? 512 : 2048;
+    return bytes >= (size_t(48) << 20) ? 512 : 2048;
 }
 size_t slot_stride(size_t bytes, size_t skew) { return (bytes + 4095) / 4096 * 4096 + slot_skew_for(bytes, skew); }
 

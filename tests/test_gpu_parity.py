@@ -505,15 +505,15 @@ def test_device_resident_part_round(fa, O, torch_gpu):
 
 
 def test_slot_skew_by_slot_size(fa, torch_gpu):
-    """The default skew (-2) is 2048 B below 64 MiB slots and 512 B from 64 MiB up (fa_api.hip
+    """The default skew (-2) is 2048 B below 48 MiB slots and 512 B from 48 MiB up (fa_api.hip
     slot_skew_for); an explicit skew applies at every size."""
     assert fa.get_tuning()["slot_skew"] == -2
     with fa.Aggregator(1) as agg:
-        for part, n, want in ((1, (64 << 20) // 4 - 1024, 2048), (2, (64 << 20) // 4, 512), (3, (64 << 20) // 2, 512)):
+        for part, n, want in ((1, (48 << 20) // 4 - 1024, 2048), (2, (48 << 20) // 4, 512), (3, (48 << 20) // 2, 512)):
             dt = fa.BF16 if part == 3 else fa.F32
             agg.define(part, n, dt, dt, 3, fa.FEDAVG)
             p = [agg.slot(part, 0, k)[0] for k in range(3)]
-            assert p[1] - p[0] == p[2] - p[1] == (64 << 20) - (4096 if part == 1 else 0) + want
+            assert p[1] - p[0] == p[2] - p[1] == (48 << 20) - (4096 if part == 1 else 0) + want
     before = fa.get_tuning()
     try:
         fa.set_tuning(slot_skew=2048)
