@@ -60,6 +60,17 @@ WORKLOADS = {
     "ns_w8": (32, 8 << 20, "f32", "f32", "north star, one rank's share at 8 GPUs (strong scaling): 32 x 32 MiB"),
 }
 ROTATE_MIN_BYTES = 1 << 30  # rotate input sets until a step's working set no longer fits the 256 MiB MALL
+T_START = time.monotonic()
+# Wall-clock budget of one bench run (the driver stops a bench at 600 s).  Every optional leg is bounded by
+# what is left of it: the live PMC passes (100 s each at most), the CPU baseline (its variants only while
+# more than 250 s are left, 60 s each), the multi-GPU secondaries of the N = 1 run (ctx_multi_secondaries).
+# Worst case before the line is printed: 2 x 100 + 120 + 230 of variants is cut at 250 s left, then the
+# single-GPU secondaries (~60-90 s of device work) and ctx children only until BUDGET_S - 30 s.
+BUDGET_S = float(os.environ.get("FA_BENCH_BUDGET_S", "480"))
+
+
+def budget_left():
+    return T_START + BUDGET_S - time.monotonic()
 
 
 def load_pkg():
@@ -97,7 +108,7 @@ def cpu_baseline(D, sample_elems, reps):
     sample = "D=%d clients x %d fp32 elements (%.0f MiB per client), %d timed reps after 1 warm-up" % (
         D, sample_elems, sample_elems * 4 / 2**20, reps)
 
-    def run(args, timeout=600):
+    def run(args, timeout=120):
         out = subprocess.run([harness] + [str(a) for a in args], capture_output=True, text=True, timeout=timeout,
                              check=True).stdout
         return json.loads(out.strip().splitlines()[-1])
@@ -110,11 +121,17 @@ def cpu_baseline(D, sample_elems, reps):
                    "sample": sample}
             extra = {}
             try:
-                r1 = run(["bench-fedavg", sample_elems, D, 1, max(2, reps // 4)])
+                def variant_timeout():
+                    left = budget_left() - 250
+                    if left < 10:
+                        raise TimeoutError("bench time budget: variants skipped")
+                    return min(60, left)
+                r1 = run(["bench-fedavg", sample_elems, D, 1, max(2, reps // 4)], timeout=variant_timeout())
                 extra["fedavg_1_core"] = {"value": round(r1["gib_s"], 3), "unit": "GiB/s", "cores": 1}
                 for t in (threads, 1):
                     for mode in ("", "arith"):
-                        lit = run(["bench-literal", 1, 1, 9, 3, 10, 8, t, 2] + ([mode] if mode else []), timeout=300)
+                        lit = run(["bench-literal", 1, 1, 9, 3, 10, 8, t, 2] + ([mode] if mode else []),
+                                  timeout=variant_timeout())
                         key = "reference_receive_loop" + ("_arith_only" if mode else "") + ("_1_core" if t == 1 else "")
                         extra[key] = {
                             "value": round(lit["gib_s"], 3), "unit": "GiB/s of parameters received", "cores": t,
@@ -165,7 +182,7 @@ def under_profiler():
     return os.environ.get("FA_BENCH_PMC_CHILD") == "1" or any(k.startswith("ROCPROF") for k in os.environ)
 
 
-def live_traffic(workload, timeout=150):
+def live_traffic(workload, timeout=100):
     """HBM bytes per launch of this run's dominant kernel, measured now: two rocprofv3 PMC passes (FETCH_SIZE,
     then WRITE_SIZE, each its own run as MI355X_MICROARCH.md prescribes) of a short single-GPU bench of the
     same workload, started as child processes before this process touches the GPU.  gfx950 correction:
@@ -641,15 +658,24 @@ def main():
     timeouts = fa.phased_timeouts(device) - timeouts0  # > 0: the persistent grid was not co-resident
     if args.layout == "range":
         wall = wall_k
-    else:
-        wall = time_client_sharded(torch, dist, shard, setup, args.layout, n, world, device, stream, args.steps,
-                                   args.warmup, args.chunks, barrier)
+    else:  # the local reductions run beside RCCL's kernels: the one-shot walk (shard.py, "Overlap")
+        walk0 = fa.get_tuning()["walk"]
+        fa.set_tuning(walk=shard.OVERLAP_WALK)
+        try:
+            wall = time_client_sharded(torch, dist, shard, setup, args.layout, n, world, device, stream,
+                                       args.steps, args.warmup, args.chunks, barrier)
+        finally:
+            fa.set_tuning(walk=walk0)
+        timeouts += fa.phased_timeouts(device) - timeouts0 - timeouts
     wall = max_over_ranks(wall)
 
     achieved = setup.algo_bytes() / (kavg * 1e-3) / 1e9
     read_peak = read_stream_peak(fa, torch, setup, stream) if args.layout == "range" and not under_profiler() \
         else None
-    committed = traffic_from_profile(args.workload, world, strong and args.layout == "range")
+    # ranks sharing one GPU (rehearsal) run the one-shot walk, so no committed profile of the phased kernel
+    # describes their launches: no traffic then
+    committed = (None, None) if shared_gpus else traffic_from_profile(args.workload, world,
+                                                                      strong and args.layout == "range")
     traffic, traffic_src = live if live[0] is not None else committed
     line = {
         "metric": "GiB/s aggregated (device-resident), D-client fp32 bucket FedAvg reduce",
@@ -683,7 +709,7 @@ def main():
                      "kernel_ms_per_launch_events_avg": round(statistics.mean(kern_ms), 4),
                      "kernel": "rank %d's launch (%s)" % (rank, "its range of every bucket" if args.layout == "range"
                                                          else "its clients' local reduction"),
-                     "phased_meeting_timeouts": timeouts,
+                     "phased_meeting_timeouts": int(max_over_ranks(timeouts)),
                      "read_stream_peak": read_peak, "frac_of_read_stream":
                          round(achieved / read_peak, 4) if read_peak else None},
         "cpu_baseline": cpu,
@@ -695,7 +721,7 @@ def main():
         setup.close()
         line["secondary"] = single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier)
         if n_dev >= 2:
-            line["secondary"].update(ctx_multi_secondaries(n_dev))
+            line["secondary"].update(ctx_multi_secondaries(n_dev, T_START + BUDGET_S))
 
     printer = LinePrinter(rank, line_out)
     if world > 1 and not args.no_secondary and args.layout == "range":
@@ -731,12 +757,21 @@ def main():
                     s2 = Setup(fa, torch, c1 - c0, n, in_dt, out_dt, 0, device, client0=c0)
                     s2.w = Setup._weights(D)[c0:c1]
                     torch.cuda.synchronize()
-                    w2 = time_client_sharded(torch, dist, shard, s2, L, n, world, device, stream, steps2, 3,
-                                             args.chunks, barrier)
+                    # the local reductions run beside RCCL's kernels: the one-shot walk (shard.py, "Overlap")
+                    walk0 = fa.get_tuning()["walk"]
+                    fa.set_tuning(walk=shard.OVERLAP_WALK)
+                    try:
+                        w2 = time_client_sharded(torch, dist, shard, s2, L, n, world, device, stream, steps2, 3,
+                                                 args.chunks, barrier)
+                    finally:
+                        fa.set_tuning(walk=walk0)
                     tb, desc2 = D * n * s_in, layout_desc_of(L, c1 - c0, world, args.chunks)
+                t2 = fa.phased_timeouts(device) - timeouts0 - timeouts
                 w2 = max_over_ranks(w2)
                 sec[L] = {"description": desc2, "clients": D, "steps": steps2,
-                          "ms_per_step": round(w2 / steps2 * 1e3, 4), "gib_s": round(tb * steps2 / w2 / 2**30, 1)}
+                          "ms_per_step": round(w2 / steps2 * 1e3, 4), "gib_s": round(tb * steps2 / w2 / 2**30, 1),
+                          "phased_meeting_timeouts": int(max_over_ranks(t2))}
+                timeouts += t2
                 s2.close()
             except Exception as e:  # noqa: BLE001 -- the ranks may now disagree: report and leave
                 traceback.print_exc()
@@ -795,6 +830,7 @@ def ctx_multi(args):
     else:
         def step():
             agg.reduce(1, w)
+    t_before = [fa.phased_timeouts(g) for g in range(G)]
     for _ in range(args.warmup):
         step()
     agg.sync()
@@ -803,17 +839,21 @@ def ctx_multi(args):
         step()
     agg.sync()
     dt = (time.perf_counter() - t0) / args.steps
+    # > 0: a phased launch's grid was not co-resident on some GPU (the rs layout never takes that kernel)
+    timeouts = sum(fa.phased_timeouts(g) - t_before[g] for g in range(G))
     out = {"layout": args.ctx_multi, "gpus": G, "workload": args.workload, "description": desc, "clients": D,
            "elems_per_client": n, "host_inclusive": args.h2d, "ms_per_round": round(dt * 1e3, 4),
            "gib_s": round(D * n * s_in / dt / 2**30, 1), "steps": args.steps,
-           "tuning": agg.get_tuning()}
+           "phased_meeting_timeouts": timeouts, "tuning": agg.get_tuning()}
     agg.close()
     print(json.dumps(out), flush=True)
 
 
-def ctx_multi_secondaries(n_dev, timeout=150):
+def ctx_multi_secondaries(n_dev, deadline, timeout=120):
     """On a node with several visible GPUs, the N = 1 run also times the in-process multi-GPU layouts over
-    all of them (child processes, time-limited: a stalled collective cannot take the main line with it)."""
+    all of them (child processes, time-limited: a stalled collective cannot take the main line with it).
+    Every child gets min(timeout, what is left before `deadline` - a 30 s margin); once less than 20 s is left
+    the rest are skipped (reported as such), so the line is printed before the driver's limit (600 s)."""
     res = {}
     # BASELINE C4 is quoted on 4 GPUs (RCCL reduce-scatter), C5 on 8 (128 x 1 GiB buckets arriving from host
     # memory, H2D overlapped over every GPU's link); the north star on all of them
@@ -823,11 +863,15 @@ def ctx_multi_secondaries(n_dev, timeout=150):
         key = "ctx_%s_%s%s_%dgpu" % (layout, workload, "_h2d" if h2d else "", gpus)
         if key in res:
             continue
+        left = deadline - time.monotonic() - 30  # deadline = T_START + BUDGET_S
+        if left < 20:
+            res[key] = {"skipped": "the bench's time budget is spent (FA_BENCH_BUDGET_S)"}
+            continue
         try:
             r = subprocess.run([sys.executable, os.path.abspath(__file__), "--ctx-multi", layout, "--workload",
                                 workload, "--ctx-gpus", str(gpus)] + (["--h2d", "--steps", "3", "--warmup", "1"] if h2d
                                                                       else ["--steps", "10", "--warmup", "2"]),
-                               capture_output=True, text=True, timeout=timeout)
+                               capture_output=True, text=True, timeout=min(timeout, left))
             res[key] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
                 {"error": "rc %d: %s" % (r.returncode, r.stderr[-300:])}
         except Exception as e:  # noqa: BLE001 -- reported, never fatal

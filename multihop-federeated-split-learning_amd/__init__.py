@@ -87,6 +87,9 @@ def lib():
         "fa_reduce_device": (I, [P, I, P, P, I, S, I, P, I, I, P, P]),
         "fa_fill_uniform": (I, [P, S, I, U64, U32, U64, P]),
         "fa_diag_read_stream": (I, [P, I, S, P]),  # diagnostics (outside fa.h)
+        "fa_diag_plan_chain": (I, [I, I, S, I, I, I, ctypes.POINTER(I), ctypes.POINTER(ctypes.c_longlong)]),
+        "fa_diag_rs_plan": (I, [S, I, I, I, I, I, I, ctypes.POINTER(I), ctypes.POINTER(I),
+                                ctypes.POINTER(ctypes.c_longlong)]),
         "fa_set_tuning": (I, [ctypes.POINTER(_Tuning)]),
         "fa_get_tuning": (I, [ctypes.POINTER(_Tuning)]),
     }
@@ -167,6 +170,27 @@ def diag_read_stream(buffers, n, stream=None):
     (n elements each, n % 4 == 0, 16-byte aligned) on `stream`; time it with events on that stream."""
     arr = (ctypes.c_void_p * len(buffers))(*[_addr(b) for b in buffers])
     check(lib().fa_diag_read_stream(arr, len(buffers), n, _stream(stream)))
+
+
+PLAN_ONE_SHOT, PLAN_SCALAR, PLAN_PHASED = 0, 1, 2
+
+
+def plan_chain(in_dtype, out_dtype, n, n_clients, walk=0, cus=256):
+    """fa_diag_plan_chain (diagnostic, host arithmetic): (kind, phases) of the launch one FedAvg chain over a
+    16-byte aligned bucket of n elements takes under fa_tuning.walk `walk` (0 = the process default) on `cus`
+    CUs; kind PLAN_PHASED with phases > 1 means chip-wide meetings."""
+    k, ph = ctypes.c_int(), ctypes.c_longlong()
+    check(lib().fa_diag_plan_chain(in_dtype, out_dtype, n, n_clients, walk, cus, ctypes.byref(k), ctypes.byref(ph)))
+    return k.value, ph.value
+
+
+def rs_plan(n, n_gpus, n_clients, chunks=0, in_dtype=F32, out_dtype=F32, cus=256):
+    """fa_diag_rs_plan (diagnostic): (launches, phased launches, most phases of one launch) that one
+    FA_SHARD_CLIENT_RS round enqueues for a bucket of n elements (the process-default tuning)."""
+    a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_longlong()
+    check(lib().fa_diag_rs_plan(n, n_gpus, n_clients, chunks, in_dtype, out_dtype, cus, ctypes.byref(a),
+                                ctypes.byref(b), ctypes.byref(c)))
+    return a.value, b.value, c.value
 
 
 def _tuning_dict(t):

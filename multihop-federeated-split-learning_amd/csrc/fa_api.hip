@@ -116,6 +116,7 @@ struct DeviceGuard {
 constexpr size_t kStageBytes = 32u << 20;  // pinned staging chunk per buffer
 constexpr size_t kShardUnit = 64;          // range shards / rs pieces: multiples of 64 elements (16-B phase kept)
 constexpr int kMaxSegments = 256;          // buckets per batched launch
+constexpr int kSegRing = 4;                // device segment tables per GPU (GpuRes::seg)
 
 // Host memcpy into / out of the pinned staging chunks, split over worker threads:
 // one thread copies ~8-10 GB/s, a PCIe Gen5 x16 link takes ~50 GB/s.  One pool per GPU, so the GPUs of a
@@ -134,6 +135,25 @@ public:
         cv_.notify_all();
         for (auto& t : th_) t.join();
     }
+    int size() const { return n_; }
+    // fn(i) for every i in [0, size()): i = 0 on the calling thread, the others on the workers; returns when
+    // all have.  One caller at a time.
+    void run(const std::function<void(int)>& fn) {
+        if (n_ == 1) {
+            fn(0);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> g(m_);
+            job_ = &fn;
+            pending_ = n_ - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        fn(0);
+        std::unique_lock<std::mutex> l(m_);
+        done_.wait(l, [&] { return pending_ == 0; });
+    }
     // dst[0, len) = src(0, len), split over the workers (the caller copies part 0).
     void copy(char* dst, size_t len, const std::function<void(size_t, size_t, char*)>& src) {
         if (n_ == 1 || len < (4u << 20)) {
@@ -141,20 +161,10 @@ public:
             return;
         }
         const size_t per = (len / n_ + 4095) / 4096 * 4096;
-        std::function<void(int)> part = [&](int p) {
+        run([&](int p) {
             const size_t lo = std::min(len, (size_t)p * per), hi = std::min(len, lo + per);
             if (hi > lo) src(lo, hi - lo, dst + lo);
-        };
-        {
-            std::lock_guard<std::mutex> g(m_);
-            job_ = &part;
-            pending_ = n_ - 1;
-            ++gen_;
-        }
-        cv_.notify_all();
-        part(0);
-        std::unique_lock<std::mutex> l(m_);
-        done_.wait(l, [&] { return pending_ == 0; });
+        });
     }
 
 private:
@@ -192,21 +202,16 @@ int default_copy_threads() {
     return (int)std::max(1u, std::min(8u, hw / 2));
 }
 
-// Runs fn(g) for g in [0, G): G > 1 on one thread per GPU (the host-side staging of each GPU is
-// independent), returning the first non-zero status.
-int for_each_gpu(int G, const std::function<int(int)>& fn) {
-    if (G == 1) return fn(0);
+// Runs fn(g) for g in [0, G): G > 1 on the context's persistent per-GPU workers (the host-side staging of
+// each GPU is independent; no thread is created per call), returning the first non-zero status.
+int for_each_gpu(CopyPool* workers, int G, const std::function<int(int)>& fn) {
+    if (G == 1 || !workers) return fn(0);
     std::vector<int> rc((size_t)G, FA_OK);
     std::vector<std::string> err((size_t)G);
-    std::vector<std::thread> th;
-    for (int g = 1; g < G; ++g)
-        th.emplace_back([&, g] {
-            rc[(size_t)g] = fn(g);
-            if (rc[(size_t)g]) err[(size_t)g] = g_err;  // g_err is thread-local
-        });
-    rc[0] = fn(0);
-    if (rc[0]) err[0] = g_err;
-    for (auto& t : th) t.join();
+    workers->run([&](int g) {
+        rc[(size_t)g] = fn(g);
+        if (rc[(size_t)g]) err[(size_t)g] = g_err;  // g_err is thread-local
+    });
     for (int g = 0; g < G; ++g)
         if (rc[(size_t)g]) {
             g_err = err[(size_t)g];
@@ -228,10 +233,19 @@ struct GpuRes {
     hipEvent_t step_ev = nullptr;  // orders the rs exchange of a piece after its reduction
     void* scratch = nullptr;       // fp32 chain accumulator for bf16-out, D > kMaxClients
     size_t scratch_bytes = 0;
-    fa::SegDesc* seg_host = nullptr;  // pinned segment table of the batched launch
-    fa::SegDesc* seg_dev = nullptr;
-    hipEvent_t seg_ev = nullptr;      // the table's last upload (the host copy is rewritten after it)
-    size_t seg_uploaded = 0;          // bytes of the table seg_dev holds (== seg_host's first bytes)
+    // Device segment tables of batched launches (fa_reduce_parts beyond the kernel-argument table): a ring,
+    // so a changed table is uploaded into a slot whose last launch is long done; each slot remembers the
+    // stream and event of its last launch, which orders a reuse or an overwrite after it (allocated on
+    // first use).
+    struct SegTable {
+        fa::SegDesc* host = nullptr;  // pinned staging of the upload
+        fa::SegDesc* dev = nullptr;
+        hipEvent_t ev = nullptr;      // recorded after the slot's last launch (its upload precedes it)
+        hipStream_t stream = nullptr; // the stream of that launch
+        size_t bytes = 0;             // bytes of the table the slot holds
+    };
+    SegTable seg[kSegRing];
+    int seg_last = -1;                // the slot of the last batched launch
     std::unique_ptr<CopyPool> pool;
     ncclComm_t nccl = nullptr;
 };
@@ -278,6 +292,7 @@ struct fa_ctx {
     CtxTuning tuning;
     std::vector<GpuRes> gpu;
     std::map<int, Part> parts;
+    std::unique_ptr<CopyPool> workers;  // G > 1: one persistent host thread per GPU (for_each_gpu)
 };
 
 namespace {
@@ -443,7 +458,19 @@ size_t slot_skew_for(size_t bytes, size_t skew) {
     if (skew != kSkewAuto) return skew;
     return bytes >= (size_t(48) << 20) ? 512 : 2048;
 }
-size_t slot_stride(size_t bytes, size_t skew) { return (bytes + 4095) / 4096 * 4096 + slot_skew_for(bytes, skew); }
+// experiment knob (tools/): FA_SLOT_ALIGN overrides the 4 KiB alignment of a slot's length before the skew
+size_t slot_align() {
+    static const size_t v = [] {
+        const char* e = std::getenv("FA_SLOT_ALIGN");
+        const long long a = e ? std::atoll(e) : 0;
+        return a >= 4096 && a % 4096 == 0 ? (size_t)a : (size_t)4096;
+    }();
+    return v;
+}
+size_t slot_stride(size_t bytes, size_t skew) {
+    const size_t a = slot_align();
+    return (bytes + a - 1) / a * a + slot_skew_for(bytes, skew);
+}
 
 inline bool holds(const Part& p, int g, int k) { return k >= p.c0[(size_t)g] && k < p.c1[(size_t)g]; }
 inline char* slot_ptr(const Part& p, int g, int k) {
@@ -532,6 +559,20 @@ int chain_range(fa_ctx* ctx, Part& p, int g, int k0, int k1, const float* w, hip
                      last ? p.out : FA_F32, FA_FEDAVG, p.divisor, init, st);
 }
 
+// Every launch of the rs layout (the piece reductions, the bf16 rounding, the test-only emulated exchange) may
+// run beside an RCCL exchange -- of the previous piece, or of the previous round.  RCCL's blocks need CU slots
+// and LDS, which a persistent phased grid holds on every CU (all 160 KiB of it) for its whole launch: the
+// exchange would wait for the reduction it is meant to overlap, and a phased grid that RCCL's blocks keep from
+// being co-resident would spin at its meetings (769 bounded waits ran out, 24 ms per launch
+// instead of 1.4).  So the rs layout never takes the phased kernel: its launches use the one-shot grid
+// (walk 2, each XCD's workgroups on one contiguous eighth), which retires workgroup by workgroup and leaves
+// room for RCCL's blocks as it goes.  fa_diag_rs_plan shows the resulting plan to the CPU suite.
+fa::Tuning rs_launch_tuning(const fa::Tuning& tu) {
+    fa::Tuning r = tu;
+    if (r.walk >= 3) r.walk = 1;
+    return r;
+}
+
 // FA_TEST_SHARED_DEVICE with FA_SHARD_CLIENT_RS: RCCL refuses two ranks on one device, so the
 // reduce-scatter of piece [a, a + G q) is replaced by its definition -- shard g block [off, off + q) :=
 // sum over h of partial_h[a + g q, a + (g + 1) q) in rank order, one launch per shard on its exchange
@@ -547,7 +588,7 @@ int emulated_reduce_scatter(fa_ctx* ctx, Part& p, size_t a, size_t q, size_t off
         GpuRes& r = ctx->gpu[(size_t)g];
         DeviceGuard dg(r.dev);
         for (int h = 0; h < G; ++h) ptrs[(size_t)h] = p.partial[(size_t)h] + a + (size_t)g * q;
-        int rc = reduce_on(ctx, g, ctx->tuning.tu, ptrs.data(), ones.data(), G, q, FA_F32,
+        int rc = reduce_on(ctx, g, rs_launch_tuning(ctx->tuning.tu), ptrs.data(), ones.data(), G, q, FA_F32,
                            static_cast<float*>(p.dout[(size_t)g]) + off, FA_F32, FA_FEDAVG, 1.0f, nullptr, r.comm);
         if (rc) return rc;
     }
@@ -601,6 +642,7 @@ int reduce_part(fa_ctx* ctx, Part& p, const float* w, hipStream_t s) {
         return FA_OK;
     }
     const auto pieces = rs_pieces(p.npad, G, ctx->tuning.rs_chunks);
+    const fa::Tuning rtu = rs_launch_tuning(ctx->tuning.tu);
     for (int g = 0; g < G; ++g) {
         GpuRes& r = ctx->gpu[(size_t)g];
         DeviceGuard dg(r.dev);
@@ -624,8 +666,8 @@ int reduce_part(fa_ctx* ctx, Part& p, const float* w, hipStream_t s) {
             if (k1 > k0) {
                 std::vector<const void*> ptrs;
                 for (int k = k0; k < k1; ++k) ptrs.push_back(slot_ptr(p, g, k) + a * dsize(p.in));
-                int rc = reduce_on(ctx, g, ctx->tuning.tu, ptrs.data(), w + k0, k1 - k0, len, p.in,
-                                   p.partial[(size_t)g] + a, FA_F32, FA_FEDAVG, p.divisor, nullptr, st);
+                int rc = reduce_on(ctx, g, rtu, ptrs.data(), w + k0, k1 - k0, len, p.in, p.partial[(size_t)g] + a,
+                                   FA_F32, FA_FEDAVG, p.divisor, nullptr, st);
                 if (rc) return rc;
             }
             FA_HIP(hipEventRecord(r.step_ev, st));
@@ -656,8 +698,8 @@ int reduce_part(fa_ctx* ctx, Part& p, const float* w, hipStream_t s) {
             GpuRes& r = ctx->gpu[(size_t)g];
             DeviceGuard dg(r.dev);
             const void* shard = p.dout[(size_t)g];
-            int rc = reduce_on(ctx, g, ctx->tuning.tu, &shard, &one, 1, p.npad / (size_t)G, FA_F32,
-                               p.dout16[(size_t)g], FA_BF16, FA_FEDAVG, 1.0f, nullptr, r.comm);
+            int rc = reduce_on(ctx, g, rtu, &shard, &one, 1, p.npad / (size_t)G, FA_F32, p.dout16[(size_t)g], FA_BF16,
+                               FA_FEDAVG, 1.0f, nullptr, r.comm);
             if (rc) return rc;
         }
     }
@@ -746,7 +788,7 @@ int submit_impl(fa_ctx* ctx, int part_id, int slot, const Gather& src, float wei
     const size_t si = dsize(p->in), total = src.total();
     if (total != p->n * si)
         return fail(FA_ERR_ARG, "part %d expects %zu bytes per receipt, got %zu", part_id, p->n * si, total);
-    rc = for_each_gpu(ctx->G, [&](int g) -> int {
+    rc = for_each_gpu(ctx->workers.get(), ctx->G, [&](int g) -> int {
         if (!holds(*p, g, slot)) return FA_OK;  // rs: only the slot's GPU receives it
         GpuRes& r = ctx->gpu[(size_t)g];
         DeviceGuard dg(r.dev);
@@ -827,7 +869,7 @@ int copy_output(fa_ctx* ctx, Part& p, const Gather& dst, bool pinned) {
         }
         return FA_OK;
     }
-    return for_each_gpu(G, [&](int g) -> int {
+    return for_each_gpu(ctx->workers.get(), G, [&](int g) -> int {
         GpuRes& r = ctx->gpu[(size_t)g];
         DeviceGuard dg(r.dev);
         const char* src = static_cast<const char*>(p.run_src[(size_t)g]);
@@ -1005,14 +1047,32 @@ int reduce_parts_impl(fa_ctx* ctx, int n_parts, const int* ids, const float* con
                         }
                     });
                     const size_t bytes = sizeof(fa::SegDesc) * (size_t)nseg;
-                    if (r.seg_uploaded != bytes || std::memcmp(r.seg_host, tab.data(), bytes) != 0) {
-                        FA_HIP(hipEventSynchronize(r.seg_ev));  // the previous upload has read the host table
-                        std::memcpy(r.seg_host, tab.data(), bytes);
-                        FA_HIP(hipMemcpyAsync(r.seg_dev, r.seg_host, bytes, hipMemcpyHostToDevice, st));
-                        FA_HIP(hipEventRecord(r.seg_ev, st));
-                        r.seg_uploaded = bytes;
+                    int ti = r.seg_last;
+                    if (ti >= 0 && r.seg[ti].bytes == bytes && std::memcmp(r.seg[ti].host, tab.data(), bytes) == 0) {
+                        // the same table again: its upload (and last launch) may have run on another stream
+                        if (r.seg[ti].stream != st) FA_HIP(hipStreamWaitEvent(st, r.seg[ti].ev, 0));
+                    } else {
+                        ti = (r.seg_last + 1) % kSegRing;
+                        GpuRes::SegTable& t = r.seg[ti];
+                        if (!t.host) {
+                            if (hipHostMalloc((void**)&t.host, sizeof(fa::SegDesc) * kMaxSegments, hipHostMallocDefault) !=
+                                    hipSuccess ||
+                                hipMalloc((void**)&t.dev, sizeof(fa::SegDesc) * kMaxSegments) != hipSuccess ||
+                                hipEventCreateWithFlags(&t.ev, hipEventDisableTiming) != hipSuccess)
+                                return fail(FA_ERR_NOMEM, "segment table allocation failed");
+                        } else {
+                            // the slot's last launch (on any stream) has read the device table, and its upload
+                            // the pinned one, before either is rewritten
+                            FA_HIP(hipEventSynchronize(t.ev));
+                        }
+                        std::memcpy(t.host, tab.data(), bytes);
+                        FA_HIP(hipMemcpyAsync(t.dev, t.host, bytes, hipMemcpyHostToDevice, st));
+                        t.bytes = bytes;
                     }
-                    FA_HIP(fa::launch_segments(r.seg_dev, nseg, blocks, in, out, max_nc, tu, st));
+                    FA_HIP(fa::launch_segments(r.seg[ti].dev, nseg, blocks, in, out, max_nc, tu, st));
+                    FA_HIP(hipEventRecord(r.seg[ti].ev, st));
+                    r.seg[ti].stream = st;
+                    r.seg_last = ti;
                 }
                 for (size_t m = m0; m < m1; ++m)
                     if ((rc = mark_done(ctx, *ps[(size_t)members[m]], g, st))) return rc;
@@ -1173,15 +1233,15 @@ int fa_create_ex(fa_ctx** out, const int* device_ids, int n_gpus, int flags) {
         GpuRes& r = ctx->gpu[(size_t)g];
         r.dev = device_ids[g];
         DeviceGuard dg(r.dev);
+        int prio_lo = 0, prio_hi = 0;
+        if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_hi = 0;
         bool ok = hipStreamCreateWithFlags(&r.compute, hipStreamNonBlocking) == hipSuccess &&
                   hipStreamCreateWithFlags(&r.copy, hipStreamNonBlocking) == hipSuccess &&
-                  hipStreamCreateWithFlags(&r.comm, hipStreamNonBlocking) == hipSuccess &&
+                  // the rs exchange's stream at the highest priority: its RCCL blocks are dispatched ahead of
+                  // the next piece's reduction waiting on the compute stream
+                  hipStreamCreateWithPriority(&r.comm, hipStreamNonBlocking, prio_hi) == hipSuccess &&
                   hipEventCreateWithFlags(&r.copy_ev, hipEventDisableTiming) == hipSuccess &&
-                  hipEventCreateWithFlags(&r.step_ev, hipEventDisableTiming) == hipSuccess &&
-                  hipEventCreateWithFlags(&r.seg_ev, hipEventDisableTiming) == hipSuccess &&
-                  hipHostMalloc((void**)&r.seg_host, sizeof(fa::SegDesc) * kMaxSegments, hipHostMallocDefault) ==
-                      hipSuccess &&
-                  hipMalloc((void**)&r.seg_dev, sizeof(fa::SegDesc) * kMaxSegments) == hipSuccess;
+                  hipEventCreateWithFlags(&r.step_ev, hipEventDisableTiming) == hipSuccess;
         for (int i = 0; ok && i < 2; ++i)
             ok = hipHostMalloc((void**)&r.stage[i], kStageBytes, hipHostMallocDefault) == hipSuccess &&
                  hipEventCreateWithFlags(&r.stage_ev[i], hipEventDisableTiming) == hipSuccess;
@@ -1191,6 +1251,7 @@ int fa_create_ex(fa_ctx** out, const int* device_ids, int n_gpus, int flags) {
         }
         r.pool.reset(new CopyPool(threads));
     }
+    if (n_gpus > 1) ctx->workers.reset(new CopyPool(n_gpus));
     if ((flags & FA_SHARD_CLIENT_RS) && !(flags & FA_TEST_SHARED_DEVICE)) {  // one RCCL communicator per GPU
         std::vector<ncclComm_t> comms((size_t)n_gpus, nullptr);
         const ncclResult_t e = ncclCommInitAll(comms.data(), n_gpus, device_ids);
@@ -1217,15 +1278,19 @@ void fa_destroy(fa_ctx* ctx) {
             if (r.stage[i]) (void)hipHostFree(r.stage[i]);
             if (r.stage_ev[i]) (void)hipEventDestroy(r.stage_ev[i]);
         }
-        if (r.seg_host) (void)hipHostFree(r.seg_host);
-        if (r.seg_dev) (void)hipFree(r.seg_dev);
-        for (hipEvent_t e : {r.copy_ev, r.step_ev, r.seg_ev})
+        for (auto& t : r.seg) {
+            if (t.host) (void)hipHostFree(t.host);
+            if (t.dev) (void)hipFree(t.dev);
+            if (t.ev) (void)hipEventDestroy(t.ev);
+        }
+        for (hipEvent_t e : {r.copy_ev, r.step_ev})
             if (e) (void)hipEventDestroy(e);
         if (r.scratch) (void)hipFree(r.scratch);
         for (hipStream_t s : {r.compute, r.copy, r.comm})
             if (s) (void)hipStreamDestroy(s);
         r.pool.reset();
     }
+    ctx->workers.reset();
     delete ctx;
 }
 
@@ -1556,6 +1621,7 @@ int fa_sync_part(fa_ctx* ctx, int part_id, const float* h_weights, void* hip_str
 int fa_phased_timeouts(int device, uint64_t* count) {
     g_err.clear();
     if (!count) return fail(FA_ERR_ARG, "count is null");
+    if (device < 0) return fail(FA_ERR_ARG, "device %d", device);
     FA_HIP(fa::phased_timeouts(device, count));
     return FA_OK;
 }
@@ -1588,6 +1654,59 @@ extern "C" int fa_diag_read_stream(const void* const* d_bufs, int nc, size_t n, 
 // when the process runs with FA_TIMELINE=1 (tools/timeline.py).
 extern "C" int fa_diag_phased_timeline(int device, unsigned long long* out, int cap) {
     return out && cap > 0 ? fa::phased_timeline(device, out, cap) : -1;
+}
+
+// Diagnostic, not part of the ABI in fa.h: the kernel plan (fa::plan_chain) of one FedAvg chain launch of n
+// elements (16-byte aligned) and nc clients under fa_tuning.walk `walk` (0 = the process default) on a chip of
+// `cus` CUs: *kind 0 one-shot grid, 1 one element per lane, 2 phased persistent grid of *phases phases (more
+// than one: chip-wide meetings).  Pure host arithmetic.
+extern "C" int fa_diag_plan_chain(int in, int out, size_t n, int nc, int walk, int cus, int* kind, long long* phases) {
+    g_err.clear();
+    if (!dvalid(in) || !dvalid(out) || walk < 0 || walk > 6 || cus < 0 || nc < 0)
+        return fail(FA_ERR_ARG, "bad plan arguments");
+    fa::Tuning tu = defaults().tu;
+    if (walk) tu.walk = walk - 1;
+    const fa::ChainPlan pl =
+        fa::plan_chain((fa_dtype)in, (fa_dtype)out, (int64_t)(n / (16 / dsize((fa_dtype)in))), nc, true, tu, cus);
+    if (kind) *kind = pl.kind;
+    if (phases) *phases = pl.phases;
+    return FA_OK;
+}
+
+// Diagnostic, not part of the ABI in fa.h: the plan of every launch one FA_SHARD_CLIENT_RS round enqueues for a
+// FedAvg bucket of n elements over n_clients clients on n_gpus GPUs of `cus` CUs (as reduce_part does: each
+// GPU's piece reductions into its fp32 partial, then, for a bf16 output, the rounding of its shard), under the
+// process-default tuning with `chunks` pieces (0 = the default).  *launches counts them, *phased_launches
+// those that take the phased kernel, *max_phases the most phases of one launch.  Pure host arithmetic.
+extern "C" int fa_diag_rs_plan(size_t n, int n_gpus, int n_clients, int chunks, int in, int out, int cus,
+                               int* launches, int* phased_launches, long long* max_phases) {
+    g_err.clear();
+    if (n_gpus < 1 || n_clients < 1 || chunks < 0 || !dvalid(in) || !dvalid(out) || cus < 0)
+        return fail(FA_ERR_ARG, "bad rs plan arguments");
+    const CtxTuning ct = defaults();
+    const fa::Tuning rtu = rs_launch_tuning(ct.tu);
+    const size_t unit = (size_t)n_gpus * kShardUnit, npad = (n + unit - 1) / unit * unit;
+    const int V = (int)(16 / dsize((fa_dtype)in));
+    int nl = 0, np = 0;
+    long long mp = 0;
+    auto note = [&](const fa::ChainPlan& pl) {
+        ++nl;
+        if (pl.kind == fa::kPlanPhased) ++np;
+        mp = std::max<long long>(mp, pl.phases);
+    };
+    const auto pieces = rs_pieces(npad, n_gpus, chunks ? chunks : ct.rs_chunks);
+    for (int g = 0; g < n_gpus; ++g) {
+        int c0, c1;
+        client_bounds(n_clients, n_gpus, g, &c0, &c1);
+        if (c1 > c0)
+            for (auto& pc : pieces)
+                note(fa::plan_chain((fa_dtype)in, FA_F32, (int64_t)((pc.second - pc.first) / V), c1 - c0, true, rtu, cus));
+        if (out == FA_BF16) note(fa::plan_chain(FA_F32, FA_BF16, (int64_t)(npad / n_gpus / 4), 1, true, rtu, cus));
+    }
+    if (launches) *launches = nl;
+    if (phased_launches) *phased_launches = np;
+    if (max_phases) *max_phases = mp;
+    return FA_OK;
 }
 
 int fa_fill_uniform(void* d_dst, size_t n, fa_dtype dt, uint64_t seed, uint32_t client, uint64_t idx0,

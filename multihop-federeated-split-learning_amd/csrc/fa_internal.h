@@ -57,8 +57,16 @@ hipError_t phased_timeouts(int dev, uint64_t* count);
 // FA_TIMELINE=1 diagnostic: copies the last phased launch's per-workgroup timeline (8 words each) on device
 // dev into out; returns the words copied (0: no timeline, -1: HIP error).
 int phased_timeline(int dev, unsigned long long* out, int cap);
-// Elements per GPU from which the phased walk applies (0: not in use); see fa_kernels.hip.
-int64_t phased_min_elems(fa_dtype in, fa_dtype out, const Tuning& tu);
+// What one FedAvg chain launch runs (plan_chain, host-only): the one-shot vector grid, the one-element-per-
+// lane kernel (mixed 16-byte phases), or the phased persistent grid (`threads` per workgroup, `regs` bytes of
+// register stage per lane, `phases` phases; phases > 1 means chip-wide meetings).
+enum { kPlanOneShot = 0, kPlanScalar = 1, kPlanPhased = 2 };
+struct ChainPlan {
+    int kind, regs, threads;
+    int64_t phases;
+};
+// cus: the device's CU count (0 = no phased kernel).
+ChainPlan plan_chain(fa_dtype in, fa_dtype out, int64_t nvec, int nc, bool vector_ok, const Tuning& tu, int cus);
 hipError_t launch_literal(const void* x, fa_dtype in, void* dst, fa_dtype out, float divisor, int64_t head,
                           int64_t nvec, int64_t n, bool vector_ok, const Tuning& tu, hipStream_t s);
 // In-place state sync: every slot t.src[0..nc) := the chain over them (continuing `init` if given).

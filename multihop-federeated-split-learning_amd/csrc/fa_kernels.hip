@@ -172,6 +172,27 @@ __device__ __forceinline__ void chain_tail(const Tab& t, int k, int r, int64_t e
     }
 }
 
+// Clients [k, k1) of the ordered chain for the V elements starting at element e, continuing acc: groups of
+// U loads in flight before their FMAs, then the grouped tail.
+template <typename IN, int U, bool LNT, class Tab = ClientTable>
+__device__ __forceinline__ void chain_from(const Tab& t, int k, int k1, int64_t e, float* acc) {
+    constexpr int V = In<IN>::kVec;
+    for (; k + U <= k1; k += U) {
+        u32x4 raw[U];  // U loads in flight before the first FMA of the group
+#pragma unroll
+        for (int u = 0; u < U; ++u) raw[u] = ld16<LNT>(reinterpret_cast<const IN*>(t.src[k + u]) + e);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            float x[V];
+            In<IN>::widen(raw[u], x);
+            const float w = t.w[k + u];
+#pragma unroll
+            for (int j = 0; j < V; ++j) acc[j] = __builtin_fmaf(x[j], w, acc[j]);
+        }
+    }
+    chain_tail<IN, U, LNT, V, Tab>(t, k, k1 - k, e, acc);
+}
+
 // The ordered chain for the V elements of every client bucket starting at element e: groups of U
 // loads in flight before their FMAs, then the grouped tail.  acc starts at +0 or at init[e..].
 // Tab: anything with t.src[k] / t.w[k] (the kernarg ClientTable, or a SegView into a batched launch's
@@ -190,21 +211,7 @@ __device__ __forceinline__ void chain_vec(const Tab& t, int nc, const float* ini
 #pragma unroll
         for (int j = 0; j < V; ++j) acc[j] = 0.0f;
     }
-    int k = 0;
-    for (; k + U <= nc; k += U) {
-        u32x4 raw[U];  // U loads in flight before the first FMA of the group
-#pragma unroll
-        for (int u = 0; u < U; ++u) raw[u] = ld16<LNT>(reinterpret_cast<const IN*>(t.src[k + u]) + e);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            float x[V];
-            In<IN>::widen(raw[u], x);
-            const float w = t.w[k + u];
-#pragma unroll
-            for (int j = 0; j < V; ++j) acc[j] = __builtin_fmaf(x[j], w, acc[j]);
-        }
-    }
-    chain_tail<IN, U, LNT, V, Tab>(t, k, nc - k, e, acc);
+    chain_from<IN, U, LNT, Tab>(t, 0, nc, e, acc);
 }
 
 // Vector body over nvec lane-vectors starting at element `head`; lane-vector v
@@ -388,7 +395,7 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
                                                                        void* out, int64_t head, int64_t nvec, int64_t n,
                                                                        unsigned* sync, int slack, int rl_last,
                                                                        int skew, int skew_last, int last_meet,
-                                                                       unsigned long long* tl) {
+                                                                       int cgroup, unsigned long long* tl) {
     constexpr int V = In<IN>::kVec, T = TH, RL = Phased<IN, REGS, TH, OUT>::RL, RR = Phased<IN, REGS, TH, OUT>::RR;
     constexpr int U = TH > 256 ? 8 : 16;  // loads in flight per wave (2 waves per SIMD at 512 threads)
     constexpr bool kPacked = std::is_same<LdsT<OUT>, uint16_t>::value;  // LDS rows hold bf16 output bits
@@ -454,17 +461,31 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
             return i < r_all ? p0 + ((int64_t)i * G + blockIdx.x) * T
                              : p0 + ((int64_t)r_all * G + (int64_t)(i - r_all) * (G / 2) + blockIdx.x / 2) * T;
         };
+        // LDS part.  cgroup > 0 (fp32 rows only): the clients in groups of cgroup, each group over all of this
+        // workgroup's rows before the next, the chain continued from the fp32 row it left in LDS -- so at any
+        // time the chip reads about cgroup client buckets, not all nc.  Same chain per element, same bits.
+        const int ng = !kPacked && cgroup > 0 && nc > cgroup ? (nc + cgroup - 1) / cgroup : 1;
 #pragma unroll 1
-        for (int i = 0; i < rl; ++i) {
-            const int64_t v = row_vec(i);
-            if (v < nvec) {
-                float acc[V];
-                chain_vec<IN, U, true, INIT>(t, nc, init, head + v * V, acc);
-                if constexpr (kPacked) {
-                    pack_bf16<V>(reinterpret_cast<uint16_t*>(&buf[(i * T + threadIdx.x) * V]), acc);
-                } else {
+        for (int gi = 0; gi < ng; ++gi) {
+            const int k0 = ng > 1 ? gi * cgroup : 0, k1 = ng > 1 ? min(nc, k0 + cgroup) : nc;
+#pragma unroll 1
+            for (int i = 0; i < rl; ++i) {
+                const int64_t v = row_vec(i);
+                if (v < nvec) {
+                    float acc[V];
+                    if (gi == 0) {
+                        chain_vec<IN, U, true, INIT>(t, k1, init, head + v * V, acc);
+                    } else {
 #pragma unroll
-                    for (int j = 0; j < V; ++j) buf[(i * T + threadIdx.x) * V + j] = acc[j];
+                        for (int j = 0; j < V; ++j) acc[j] = (float)buf[(i * T + threadIdx.x) * V + j];
+                        chain_from<IN, U, true>(t, k0, k1, head + v * V, acc);
+                    }
+                    if constexpr (kPacked) {
+                        pack_bf16<V>(reinterpret_cast<uint16_t*>(&buf[(i * T + threadIdx.x) * V]), acc);
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < V; ++j) buf[(i * T + threadIdx.x) * V + j] = acc[j];
+                    }
                 }
             }
         }
@@ -813,9 +834,9 @@ PhasedDevice* phased_device() {
         int cus = 0;
         unsigned* p = nullptr;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return;
-        if (hipMalloc((void**)&p, sizeof(unsigned) * kSyncStride * kSyncSlots) != hipSuccess) return;
-        if (hipMemset(p, 0, sizeof(unsigned) * kSyncStride * kSyncSlots) != hipSuccess ||
-            hipDeviceSynchronize() != hipSuccess) {
+        const size_t words = (size_t)kSyncStride * kSyncSlots;
+        if (hipMalloc((void**)&p, sizeof(unsigned) * words) != hipSuccess) return;
+        if (hipMemset(p, 0, sizeof(unsigned) * words) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
             (void)hipFree(p);
             return;
         }
@@ -854,6 +875,16 @@ int phased_skew(int RL) {
     return std::min(v >= 0 ? v : RL >= 40 ? RL / 10 : 0, RL / 2 - 1);  // the bf16 form (20 rows): none
 }
 
+// Clients per group of the phased kernel's LDS part (fedavg_phased_kernel's cgroup; 0 = all at once):
+// FA_PHASED_CGROUP (experiment knob).
+int phased_cgroup() {
+    static const int v = [] {
+        const char* e = std::getenv("FA_PHASED_CGROUP");
+        return e ? std::max(0, std::atoi(e)) : 0;
+    }();
+    return v;
+}
+
 // Enqueue one phased launch on stream s, on the stream's counter slot.
 template <typename Kern>
 hipError_t phased_enqueue(PhasedDevice* d, Kern kern, int th, int RL, int RR, hipStream_t s, const ClientTable& t,
@@ -879,7 +910,8 @@ hipError_t phased_enqueue(PhasedDevice* d, Kern kern, int th, int RL, int RR, hi
     // FA_TIMELINE: a launch without meetings leaves their stamps alone, so clear the previous launch's
     if (d->tl) (void)hipMemsetAsync(d->tl, 0, sizeof(unsigned long long) * 8 * d->cus, s);
     hipLaunchKernelGGL(kern, dim3((unsigned)d->cus), dim3(th), 0, s, t, nc, init, out, head, nvec, n,
-                       d->sync + slot * kSyncStride, slack, rl_last, skew, skew_last, last_meet, d->tl);
+                       d->sync + slot * kSyncStride, slack, rl_last, skew, skew_last, last_meet, phased_cgroup(),
+                       d->tl);
     return hipGetLastError();
 }
 
@@ -894,29 +926,20 @@ bool phased_fits(std::atomic<int>& occ, Kern kern, int th) {
     return o >= 1;
 }
 
-// The phased kernel when it applies (walk 3 = fa_tuning.walk 4, vector path, at least one full phase
-// of work -- or any size when `sized`, see launch_phased --, one workgroup per CU co-resident); otherwise
-// hipErrorNotSupported and the caller takes the one-shot grid.
+// The phased kernel launch of one instantiation (the plan, below, chose it and the bucket's size): one
+// workgroup per CU, all co-resident -- hipErrorNotSupported if not even one fits (the caller then takes the
+// one-shot grid).
 template <typename IN, typename OUT, int REGS, int TH>
-hipError_t launch_phased_r(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
-                           int64_t n, hipStream_t s, bool sized = false) {
-    PhasedDevice* d = phased_device();
-    if (!d) return hipErrorNotSupported;
+hipError_t launch_phased_r(PhasedDevice* d, const ClientTable& t, int nc, const float* init, void* out, int64_t head,
+                           int64_t nvec, int64_t n, hipStream_t s) {
     constexpr int RL = Phased<IN, REGS, TH, OUT>::RL, RR = Phased<IN, REGS, TH, OUT>::RR;
-    const int64_t per_phase = (int64_t)d->cus * TH * (RL + RR);
-    // experiment knob (tools/): FA_PHASED_MIN_VECS lowers the smallest bucket the phased kernel takes
-    static const int64_t min_env = [] {
-        const char* e = std::getenv("FA_PHASED_MIN_VECS");
-        return e ? (int64_t)std::atoll(e) : (int64_t)-1;
-    }();
-    if (!sized && nvec < (min_env >= 0 ? min_env : per_phase)) return hipErrorNotSupported;
     static std::atomic<int> occ[2] = {-1, -1};  // per INIT variant
     auto kern = init ? fedavg_phased_kernel<IN, OUT, true, REGS, false, TH> : fedavg_phased_kernel<IN, OUT, false, REGS, false, TH>;
     if (!phased_fits(occ[init ? 1 : 0], kern, TH)) return hipErrorNotSupported;
     return phased_enqueue(d, kern, TH, RL, RR, s, t, nc, init, out, head, nvec, n);
 }
 
-// Clients from which a bucket smaller than one phase takes a phase sized to it (launch_phased); fewer
+// Clients from which a bucket smaller than one phase takes a phase sized to it (plan_chain); fewer
 // clients make the output a larger share of the traffic, and its write burst after the meeting costs
 // more than the one-shot grid's interleaving (C2, D = 8: 0.085 vs 0.075 ms).
 int sized_min_clients() {
@@ -927,70 +950,55 @@ int sized_min_clients() {
     return v;
 }
 
-// One phase sized to a bucket below one full phase: q = vectors per lane; the register stage takes the
-// largest RR <= q from the instantiated set and LDS the rest (q - RR <= RL), so every lane holds q or
-// q - 1 vectors.  E.g. the strong-scaled north star at 4 ranks (16.8 M f32 elements per rank): q = 64 ->
-// 48 in registers + 16 in LDS, where the full-phase layout gave half the waves 88 and half 40.
-template <typename IN, typename OUT, int TH>
-hipError_t launch_phased_sized(const ClientTable& t, int nc, const float* init, void* out, int64_t head,
-                               int64_t nvec, int64_t n, hipStream_t s) {
-    PhasedDevice* d = phased_device();
-    if (!d || nc < sized_min_clients()) return hipErrorNotSupported;
-    const int64_t lanes = (int64_t)d->cus * TH;
-    const int64_t q = (nvec + lanes - 1) / lanes;
-    if constexpr (std::is_same<IN, float>::value) {  // V = 4: RR = REGS / 4
-        if (q >= 48) return launch_phased_r<IN, OUT, 192, TH>(t, nc, init, out, head, nvec, n, s, true);
-        if (q >= 32) return launch_phased_r<IN, OUT, 128, TH>(t, nc, init, out, head, nvec, n, s, true);
-        if (q >= 24) return launch_phased_r<IN, OUT, 96, TH>(t, nc, init, out, head, nvec, n, s, true);
-        if (q >= 16) return launch_phased_r<IN, OUT, 64, TH>(t, nc, init, out, head, nvec, n, s, true);
-        if (q >= 8) return launch_phased_r<IN, OUT, 32, TH>(t, nc, init, out, head, nvec, n, s, true);
-    } else {  // V = 8: RR = REGS / 8
-        if (q >= 12) return launch_phased_r<IN, OUT, 96, TH>(t, nc, init, out, head, nvec, n, s, true);
-        if (q >= 8) return launch_phased_r<IN, OUT, 64, TH>(t, nc, init, out, head, nvec, n, s, true);
-        if (q >= 4) return launch_phased_r<IN, OUT, 32, TH>(t, nc, init, out, head, nvec, n, s, true);
-    }
-    return hipErrorNotSupported;
+// experiment knob (tools/): FA_PHASED_MIN_VECS lowers the smallest bucket that takes a full phase
+int64_t phased_min_vecs_env() {
+    static const int64_t v = [] {
+        const char* e = std::getenv("FA_PHASED_MIN_VECS");
+        return e ? (int64_t)std::atoll(e) : (int64_t)-1;
+    }();
+    return v;
 }
 
-// Smallest bucket (elements of dtype `in` per GPU) that the phased walk of `tu` takes on the current
-// device, or 0 when the phased kernel is not in use.
-int64_t phased_min_elems_impl(fa_dtype in, fa_dtype out, const Tuning& tu) {
-    if (tu.walk < 3 || tu.walk > 5) return 0;
-    PhasedDevice* d = phased_device();
-    if (!d) return 0;
-    const bool big = tu.walk == 5 || (tu.walk == 4 && in == FA_BF16);  // the 512-thread form
-    const int regs = big ? 96 : tu.walk == 4 ? 192 : 128, th = big ? 512 : kPhasedThreads;
-    const int V = in == FA_F32 ? 4 : 8;
-    const int rl = 160 * 1024 / (th * V * (out == FA_BF16 ? 2 : 4)), rr = regs / V;  // Phased<>::RL
-    return (int64_t)d->cus * th * (rl + rr) * V;
-}
+template <typename T> constexpr fa_dtype dtype_of() { return std::is_same<T, float>::value ? FA_F32 : FA_BF16; }
 
+// The instantiations a plan may name (threads, register-stage bytes per lane): 256-thread f32 forms with
+// the register stages of the sized phases (192, 128, 32), the 512-thread form of walk 6 and of bf16 inputs
+// (96, and 64 / 32 for sized bf16 phases), and walk 4's 128-register form.
 template <typename IN, typename OUT>
-hipError_t launch_phased(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
-                         int64_t n, const Tuning& tu, hipStream_t s) {
-    if (tu.walk == 3) return launch_phased_r<IN, OUT, 128, 256>(t, nc, init, out, head, nvec, n, s);
-    if (tu.walk == 4) {  // the default: bf16 inputs take the 512-thread form (2 waves per SIMD hide the
-                         // widening VALU work of 8 elements per load: C3 0.430 vs 0.439 ms), f32 the
-                         // 256-thread one (C4 5.43 vs 5.49 ms, C5's share 2.55 vs 2.56), gpurun_out r01s25
-        constexpr bool bf = std::is_same<IN, uint16_t>::value;
-        constexpr int TH = bf ? 512 : 256;
-        const hipError_t e = bf ? launch_phased_r<IN, OUT, 96, 512>(t, nc, init, out, head, nvec, n, s)
-                                : launch_phased_r<IN, OUT, 192, 256>(t, nc, init, out, head, nvec, n, s);
-        if (e != hipErrorNotSupported) return e;
-        return launch_phased_sized<IN, OUT, TH>(t, nc, init, out, head, nvec, n, s);
+hipError_t launch_phased_plan(PhasedDevice* d, const ChainPlan& pl, const ClientTable& t, int nc, const float* init,
+                              void* out, int64_t head, int64_t nvec, int64_t n, hipStream_t s) {
+    constexpr bool bf = std::is_same<IN, uint16_t>::value;
+    switch (pl.threads * 1000 + pl.regs) {
+        case 256128: return launch_phased_r<IN, OUT, 128, 256>(d, t, nc, init, out, head, nvec, n, s);
+        case 512096: return launch_phased_r<IN, OUT, 96, 512>(d, t, nc, init, out, head, nvec, n, s);
+        default: break;
     }
-    if (tu.walk == 5) return launch_phased_r<IN, OUT, 96, 512>(t, nc, init, out, head, nvec, n, s);
+    if constexpr (!bf) {
+        switch (pl.threads * 1000 + pl.regs) {
+            case 256192: return launch_phased_r<IN, OUT, 192, 256>(d, t, nc, init, out, head, nvec, n, s);
+            case 256032: return launch_phased_r<IN, OUT, 32, 256>(d, t, nc, init, out, head, nvec, n, s);
+            default: break;
+        }
+    } else {
+        switch (pl.threads * 1000 + pl.regs) {
+            case 512064: return launch_phased_r<IN, OUT, 64, 512>(d, t, nc, init, out, head, nvec, n, s);
+            case 512032: return launch_phased_r<IN, OUT, 32, 512>(d, t, nc, init, out, head, nvec, n, s);
+            default: break;
+        }
+    }
     return hipErrorNotSupported;
 }
 
 template <typename IN, typename OUT>
 hipError_t launch_chain_t(const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
                           int64_t n, bool vector_ok, const Tuning& tu, hipStream_t s) {
-    if (vector_ok) {
-        const hipError_t e = launch_phased<IN, OUT>(t, nc, init, out, head, nvec, n, tu, s);
+    PhasedDevice* d = vector_ok && tu.walk >= 3 && tu.walk <= 5 ? phased_device() : nullptr;
+    const ChainPlan pl = plan_chain(dtype_of<IN>(), dtype_of<OUT>(), nvec, nc, vector_ok, tu, d ? d->cus : 0);
+    if (pl.kind == kPlanPhased) {
+        const hipError_t e = launch_phased_plan<IN, OUT>(d, pl, t, nc, init, out, head, nvec, n, s);
         if (e != hipErrorNotSupported) return e;
     }
-    if (!vector_ok) {
+    if (pl.kind == kPlanScalar) {
         const int64_t g = grid_scalar(n, tu);
         if (init)
             hipLaunchKernelGGL((fedavg_chain_scalar_kernel<IN, OUT, true>), dim3((unsigned)g), dim3(tu.block), 0, s,
@@ -1006,13 +1014,63 @@ hipError_t launch_chain_t(const ClientTable& t, int nc, const float* init, void*
 
 }  // namespace
 
-int64_t phased_min_elems(fa_dtype in, fa_dtype out, const Tuning& tu) { return phased_min_elems_impl(in, out, tu); }
+// ---------------------------------------------------------------- launch planning
+//
+// Which kernel one FedAvg chain launch takes, decided on the host from the bucket's shape, the tuning and
+// the device's CU count alone (no device call), so that fa_diag_plan_chain can show the selection to the
+// CPU suite.  The phased kernel takes buckets of at least one full phase (walks 4-6), and with walk 5 (the
+// default) also buckets below one phase with >= sized_min_clients() clients, in one phase sized to them,
+// q vectors per lane spread evenly (phased_rl_last): up to RL of them go to LDS alone and the register stage
+// stays empty, so the smallest instantiation serves every q <= RL; above RL the register stage takes the
+// largest RR <= q of the instantiated set and LDS the rest (q - RR <= RL).  E.g. the strong-scaled north
+// star at 4 ranks (16.8 M f32 elements per rank): q = 64 -> 48 in registers + 16 in LDS, where the
+// full-phase layout gave half the waves 88 and half 40; at 8 ranks q = 32 -> all 32 in LDS.
+ChainPlan plan_chain(fa_dtype in, fa_dtype out, int64_t nvec, int nc, bool vector_ok, const Tuning& tu, int cus) {
+    ChainPlan p{vector_ok ? kPlanOneShot : kPlanScalar, 0, 0, 0};
+    if (!vector_ok || cus <= 0 || tu.walk < 3 || tu.walk > 5) return p;
+    const bool bf = in == FA_BF16;
+    const int V = bf ? 8 : 4;
+    // walk 4 (fa_tuning.walk 5, the default): bf16 inputs take the 512-thread form (2 waves per SIMD hide
+    // the widening VALU work of 8 elements per load: C3 0.430 vs 0.439 ms), f32 the 256-thread one (C4 5.43
+    // vs 5.49 ms, C5's share 2.55 vs 2.56), gpurun_out r01s25
+    const int th = tu.walk == 3 ? 256 : (tu.walk == 5 || bf) ? 512 : 256;
+    int regs = tu.walk == 3 ? 128 : (tu.walk == 5 || bf) ? 96 : 192;
+    const int rl = 160 * 1024 / (th * V * (out == FA_BF16 ? 2 : 4));  // Phased<>::RL
+    const int64_t lanes = (int64_t)cus * th;
+    const int64_t env = phased_min_vecs_env();
+    if (nvec < (env >= 0 ? env : lanes * (rl + regs / V))) {  // below one full phase
+        if (tu.walk != 4 || nc < sized_min_clients()) return p;
+        const int64_t q = (nvec + lanes - 1) / lanes;
+        if (q < (bf ? 4 : 8)) return p;  // too few vectors per lane: the one-shot grid
+        // register stages (bytes per lane) instantiated for the sized phase, largest first
+        static const int kF32[] = {192, 128, 32}, kBf16[] = {96, 64, 32};
+        const int* tiers = bf ? kBf16 : kF32;
+        regs = tiers[2];  // q <= RL: LDS only, the register stage unused
+        if (q > rl)
+            for (int i = 0; i < 3; ++i)
+                if (q >= tiers[i] / V) {
+                    regs = tiers[i];
+                    break;
+                }
+    }
+    const int skew = cus >= 256 && cus % 16 == 0 ? phased_skew(rl) : 0;  // as phased_enqueue
+    const int64_t per_phase = lanes * (rl + regs / V) - (int64_t)(cus / 2) * th * skew;
+    return ChainPlan{kPlanPhased, regs, th, (nvec + per_phase - 1) / per_phase};
+}
 
 hipError_t phased_timeouts(int dev, uint64_t* count) {
     *count = 0;
     if (dev < 0 || dev >= kMaxDevices || !g_phased[dev].sync) return hipSuccess;  // no phased launch yet
+    // on that device (the caller's current one may differ), after the launches still in flight there: they
+    // run on non-blocking streams, which a plain hipMemcpy would not wait for
+    int prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    hipError_t e = hipSetDevice(dev);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
     std::vector<unsigned> tab((size_t)kSyncStride * kSyncSlots);
-    const hipError_t e = hipMemcpy(tab.data(), g_phased[dev].sync, tab.size() * sizeof(unsigned), hipMemcpyDeviceToHost);
+    if (e == hipSuccess)
+        e = hipMemcpy(tab.data(), g_phased[dev].sync, tab.size() * sizeof(unsigned), hipMemcpyDeviceToHost);
+    if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
     if (e != hipSuccess) return e;
     for (int slot = 0; slot < kSyncSlots; ++slot) *count += tab[(size_t)slot * kSyncStride + 2];
     return hipSuccess;
@@ -1183,13 +1241,8 @@ hipError_t launch_segments(const SegDesc* d_segs, int nseg, int64_t blocks, fa_d
 
 bool phased_takes(fa_dtype in, fa_dtype out, int64_t nvec, int nc, const Tuning& tu) {
     if (tu.walk < 3 || tu.walk > 5) return false;
-    const int64_t full = phased_min_elems_impl(in, out, tu) / (in == FA_F32 ? 4 : 8);
-    if (full <= 0) return false;
-    if (nvec >= full) return true;
-    if (tu.walk != 4 || nc < sized_min_clients()) return false;
     PhasedDevice* d = phased_device();
-    const int64_t lanes = (int64_t)d->cus * (in == FA_F32 ? 256 : 512);
-    return (nvec + lanes - 1) / lanes >= (in == FA_F32 ? 8 : 4);
+    return d && plan_chain(in, out, nvec, nc, true, tu, d->cus).kind == kPlanPhased;
 }
 
 // Read-stream probe (SURVEY.md 8d "also report a measured read-STREAM peak").  From one phase up it is the
@@ -1216,9 +1269,12 @@ __global__ __launch_bounds__(256) void read_probe_kernel(const ClientTable t, in
 
 hipError_t launch_read_probe(const ClientTable& t, int nc, int64_t nvec, float* sink, hipStream_t s) {
     // from one phase up: the phased kernel itself with no output (its reads, LDS and meetings, no writes)
-    const hipError_t e = launch_phased_r<float, float, 192, 256>(t, nc, nullptr, nullptr, 0, nvec, nvec * 4, s);
-    if (e != hipErrorNotSupported) return e;
     PhasedDevice* d = phased_device();
+    Tuning tu{256, 0, 16, 1, 2, 4};  // walk 5's f32 form, full phases only (no sized phase: nc = 0)
+    if (d && plan_chain(FA_F32, FA_F32, nvec, 0, true, tu, d->cus).kind == kPlanPhased) {
+        const hipError_t e = launch_phased_r<float, float, 192, 256>(d, t, nc, nullptr, nullptr, 0, nvec, nvec * 4, s);
+        if (e != hipErrorNotSupported) return e;
+    }
     const int g = (d ? d->cus : 256) * 8;
     hipLaunchKernelGGL(read_probe_kernel, dim3((unsigned)g), dim3(256), 0, s, t, nc, nvec, sink);
     return hipGetLastError();

@@ -178,8 +178,10 @@ public:
     }
     ~Aggregator() { fa_destroy(ctx_); }
 
-    // Consumes one receipt of bucket `mp` into its client slot.
-    void absorb(const Receipt& r) {
+    // Consumes one receipt of bucket `mp` into its client slot.  Returns whether it is the first receipt of
+    // this (owner, bucket) in the round: a retransmission replaces the slot's contents (the last one wins,
+    // as a second torch::load would) but is not another receipt -- the phase waits for D distinct owners.
+    bool absorb(const Receipt& r) {
         const auto t0 = std::chrono::steady_clock::now();
         TorchArchive ar;
         std::string err;
@@ -224,9 +226,11 @@ public:
             FA_CHECK(fa_submit(ctx_, r.model_part, slot, flat.data(), weight_of(r.client_id)));
         }
         b.bytes_in += r.blob_len;
-        b.arrived.insert(r.client_id);
+        const bool first = b.arrived.insert(r.client_id).second;
         b.last = r;  // template of the reply: the last receipt (its buffers travel back, as in the reference)
         st_.absorb_s += secs_since(t0);
+        if (!first) std::cerr << "[aggregator] part " << r.model_part << ": owner " << r.client_id << " sent it again\n";
+        return first;
     }
 
     // Reduces bucket mp and returns the framed reply, built once and shared by every destination:
@@ -427,17 +431,24 @@ int main(int argc, char** argv) {
 
     for (int round = 0; o.rounds < 0 || round < o.rounds; ++round) {
         // phase 1: model part 1 from every data owner (aggregator.cpp:59-93)
+        // Receipt accounting (the reference counts raw receipts, aggregator.cpp:59-92 / :112-149): a phase
+        // ends when every data owner's receipt of every bucket of the phase is in, counted as distinct
+        // (owner, bucket) pairs, so a retransmitted receipt replaces its slot instead of ending the phase
+        // early with another owner missing.  A receipt of the other phase is always a retransmission of an
+        // earlier one: a data owner sends its last-part layers only after it has received the phase-1 reply
+        // (data_owner.cpp:228-245), which goes out after phase 1 ends, and its next part 1 only after every
+        // phase-2 reply, which goes out after phase 2 ends.  So it is ignored (named in the log), never carried
+        // into a later phase, where it would stand for a receipt its owner has not sent yet.
         auto t0 = std::chrono::steady_clock::now();
-        std::vector<Receipt> early;  // phase-2 receipts that overtook phase 1 (not in the reference's FIFO)
         int received = 0;
         while (received < o.data_owners) {
             Receipt r = wait_receipt(net, o, agg, {1}, round, 1);
             if (r.model_part != 1) {
-                early.push_back(std::move(r));
+                std::cerr << "[aggregator] part " << r.model_part << " from owner " << r.client_id
+                          << " during phase 1 (a retransmission of the last round's): ignored\n";
                 continue;
             }
-            agg.absorb(r);
-            ++received;
+            if (agg.absorb(r)) ++received;
         }
         const double recv1 = secs_since(t0);
         const size_t in1 = agg.bytes_in(1);
@@ -451,20 +462,19 @@ int main(int argc, char** argv) {
         auto t2 = std::chrono::steady_clock::now();
         int got = 0;
         const int want = o.data_owners * L;
-        for (auto& r : early) {
-            agg.absorb(r);
-            ++got;
-        }
         std::vector<int> mps;
         for (int mp = 2; mp <= L + 1; ++mp) mps.push_back(mp);
         while (got < want) {
             Receipt r = wait_receipt(net, o, agg, mps, round, 2);
+            if (r.model_part == 1) {  // a retransmission of this round's part 1 (above), already reduced
+                std::cerr << "[aggregator] part 1 from owner " << r.client_id << " during phase 2: ignored\n";
+                continue;
+            }
             if (r.model_part < 2 || r.model_part > L + 1) {
                 std::cerr << "[aggregator] unexpected model_part " << r.model_part << " in phase 2\n";
                 continue;
             }
-            agg.absorb(r);
-            ++got;
+            if (agg.absorb(r)) ++got;
         }
         const double recv2 = secs_since(t2);
         size_t in2 = 0;

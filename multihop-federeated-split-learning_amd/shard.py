@@ -20,10 +20,18 @@ are partitioned instead:
 
 The local reduction is a callable so the exchange logic runs unchanged on CPU
 tensors under gloo in tests; on the GPU it is ``fa_reducer`` (libfa.so).
+
+Overlap: in ``rs`` and ``chain`` the local reductions run while RCCL's kernels
+move the previous chunk.  RCCL's blocks need CUs and LDS that the phased
+persistent grid (the default walk for large buckets) holds on every CU for its
+whole launch, so run these layouts with the one-shot walk:
+``fa.set_tuning(walk=OVERLAP_WALK)`` (bench.py does; the in-process
+FA_SHARD_CLIENT_RS layout of libfa.so does the same by itself).
 """
 import numpy as np
 
 UNIT = 64  # shard boundaries in elements (keeps every shard's 16-byte phase)
+OVERLAP_WALK = 2  # fa_tuning.walk of reductions that run beside a collective: the one-shot XCD walk
 
 
 def range_bounds(n, world, rank, unit=UNIT):

@@ -156,6 +156,33 @@ def test_missing_owner_is_reported_and_times_out(torch_gpu, drop_phase):
             agg.kill()
 
 
+@pytest.mark.parametrize("extra", [[], ["--eager"]])
+def test_retransmitted_receipts_count_once(torch_gpu, extra):
+    """One data owner sends every receipt twice.  The reference counts raw receipts (aggregator.cpp:59-92,
+    :112-149), so its phase would end one owner short; fa_aggregator counts distinct (owner, bucket) pairs:
+    the duplicate replaces the slot, the round waits for every owner and every reply is bit-exact."""
+    D, rounds, base = 4, 2, pick_base()
+    agg = subprocess.Popen([AGG, "-i", "-1", "-d", str(D), "-c", "1", "--rounds", str(rounds), "--port-base",
+                            str(base), "--stall-report", "5", "--receipt-timeout", "30"] + extra,
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        time.sleep(0.5)
+        r = subprocess.run([OWNERS, "--blobs", os.path.join(GOLDEN, "lenet5_c1"), "--parts", "1,2,3", "-d", str(D),
+                            "-c", "1", "--rounds", str(rounds), "--port-base", str(base), "--model-name", "2",
+                            "--start", "6", "--end", "1", "--retransmit", "2", "--reply-timeout", "60"],
+                           capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res = json.loads(r.stdout.strip().splitlines()[-1])
+        assert res["ok"] and res["rounds"] == rounds
+        out, err = agg.communicate(timeout=60)
+        assert agg.returncode == 0, err[-2000:]
+        assert sum(l.startswith("{") for l in out.splitlines()) == rounds
+        assert "sent it again" in err or "ignored" in err  # the duplicates were seen, and not counted
+    finally:
+        if agg.poll() is None:
+            agg.kill()
+
+
 @pytest.mark.parametrize("extra", [[], ["--eager"], ["--mode", "literal"], ["--layout", "rs", "--rs-chunks", "3"]])
 def test_bf16_parts_over_tcp(torch_gpu, tmp_path, extra):
     """BASELINE config C3's dtype through the drop-in process: owners send bf16 model parts

@@ -8,7 +8,7 @@
 //
 //   fa_fake_owners --blobs DIR --parts 1,2,3 -d D -c C [--rounds R] [--mode fedavg|literal]
 //                  [--port-base P] [--model-name N --model-type T --start S --end E] [--seed X]
-//                  [--drop-owner K [--drop-phase P]] [--reply-timeout S]
+//                  [--drop-owner K [--drop-phase P]] [--retransmit K] [--reply-timeout S]
 //                  [--sequential]   (owners send at once, one connection each, unless --sequential
 //                                    or --mode literal, whose result depends on the arrival order)
 // Prints one JSON line: {"ok": bool, "rounds": R, "checked_elems": ..., "round_ms": [...]}.
@@ -68,6 +68,7 @@ int main(int argc, char** argv) {
     float divisor = 1000.0f;
     bool concurrent = true;
     int drop_owner = -1, drop_phase = 1;  // failure injection: owner K never sends its phase-P receipts
+    int retransmit = -1;                  // owner K sends every receipt twice (a retransmission)
     long reply_timeout_ms = 600000;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
@@ -88,6 +89,7 @@ int main(int argc, char** argv) {
         else if (a == "--sequential") concurrent = false;
         else if (a == "--drop-owner") drop_owner = std::atoi(v), ++i;
         else if (a == "--drop-phase") drop_phase = std::atoi(v), ++i;
+        else if (a == "--retransmit") retransmit = std::atoi(v), ++i;
         else if (a == "--reply-timeout") reply_timeout_ms = (long)(std::atof(v) * 1000), ++i;
         else {
             std::cerr << "unknown argument " << a << "\n";
@@ -221,7 +223,8 @@ int main(int argc, char** argv) {
                     if ((phase == 1) != (p.mp == 1)) continue;
                     if (k == drop_owner && phase == drop_phase) continue;  // this owner "died"
                     by_owner[k].push_back(frames[p.mp][k]);
-                    ++sent;
+                    if (k == retransmit) by_owner[k].push_back(frames[p.mp][k]);  // the same receipt again
+                    ++sent;  // one reply per bucket and destination, retransmission or not
                 }
             if (concurrent) {  // every owner is its own process in the reference: they send at once
                 std::vector<std::thread> th;
