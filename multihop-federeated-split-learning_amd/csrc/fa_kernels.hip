@@ -395,7 +395,7 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
                                                                        void* out, int64_t head, int64_t nvec, int64_t n,
                                                                        unsigned* sync, int slack, int rl_last,
                                                                        int skew, int skew_last, int last_meet,
-                                                                       int cgroup, unsigned long long* tl) {
+                                                                       unsigned long long* tl) {
     constexpr int V = In<IN>::kVec, T = TH, RL = Phased<IN, REGS, TH, OUT>::RL, RR = Phased<IN, REGS, TH, OUT>::RR;
     constexpr int U = TH > 256 ? 8 : 16;  // loads in flight per wave (2 waves per SIMD at 512 threads)
     constexpr bool kPacked = std::is_same<LdsT<OUT>, uint16_t>::value;  // LDS rows hold bf16 output bits
@@ -461,31 +461,17 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
             return i < r_all ? p0 + ((int64_t)i * G + blockIdx.x) * T
                              : p0 + ((int64_t)r_all * G + (int64_t)(i - r_all) * (G / 2) + blockIdx.x / 2) * T;
         };
-        // LDS part.  cgroup > 0 (fp32 rows only): the clients in groups of cgroup, each group over all of this
-        // workgroup's rows before the next, the chain continued from the fp32 row it left in LDS -- so at any
-        // time the chip reads about cgroup client buckets, not all nc.  Same chain per element, same bits.
-        const int ng = !kPacked && cgroup > 0 && nc > cgroup ? (nc + cgroup - 1) / cgroup : 1;
 #pragma unroll 1
-        for (int gi = 0; gi < ng; ++gi) {
-            const int k0 = ng > 1 ? gi * cgroup : 0, k1 = ng > 1 ? min(nc, k0 + cgroup) : nc;
-#pragma unroll 1
-            for (int i = 0; i < rl; ++i) {
-                const int64_t v = row_vec(i);
-                if (v < nvec) {
-                    float acc[V];
-                    if (gi == 0) {
-                        chain_vec<IN, U, true, INIT>(t, k1, init, head + v * V, acc);
-                    } else {
+        for (int i = 0; i < rl; ++i) {
+            const int64_t v = row_vec(i);
+            if (v < nvec) {
+                float acc[V];
+                chain_vec<IN, U, true, INIT>(t, nc, init, head + v * V, acc);
+                if constexpr (kPacked) {
+                    pack_bf16<V>(reinterpret_cast<uint16_t*>(&buf[(i * T + threadIdx.x) * V]), acc);
+                } else {
 #pragma unroll
-                        for (int j = 0; j < V; ++j) acc[j] = (float)buf[(i * T + threadIdx.x) * V + j];
-                        chain_from<IN, U, true>(t, k0, k1, head + v * V, acc);
-                    }
-                    if constexpr (kPacked) {
-                        pack_bf16<V>(reinterpret_cast<uint16_t*>(&buf[(i * T + threadIdx.x) * V]), acc);
-                    } else {
-#pragma unroll
-                        for (int j = 0; j < V; ++j) buf[(i * T + threadIdx.x) * V + j] = acc[j];
-                    }
+                    for (int j = 0; j < V; ++j) buf[(i * T + threadIdx.x) * V + j] = acc[j];
                 }
             }
         }
@@ -875,16 +861,6 @@ int phased_skew(int RL) {
     return std::min(v >= 0 ? v : RL >= 40 ? RL / 10 : 0, RL / 2 - 1);  // the bf16 form (20 rows): none
 }
 
-// Clients per group of the phased kernel's LDS part (fedavg_phased_kernel's cgroup; 0 = all at once):
-// FA_PHASED_CGROUP (experiment knob).
-int phased_cgroup() {
-    static const int v = [] {
-        const char* e = std::getenv("FA_PHASED_CGROUP");
-        return e ? std::max(0, std::atoi(e)) : 0;
-    }();
-    return v;
-}
-
 // Enqueue one phased launch on stream s, on the stream's counter slot.
 template <typename Kern>
 hipError_t phased_enqueue(PhasedDevice* d, Kern kern, int th, int RL, int RR, hipStream_t s, const ClientTable& t,
@@ -910,8 +886,7 @@ hipError_t phased_enqueue(PhasedDevice* d, Kern kern, int th, int RL, int RR, hi
     // FA_TIMELINE: a launch without meetings leaves their stamps alone, so clear the previous launch's
     if (d->tl) (void)hipMemsetAsync(d->tl, 0, sizeof(unsigned long long) * 8 * d->cus, s);
     hipLaunchKernelGGL(kern, dim3((unsigned)d->cus), dim3(th), 0, s, t, nc, init, out, head, nvec, n,
-                       d->sync + slot * kSyncStride, slack, rl_last, skew, skew_last, last_meet, phased_cgroup(),
-                       d->tl);
+                       d->sync + slot * kSyncStride, slack, rl_last, skew, skew_last, last_meet, d->tl);
     return hipGetLastError();
 }
 

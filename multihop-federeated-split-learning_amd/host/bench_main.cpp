@@ -1,7 +1,8 @@
 // bench_main.cpp -- fa_bench: the device-resident round timed from C++ through the C ABI alone (no
 // Python, no torch), as the reference's aggregator process would drive it (aggregator.cpp:55-167 on
 // libfa): fa_create -> fa_bucket_define -> the client slots filled in place (fa_fill_uniform on
-// fa_bucket_slot) -> fa_reduce_part per round.  One GPU: HIP events on the launch stream; several
+// fa_bucket_slot) -> fa_reduce_part per round.  One GPU, range layout: HIP events on the launch stream;
+// the rs layout (its exchange and bf16 rounding run on the context's own exchange stream) and several GPUs
 // (FA_SHARD_RANGE or FA_SHARD_CLIENT_RS over the first G devices): host wall clock around the rounds,
 // fa_sync at both ends.  Prints one JSON line with bench.py's metric (GiB/s of client input).
 //
@@ -80,7 +81,7 @@ int main(int argc, char** argv) {
     fa_ctx* ctx = nullptr;
     check(fa_create(&ctx, gpus, flags), "fa_create");
     const int part = 1, D = wl->clients;
-    const fa_dtype out = rs ? FA_F32 : wl->out;  // the rs layout sums fp32 partials into an fp32 result
+    const fa_dtype out = wl->out;  // the rs layout sums fp32 partials, rounded once for a bf16 output
     const size_t n = wl->elems, s_in = wl->in == FA_F32 ? 4 : 2, s_out = out == FA_F32 ? 4 : 2;
     check(fa_bucket_define(ctx, part, n, wl->in, out, D, FA_FEDAVG), "fa_bucket_define");
     // synthetic client buckets generated in HBM (bench.py's inputs: seed 0x5EED, client k, global index)
@@ -100,7 +101,7 @@ int main(int argc, char** argv) {
     hip_check(hipSetDevice(0), "hipSetDevice");
     std::vector<float> w((size_t)D, 1.0f / (float)D);
     double ms = 0;
-    if (gpus == 1) {
+    if (gpus == 1 && !rs) {
         hipStream_t s;
         hip_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
         hipEvent_t a, b;

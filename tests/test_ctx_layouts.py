@@ -276,3 +276,40 @@ def test_reduce_parts_device_table_and_reuse(fa, O, torch_gpu):
         agg.reduce_parts([20, 21, 22], weights=[ws[20], ws[21], ws[22]])
         for pid in (20, 21, 22):
             assert_bits(agg.copy_output(pid), O.fedavg(xs[pid], ws[pid]))
+
+
+def test_reduce_parts_device_tables_across_streams(fa, O, torch_gpu):
+    """Device segment tables (batches of more than 8 buckets) used from two streams without a sync between:
+    an explicit stream kept busy, then the context's compute stream.  Each batch's table
+    lives in its own slot of the per-GPU ring until its launch is done, a reused table orders itself after
+    the upload on the other stream, and every bucket ends bit-exact."""
+    torch = torch_gpu
+    D = 6
+    P = {pid: n for pid, n in zip(range(1, 11), [3, 64, 65, 1000, 4099, 77_777, 5, 30_001, 12, 130])}
+    Q = {pid: n for pid, n in zip(range(21, 31), [7, 63, 129, 999, 4097, 50_000, 9, 20_001, 16, 131])}
+    A = torch.cuda.Stream()
+    busy = torch.empty(1 << 27, dtype=torch.float32, device="cuda")
+    with fa.Aggregator(1) as agg:
+        xs = {}
+        for pid, n in {**P, **Q}.items():
+            agg.define(pid, n, fa.F32, fa.F32, D, fa.FEDAVG)
+            xs[pid] = host_clients(O, 400 + pid, D, n)
+            for k in range(D):
+                ptr, cnt, _ = agg.slot(pid, 0, k)
+                fa.fill_uniform(ptr, cnt, fa.F32, 400 + pid, k)
+        torch.cuda.synchronize()
+        for rep in range(3):
+            wP, wQ = O.weights(D, seed=10 + rep), O.weights(D, seed=50 + rep)
+            fa.fill_uniform(busy, busy.numel(), fa.F32, 1, rep, stream=A)  # stream A starts late
+            agg.reduce_parts(list(P), weights=[wP] * len(P), stream=A)
+            agg.reduce_parts(list(Q), weights=[wQ] * len(Q))  # a new table on the compute stream
+            if rep == 2:  # the same table again, now on the compute stream: after its upload on A
+                fa.fill_uniform(busy, busy.numel(), fa.F32, 2, rep, stream=A)
+                agg.reduce_parts(list(P), weights=[wP] * len(P), stream=A)
+                agg.reduce_parts(list(P), weights=[wP] * len(P))
+            torch.cuda.synchronize()
+            agg.sync()
+            for pid in P:
+                assert_bits(agg.copy_output(pid), O.fedavg(xs[pid], wP))
+            for pid in Q:
+                assert_bits(agg.copy_output(pid), O.fedavg(xs[pid], wQ))

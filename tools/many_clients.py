@@ -41,6 +41,9 @@ def main():
     import bench
     fa = bench.load_pkg()
     fa.lib()
+    tune = os.environ.get("MC_TUNE", "")  # e.g. "slot_skew=4608": process tuning defaults before any context
+    if tune:
+        fa.set_tuning(**{k: int(v) for k, v in (kv.split("=") for kv in tune.split(","))})
     stream = torch.cuda.Stream()
     for name in names:
         D, n = CONFIGS[name]
@@ -73,7 +76,7 @@ def main():
             ms = statistics.median([a.elapsed_time(b) for a, b in evs[3:]])
             algo = (D + 1) * n * 4
             moved = D * n * 4 if G < 0 else algo + (2 * n * 4 * (-(-D // G) - 1) if G else 0)
-            print(json.dumps({"config": name, "clients": D, "elems": n, "group": G, "median_ms": round(ms, 4),
+            print(json.dumps({"tune": os.environ.get("MC_TUNE", ""), "config": name, "clients": D, "elems": n, "group": G, "median_ms": round(ms, 4),
                               "algo_frac": round(algo / (ms * 1e-3) / 8e12, 4),
                               "moved_TBs": round(moved / (ms * 1e-3) / 1e12, 3),
                               "timeouts": fa.phased_timeouts(0)}), flush=True)
