@@ -660,7 +660,8 @@ def main():
         wall = wall_k
     else:  # the local reductions run beside RCCL's kernels: the one-shot walk (shard.py, "Overlap")
         walk0 = fa.get_tuning()["walk"]
-        fa.set_tuning(walk=shard.OVERLAP_WALK)
+        if world > 1:  # one rank runs no collective
+            fa.set_tuning(walk=shard.OVERLAP_WALK)
         try:
             wall = time_client_sharded(torch, dist, shard, setup, args.layout, n, world, device, stream,
                                        args.steps, args.warmup, args.chunks, barrier)

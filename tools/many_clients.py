@@ -30,6 +30,10 @@ CONFIGS = {
     "c4": (64, 139_611_210),
     "c5r": (128, 1 << 25),
     "c5": (128, 1 << 28),
+    # C4's slots (64 x 533 MiB), but every launch reduces only their first 32 M elements -- d64's launch on
+    # C4's addresses: slow like C4 -> the slots' placement costs; fast like d64 -> the launch's length does
+    "c4sub": (64, 139_611_210, 32 << 20),
+    "c5sub": (128, 1 << 28, 1 << 25),  # C5's slots, c5r's launch
 }
 
 
@@ -46,14 +50,18 @@ def main():
         fa.set_tuning(**{k: int(v) for k, v in (kv.split("=") for kv in tune.split(","))})
     stream = torch.cuda.Stream()
     for name in names:
-        D, n = CONFIGS[name]
+        D, n, *sub = CONFIGS[name]
         s = bench.Setup(fa, torch, D, n, "f32", "f32", 0, 0)
         torch.cuda.synchronize()
         cl = s.clients(0)
         out = s.agg.output(0)
+        if sub:  # only the first sub[0] elements of every slot, through fa_reduce_device
+            n = sub[0]
         for G in groups:
             if G and G >= D:
                 continue
+            if sub and G == 0:
+                G = D  # one fa_reduce_device launch over all D clients
 
             def launch(k):
                 if G < 0:  # read-only probe over the same slots (fa_diag_read_stream; FA_PHASED_MIN_VECS=0
