@@ -34,7 +34,13 @@ CONFIGS = {
     # C4's addresses: slow like C4 -> the slots' placement costs; fast like d64 -> the launch's length does
     "c4sub": (64, 139_611_210, 32 << 20),
     "c5sub": (128, 1 << 28, 1 << 25),  # C5's slots, c5r's launch
+    # c5r's launch inside C5's pool at c5r's own slot spacing (128 MiB + 512 B): the same relative addresses as
+    # c5r, C5's allocation -- slow like c5sub -> the allocation costs, fast like c5r -> the spacing does
+    "c5sub_s128": (128, 1 << 28, 1 << 25, (128 << 20) + 512),
+    "c5sub_s1g": (128, 1 << 28, 1 << 25, (1 << 30) + 512 + 4096),  # 1 GiB spacing with a 4.5 KiB skew
 }
+for _mib in (256, 512, 768, 1022, 958, 1024):  # spacing sweep inside C5's pool (r03s13)
+    CONFIGS["c5sub_m%d" % _mib] = (128, 1 << 28, 1 << 25, (_mib << 20) + 512)
 
 
 def main():
@@ -57,6 +63,8 @@ def main():
         out = s.agg.output(0)
         if sub:  # only the first sub[0] elements of every slot, through fa_reduce_device
             n = sub[0]
+            if len(sub) > 1:  # the clients at another spacing inside the same pool
+                cl = [cl[0] + k * sub[1] for k in range(D)]
         for G in groups:
             if G and G >= D:
                 continue
