@@ -472,6 +472,18 @@ size_t slot_stride(size_t bytes, size_t skew) {
     return (bytes + a - 1) / a * a + slot_skew_for(bytes, skew);
 }
 
+// A part's device pool.  Experiment knob (tools/): FA_ALLOC_CONTIG=1 asks for physically contiguous memory
+// (hipDeviceMallocContiguous) and falls back to hipMalloc when that fails.
+hipError_t pool_alloc(void** p, size_t bytes) {
+    static const bool contig = [] {
+        const char* e = std::getenv("FA_ALLOC_CONTIG");
+        return e && std::atoi(e) > 0;
+    }();
+    if (contig && hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) return hipSuccess;
+    (void)hipGetLastError();
+    return hipMalloc(p, bytes);
+}
+
 inline bool holds(const Part& p, int g, int k) { return k >= p.c0[(size_t)g] && k < p.c1[(size_t)g]; }
 inline char* slot_ptr(const Part& p, int g, int k) {
     return p.pool[(size_t)g] + (size_t)(k - p.c0[(size_t)g]) * p.stride[(size_t)g];
@@ -1368,7 +1380,7 @@ int fa_bucket_define(fa_ctx* ctx, int part_id, size_t n_elems, fa_dtype in, fa_d
         const size_t extra_off = out_off + (out_bytes + 4095) / 4096 * 4096 + shard16_bytes;
         const size_t extra_bytes = rs ? p.npad * 4 : eager ? p.cnt[g] * 4 : 0;
         const size_t bytes = std::max<size_t>(1, extra_off + extra_bytes);
-        if (hipMalloc((void**)&p.pool[g], bytes) != hipSuccess) {
+        if (pool_alloc((void**)&p.pool[g], bytes) != hipSuccess) {
             (void)hipGetLastError();
             free_part(ctx, p);
             return fail(FA_ERR_NOMEM, "device alloc of %zu B failed on GPU %zu", bytes, g);
