@@ -267,9 +267,9 @@ class Setup:
         for s in range(self.nsets):
             self.agg.define(s, n, self.in_dt, self.out_dt, D, fa.FEDAVG if mode is None else mode)
             for k in range(D):
-                ptr, cnt, _ = self.agg.slot(s, 0, k)
-                # global client id and element offset: ranks hold disjoint clients or slices of one bucket
-                fa.fill_uniform(ptr, cnt, self.in_dt, seed + s, client0 + k, idx0=elem0)
+                for ptr, cnt, off in self.agg.pieces(s, 0, k):
+                    # global client id and element offset: ranks hold disjoint clients or slices of one bucket
+                    fa.fill_uniform(ptr, cnt, self.in_dt, seed + s, client0 + k, idx0=elem0 + off)
         self.w = self._weights(D)
 
     @staticmethod
@@ -808,10 +808,11 @@ def ctx_multi(args):
         with torch.cuda.device(g):
             for k in range(D):
                 try:
-                    ptr, cnt, off = agg.slot(1, g, k)
+                    pcs = agg.pieces(1, g, k)
                 except fa.FaError:  # rs: the client lives on another GPU
                     continue
-                fa.fill_uniform(ptr, cnt, idt, 0x5EED, k, idx0=off)
+                for ptr, cnt, off in pcs:
+                    fa.fill_uniform(ptr, cnt, idt, 0x5EED, k, idx0=off)
     for g in range(G):
         torch.cuda.synchronize(g)
     w = Setup._weights(D)

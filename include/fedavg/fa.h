@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 4
+#define FA_ABI_VERSION 5
 
 typedef struct fa_ctx fa_ctx; /* opaque: device slots, streams, pinned staging */
 
@@ -147,6 +147,15 @@ int fa_reduce_part(fa_ctx* ctx, int part_id, const float* h_weights, void* hip_s
  * simultaneous loads spread over HBM channels. */
 int fa_bucket_slot(fa_ctx* ctx, int part_id, int gpu, int client_slot, void** d_ptr, size_t* n_elems,
                    size_t* elem_offset);
+/* Range layout: a GPU whose client slots would span more than 48 GiB holds them as pieces of <= 16 GiB of
+ * slots each (FA_PIECE_SPAN / FA_PIECE_SPLIT override at fa_bucket_define), reduced one launch
+ * per piece.  fa_bucket_slot then fails (FA_ERR_STATE); a slot is written piece by piece instead.
+ * n_pieces: 1 for every other part. */
+int fa_bucket_pieces(fa_ctx* ctx, int part_id, int gpu, int* n_pieces);
+/* Piece `piece` of client slot `client_slot` on GPU `gpu`: n_elems elements of the input dtype covering
+ * bucket elements [elem_offset, elem_offset+n_elems). */
+int fa_bucket_piece(fa_ctx* ctx, int part_id, int gpu, int piece, int client_slot, void** d_ptr, size_t* n_elems,
+                    size_t* elem_offset);
 /* The part's device output on GPU `gpu` (range: its shard, `out` dtype; rs: its fp32 shard, the blocks
  * fa_rs_segments lists, concatenated). */
 int fa_bucket_output(fa_ctx* ctx, int part_id, int gpu, void** d_ptr);

@@ -62,6 +62,8 @@ def lib():
         "fa_create_ex": (I, [ctypes.POINTER(P), ctypes.POINTER(I), I, I]),
         "fa_reduce_part": (I, [P, I, P, P]),
         "fa_bucket_slot": (I, [P, I, I, I, ctypes.POINTER(P), ctypes.POINTER(S), ctypes.POINTER(S)]),
+        "fa_bucket_pieces": (I, [P, I, I, ctypes.POINTER(I)]),
+        "fa_bucket_piece": (I, [P, I, I, I, I, ctypes.POINTER(P), ctypes.POINTER(S), ctypes.POINTER(S)]),
         "fa_bucket_output": (I, [P, I, I, ctypes.POINTER(P)]),
         "fa_sync": (I, [P]),
         "fa_copy_output": (I, [P, I, P]),
@@ -90,6 +92,7 @@ def lib():
         "fa_diag_plan_chain": (I, [I, I, S, I, I, I, ctypes.POINTER(I), ctypes.POINTER(ctypes.c_longlong)]),
         "fa_diag_rs_plan": (I, [S, I, I, I, I, I, I, ctypes.POINTER(I), ctypes.POINTER(I),
                                 ctypes.POINTER(ctypes.c_longlong)]),
+        "fa_diag_pieces": (I, [S, I, I, ctypes.POINTER(I), ctypes.POINTER(S)]),
         "fa_set_tuning": (I, [ctypes.POINTER(_Tuning)]),
         "fa_get_tuning": (I, [ctypes.POINTER(_Tuning)]),
     }
@@ -191,6 +194,14 @@ def rs_plan(n, n_gpus, n_clients, chunks=0, in_dtype=F32, out_dtype=F32, cus=256
     check(lib().fa_diag_rs_plan(n, n_gpus, n_clients, chunks, in_dtype, out_dtype, cus, ctypes.byref(a),
                                 ctypes.byref(b), ctypes.byref(c)))
     return a.value, b.value, c.value
+
+
+def piece_plan(n, held, in_dtype=F32):
+    """fa_diag_pieces (diagnostic): (pieces, elements per piece) of a range-layout GPU holding `held` slots of
+    n elements (the current FA_PIECE_SPAN / FA_PIECE_SPLIT environment)."""
+    a, b = ctypes.c_int(), ctypes.c_size_t()
+    check(lib().fa_diag_pieces(n, held, in_dtype, ctypes.byref(a), ctypes.byref(b)))
+    return a.value, b.value
 
 
 def _tuning_dict(t):
@@ -348,6 +359,19 @@ class Aggregator:
         check(lib().fa_bucket_slot(self.handle, part_id, gpu, client_slot, ctypes.byref(ptr), ctypes.byref(n),
                                    ctypes.byref(off)))
         return ptr.value, n.value, off.value
+
+    def pieces(self, part_id, gpu, client_slot):
+        """[(device address, n_elems, elem_offset)] of every piece of a client slot, in element order (one
+        entry unless the GPU's slots span more than the piece threshold, fa_bucket_pieces)."""
+        npc = ctypes.c_int()
+        check(lib().fa_bucket_pieces(self.handle, part_id, gpu, ctypes.byref(npc)))
+        out = []
+        for j in range(npc.value):
+            ptr, n, off = ctypes.c_void_p(), ctypes.c_size_t(), ctypes.c_size_t()
+            check(lib().fa_bucket_piece(self.handle, part_id, gpu, j, client_slot, ctypes.byref(ptr),
+                                        ctypes.byref(n), ctypes.byref(off)))
+            out.append((ptr.value, n.value, off.value))
+        return out
 
     def progress(self, part_id):
         """fa_bucket_progress: (receipts submitted this round, leading slots already reduced)."""

@@ -266,7 +266,13 @@ struct Part {
     std::vector<size_t> off, cnt;  // per GPU: bucket elements held by its slots (range: its shard; rs: [0, n))
     std::vector<int> c0, c1;       // per GPU: the client slots it holds, [c0, c1)
     std::vector<char*> pool;       // per GPU: its client slots + the output (+ rs partial, eager acc)
-    std::vector<size_t> stride;    // per GPU: bytes between consecutive slots
+    std::vector<size_t> stride;    // per GPU: bytes between consecutive slots of one piece
+    // Pieces (range layout): a GPU whose slots would span more than 48 GiB (piece_len_for) holds its range as
+    // npiece[g] pieces of piece_len[g] elements (the last one shorter): piece j of every slot lies in the
+    // j-th region of the pool (slots of one piece stride[g] apart), so one launch reads clients that lie
+    // close together (the address span).  One piece = the plain layout.
+    std::vector<int> npiece;
+    std::vector<size_t> piece_len;
     std::vector<void*> dout;       // per GPU: the output (range: cnt elements of `out`; rs: its fp32 shard)
     std::vector<void*> dout16;     // rs with a bf16 output: per GPU, its shard rounded to bf16 (the copy-out's source)
     std::vector<float*> partial;   // rs: per GPU, fp32 partial over its clients, npad elements
@@ -484,10 +490,38 @@ hipError_t pool_alloc(void** p, size_t bytes) {
     return hipMalloc(p, bytes);
 }
 
-inline bool holds(const Part& p, int g, int k) { return k >= p.c0[(size_t)g] && k < p.c1[(size_t)g]; }
-inline char* slot_ptr(const Part& p, int g, int k) {
-    return p.pool[(size_t)g] + (size_t)(k - p.c0[(size_t)g]) * p.stride[(size_t)g];
+// Range pieces ("the address span").  A GPU whose held slots span more than 48 GiB reads
+// them much slower than their bytes say (C5, 128 x 1 GiB: 0.76-0.80 of HBM; the same bytes as 8 pools of
+// 16 GiB: +6-13%, gpurun_out r03s19): the range layout then cuts its elements into pieces of <= 16 GiB of
+// slots each (a multiple of 64 elements) and reduces them one launch after another.  Below the threshold
+// (C4's 34 GiB included: no gain measured) a part is one piece.  Knobs (tests and tools/): FA_PIECE_SPAN
+// = bytes of slots per piece (0: never cut), FA_PIECE_SPLIT = the span above which a GPU's slots are cut;
+// read at each fa_bucket_define.
+size_t piece_len_for(size_t held, size_t cnt, size_t si) {
+    auto env = [](const char* k, long long d) {
+        const char* e = std::getenv(k);
+        return e ? std::atoll(e) : d;
+    };
+    const long long piece = env("FA_PIECE_SPAN", 16LL << 30), split = env("FA_PIECE_SPLIT", 48LL << 30);
+    const size_t span = held * cnt * si;
+    if (piece <= 0 || held == 0 || cnt == 0 || span <= (size_t)std::max(0LL, split)) return std::max<size_t>(cnt, 1);
+    const size_t n = (span + (size_t)piece - 1) / (size_t)piece;
+    const size_t len = ((cnt + n - 1) / n + 63) / 64 * 64;
+    return std::max<size_t>(64, std::min(len, cnt));
 }
+
+inline bool holds(const Part& p, int g, int k) { return k >= p.c0[(size_t)g] && k < p.c1[(size_t)g]; }
+// Piece j of GPU g: GPU-local elements [piece_lo, piece_lo + piece_cnt), the slot of client k at piece_ptr.
+inline size_t piece_lo(const Part& p, int g, int j) { return (size_t)j * p.piece_len[(size_t)g]; }
+inline size_t piece_cnt(const Part& p, int g, int j) {
+    const size_t lo = piece_lo(p, g, j), n = p.cnt[(size_t)g];
+    return lo >= n ? 0 : std::min(p.piece_len[(size_t)g], n - lo);
+}
+inline char* piece_ptr(const Part& p, int g, int k, int j) {
+    const size_t held = (size_t)(p.c1[(size_t)g] - p.c0[(size_t)g]);
+    return p.pool[(size_t)g] + ((size_t)j * held + (size_t)(k - p.c0[(size_t)g])) * p.stride[(size_t)g];
+}
+inline char* slot_ptr(const Part& p, int g, int k) { return piece_ptr(p, g, k, 0); }  // one-piece parts
 
 int check_part(fa_ctx* ctx, int part_id, Part** out) {
     if (!ctx) return fail(FA_ERR_ARG, "ctx is null");
@@ -562,13 +596,18 @@ int mark_done(fa_ctx*, Part& p, int g, hipStream_t s) {
 // Range layout: enqueue the ordered chain over clients [k0, k1) of part p on GPU g, continuing the
 // fp32 accumulator when k0 > 0 (accumulate on arrival) and writing the output dtype when k1 == D.
 int chain_range(fa_ctx* ctx, Part& p, int g, int k0, int k1, const float* w, hipStream_t st) {
-    std::vector<const void*> ptrs;
-    for (int k = k0; k < k1; ++k) ptrs.push_back(slot_ptr(p, g, k));
     const bool last = k1 == p.D;
-    const float* init = k0 > 0 ? p.acc[(size_t)g] : nullptr;
-    void* dst = last ? p.dout[(size_t)g] : (void*)p.acc[(size_t)g];
-    return reduce_on(ctx, g, ctx->tuning.tu, ptrs.data(), w + k0, k1 - k0, p.cnt[(size_t)g], p.in, dst,
-                     last ? p.out : FA_F32, FA_FEDAVG, p.divisor, init, st);
+    for (int j = 0; j < p.npiece[(size_t)g]; ++j) {
+        const size_t lo = piece_lo(p, g, j);
+        std::vector<const void*> ptrs;
+        for (int k = k0; k < k1; ++k) ptrs.push_back(piece_ptr(p, g, k, j));
+        const float* init = k0 > 0 ? p.acc[(size_t)g] + lo : nullptr;
+        void* dst = last ? static_cast<char*>(p.dout[(size_t)g]) + lo * dsize(p.out) : (void*)(p.acc[(size_t)g] + lo);
+        int rc = reduce_on(ctx, g, ctx->tuning.tu, ptrs.data(), w + k0, k1 - k0, piece_cnt(p, g, j), p.in, dst,
+                           last ? p.out : FA_F32, FA_FEDAVG, p.divisor, init, st);
+        if (rc) return rc;
+    }
+    return FA_OK;
 }
 
 // Every launch of the rs layout (the piece reductions, the bf16 rounding, the test-only emulated exchange) may
@@ -620,15 +659,18 @@ int reduce_part(fa_ctx* ctx, Part& p, const float* w, hipStream_t s) {
             hipStream_t st = s ? s : r.compute;
             int rc = wait_copies(ctx, g, st);
             if (rc) return rc;
-            if (p.mode == FA_LITERAL) {
-                const void* last = slot_ptr(p, g, p.last_slot >= 0 ? p.last_slot : p.D - 1);
-                rc = reduce_on(ctx, g, ctx->tuning.tu, &last, w, 1, p.cnt[(size_t)g], p.in, p.dout[(size_t)g], p.out,
-                               FA_LITERAL, p.divisor, nullptr, st);
-            } else {
-                std::vector<const void*> ptrs;
-                for (int k = 0; k < p.D; ++k) ptrs.push_back(slot_ptr(p, g, k));
-                rc = reduce_on(ctx, g, ctx->tuning.tu, ptrs.data(), w, p.D, p.cnt[(size_t)g], p.in, p.dout[(size_t)g],
-                               p.out, FA_FEDAVG, p.divisor, nullptr, st);
+            for (int j = 0; j < p.npiece[(size_t)g] && !rc; ++j) {  // one launch per piece, in order
+                void* dst = static_cast<char*>(p.dout[(size_t)g]) + piece_lo(p, g, j) * dsize(p.out);
+                if (p.mode == FA_LITERAL) {
+                    const void* last = piece_ptr(p, g, p.last_slot >= 0 ? p.last_slot : p.D - 1, j);
+                    rc = reduce_on(ctx, g, ctx->tuning.tu, &last, w, 1, piece_cnt(p, g, j), p.in, dst, p.out,
+                                   FA_LITERAL, p.divisor, nullptr, st);
+                } else {
+                    std::vector<const void*> ptrs;
+                    for (int k = 0; k < p.D; ++k) ptrs.push_back(piece_ptr(p, g, k, j));
+                    rc = reduce_on(ctx, g, ctx->tuning.tu, ptrs.data(), w, p.D, piece_cnt(p, g, j), p.in, dst, p.out,
+                                   FA_FEDAVG, p.divisor, nullptr, st);
+                }
             }
             if (rc || (rc = mark_done(ctx, p, g, st))) return rc;
         }
@@ -805,12 +847,24 @@ int submit_impl(fa_ctx* ctx, int part_id, int slot, const Gather& src, float wei
         GpuRes& r = ctx->gpu[(size_t)g];
         DeviceGuard dg(r.dev);
         const size_t base = p->off[(size_t)g] * si;
-        char* ds = slot_ptr(*p, g, slot);
         const size_t bytes = p->cnt[(size_t)g] * si;
+        // bytes [x, x + len) of this GPU's range -> fn(device address, x', take) per stretch within one piece
+        const size_t piece_bytes = p->piece_len[(size_t)g] * si;
+        auto to_device = [&](size_t x, size_t len, const std::function<void(char*, size_t, size_t)>& fn) {
+            while (len > 0) {
+                const int j = (int)(x / piece_bytes);
+                const size_t in = x - (size_t)j * piece_bytes, take = std::min(len, piece_bytes - in);
+                fn(piece_ptr(*p, g, slot, j) + in, x, take);
+                x += take;
+                len -= take;
+            }
+        };
         if (pinned) {  // pinned segments: DMA straight from them, one copy per piece of this GPU's range
             hipError_t e = hipSuccess;
             src.pieces(base, bytes, [&](char* piece, size_t rel, size_t take) {
-                if (e == hipSuccess) e = hipMemcpyAsync(ds + rel, piece, take, hipMemcpyHostToDevice, r.copy);
+                to_device(rel, take, [&](char* dev, size_t x, size_t t) {
+                    if (e == hipSuccess) e = hipMemcpyAsync(dev, piece + (x - rel), t, hipMemcpyHostToDevice, r.copy);
+                });
             });
             ++r.copy_gen;
             FA_HIP(e);
@@ -824,7 +878,11 @@ int submit_impl(fa_ctx* ctx, int part_id, int slot, const Gather& src, float wei
             r.stage_i ^= 1;
             FA_HIP(hipEventSynchronize(r.stage_ev[i]));
             r.pool->copy(r.stage[i], b, [&](size_t lo, size_t len, char* d) { src.copy_out(base + o + lo, len, d); });
-            FA_HIP(hipMemcpyAsync(ds + o, r.stage[i], b, hipMemcpyHostToDevice, r.copy));
+            hipError_t e = hipSuccess;
+            to_device(o, b, [&](char* dev, size_t x, size_t t) {
+                if (e == hipSuccess) e = hipMemcpyAsync(dev, r.stage[i] + (x - o), t, hipMemcpyHostToDevice, r.copy);
+            });
+            FA_HIP(e);
             FA_HIP(hipEventRecord(r.stage_ev[i], r.copy));
         }
         return FA_OK;
@@ -978,7 +1036,8 @@ int reduce_parts_impl(fa_ctx* ctx, int n_parts, const int* ids, const float* con
         bool batch = !p.rs && p.mode == FA_FEDAVG && p.D <= fa::kMaxClients;
         for (int g = 0; batch && g < ctx->G; ++g) {
             DeviceGuard dg(ctx->gpu[(size_t)g].dev);
-            batch = !fa::phased_takes(p.in, p.out, (int64_t)(p.cnt[(size_t)g] * dsize(p.in) / 16), p.D, tu);
+            batch = p.npiece[(size_t)g] == 1 &&
+                    !fa::phased_takes(p.in, p.out, (int64_t)(p.cnt[(size_t)g] * dsize(p.in) / 16), p.D, tu);
         }
         if (batch) groups[{(int)p.in, (int)p.out}].push_back(i);
         else single.push_back(i);
@@ -1357,6 +1416,8 @@ int fa_bucket_define(fa_ctx* ctx, int part_id, size_t n_elems, fa_dtype in, fa_d
     p.dout.assign(G, nullptr);
     p.dout16.assign(G, nullptr);
     p.stride.assign(G, 0);
+    p.npiece.assign(G, 1);
+    p.piece_len.assign(G, 0);
     p.partial.assign(G, nullptr);
     p.acc.assign(G, nullptr);
     p.done.assign(G, nullptr);
@@ -1369,14 +1430,21 @@ int fa_bucket_define(fa_ctx* ctx, int part_id, size_t n_elems, fa_dtype in, fa_d
             free_part(ctx, p);
             return fail(FA_ERR_HIP, "event creation failed");
         }
-        const size_t slot_elems = rs ? p.npad : p.cnt[g];
         const size_t held = (size_t)(p.c1[g] - p.c0[g]);
-        p.stride[g] = slot_stride(slot_elems * dsize(in), ctx->tuning.slot_skew);
-        // one allocation: slots, then the output (range: cnt of `out`; rs: the fp32 shard, + its bf16
-        // rounding for a bf16 output), then the rs partial or the eager accumulator, each 4 KiB aligned
+        if (rs) {
+            p.npiece[g] = 1;
+            p.piece_len[g] = p.npad;
+        } else {
+            p.piece_len[g] = piece_len_for(held, p.cnt[g], dsize(in));
+            p.npiece[g] = p.cnt[g] ? (int)((p.cnt[g] + p.piece_len[g] - 1) / p.piece_len[g]) : 1;
+        }
+        p.stride[g] = slot_stride(p.piece_len[g] * dsize(in), ctx->tuning.slot_skew);
+        // one allocation: the slots (piece-major: piece j of every held slot, then piece j+1), then the
+        // output (range: cnt of `out`; rs: the fp32 shard, + its bf16 rounding for a bf16 output), then the
+        // rs partial or the eager accumulator, each 4 KiB aligned
         const size_t shard16_bytes = rs && out == FA_BF16 ? (p.npad / G * 2 + 4095) / 4096 * 4096 : 0;
         const size_t out_bytes = rs ? p.npad / G * 4 : p.cnt[g] * dsize(out);
-        const size_t out_off = held * p.stride[g];
+        const size_t out_off = (size_t)p.npiece[g] * held * p.stride[g];
         const size_t extra_off = out_off + (out_bytes + 4095) / 4096 * 4096 + shard16_bytes;
         const size_t extra_bytes = rs ? p.npad * 4 : eager ? p.cnt[g] * 4 : 0;
         const size_t bytes = std::max<size_t>(1, extra_off + extra_bytes);
@@ -1514,9 +1582,41 @@ int fa_bucket_slot(fa_ctx* ctx, int part_id, int gpu, int client_slot, void** d_
     if (!holds(*p, gpu, client_slot))
         return fail(FA_ERR_ARG, "client slot %d is not held by GPU %d (rs layout: slots [%d,%d))", client_slot, gpu,
                     p->c0[(size_t)gpu], p->c1[(size_t)gpu]);
+    if (p->npiece[(size_t)gpu] > 1)
+        return fail(FA_ERR_STATE, "part %d is held as %d pieces on GPU %d: use fa_bucket_piece", part_id,
+                    p->npiece[(size_t)gpu], gpu);
     if (d_ptr) *d_ptr = slot_ptr(*p, gpu, client_slot);
     if (n_elems) *n_elems = p->cnt[(size_t)gpu];
     if (elem_offset) *elem_offset = p->off[(size_t)gpu];
+    return FA_OK;
+}
+
+int fa_bucket_pieces(fa_ctx* ctx, int part_id, int gpu, int* n_pieces) {
+    g_err.clear();
+    Part* p;
+    int rc = check_part(ctx, part_id, &p);
+    if (rc) return rc;
+    if (gpu < 0 || gpu >= ctx->G) return fail(FA_ERR_ARG, "gpu %d out of range", gpu);
+    if (!n_pieces) return fail(FA_ERR_ARG, "n_pieces is null");
+    *n_pieces = p->npiece[(size_t)gpu];
+    return FA_OK;
+}
+
+int fa_bucket_piece(fa_ctx* ctx, int part_id, int gpu, int piece, int client_slot, void** d_ptr, size_t* n_elems,
+                    size_t* elem_offset) {
+    g_err.clear();
+    Part* p;
+    int rc = check_part(ctx, part_id, &p);
+    if (rc) return rc;
+    if (gpu < 0 || gpu >= ctx->G) return fail(FA_ERR_ARG, "gpu %d out of range", gpu);
+    if (piece < 0 || piece >= p->npiece[(size_t)gpu]) return fail(FA_ERR_ARG, "piece %d out of range", piece);
+    if (client_slot < 0 || client_slot >= p->D) return fail(FA_ERR_ARG, "client slot %d out of range", client_slot);
+    if (!holds(*p, gpu, client_slot))
+        return fail(FA_ERR_ARG, "client slot %d is not held by GPU %d (rs layout: slots [%d,%d))", client_slot, gpu,
+                    p->c0[(size_t)gpu], p->c1[(size_t)gpu]);
+    if (d_ptr) *d_ptr = piece_ptr(*p, gpu, client_slot, piece);
+    if (n_elems) *n_elems = piece_cnt(*p, gpu, piece);
+    if (elem_offset) *elem_offset = p->off[(size_t)gpu] + piece_lo(*p, gpu, piece);
     return FA_OK;
 }
 
@@ -1622,10 +1722,12 @@ int fa_sync_part(fa_ctx* ctx, int part_id, const float* h_weights, void* hip_str
     for (int g = 0; g < ctx->G; ++g) {
         GpuRes& r = ctx->gpu[(size_t)g];
         DeviceGuard dg(r.dev);
-        for (int k = 0; k < p->D; ++k) ptrs[(size_t)k] = slot_ptr(*p, g, k);
         hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : r.compute;
         if ((rc = wait_copies(ctx, g, st))) return rc;  // the slots' submits land first
-        if ((rc = sync_on(ctx, g, ctx->tuning.tu, ptrs.data(), w, p->D, p->cnt[(size_t)g], p->in, st))) return rc;
+        for (int j = 0; j < p->npiece[(size_t)g]; ++j) {
+            for (int k = 0; k < p->D; ++k) ptrs[(size_t)k] = piece_ptr(*p, g, k, j);
+            if ((rc = sync_on(ctx, g, ctx->tuning.tu, ptrs.data(), w, p->D, piece_cnt(*p, g, j), p->in, st))) return rc;
+        }
     }
     return FA_OK;
 }
@@ -1718,6 +1820,18 @@ extern "C" int fa_diag_rs_plan(size_t n, int n_gpus, int n_clients, int chunks, 
     if (launches) *launches = nl;
     if (phased_launches) *phased_launches = np;
     if (max_phases) *max_phases = mp;
+    return FA_OK;
+}
+
+// Diagnostic, not part of the ABI in fa.h: how a range-layout GPU holding `held` slots of n elements of
+// `in` cuts them (piece_len_for, the current FA_PIECE_SPAN / FA_PIECE_SPLIT): *n_pieces pieces of
+// *piece_elems elements (the last one shorter).  Pure host arithmetic.
+extern "C" int fa_diag_pieces(size_t n, int held, int in, int* n_pieces, size_t* piece_elems) {
+    g_err.clear();
+    if (held < 0 || !dvalid(in)) return fail(FA_ERR_ARG, "bad piece arguments");
+    const size_t len = piece_len_for((size_t)held, n, dsize((fa_dtype)in));
+    if (n_pieces) *n_pieces = n ? (int)((n + len - 1) / len) : 1;
+    if (piece_elems) *piece_elems = len;
     return FA_OK;
 }
 

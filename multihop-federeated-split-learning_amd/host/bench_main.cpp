@@ -87,12 +87,15 @@ int main(int argc, char** argv) {
     // synthetic client buckets generated in HBM (bench.py's inputs: seed 0x5EED, client k, global index)
     for (int g = 0; g < gpus; ++g) {
         hip_check(hipSetDevice(g), "hipSetDevice");
-        for (int k = 0; k < D; ++k) {
-            void* p = nullptr;
-            size_t cnt = 0, off = 0;
-            if (fa_bucket_slot(ctx, part, g, k, &p, &cnt, &off) != FA_OK) continue;  // rs: another GPU's client
-            check(fa_fill_uniform(p, cnt, wl->in, 0x5EED, (uint32_t)k, off, nullptr), "fa_fill_uniform");
-        }
+        int npc = 1;
+        check(fa_bucket_pieces(ctx, part, g, &npc), "fa_bucket_pieces");
+        for (int k = 0; k < D; ++k)
+            for (int j = 0; j < npc; ++j) {
+                void* p = nullptr;
+                size_t cnt = 0, off = 0;
+                if (fa_bucket_piece(ctx, part, g, j, k, &p, &cnt, &off) != FA_OK) break;  // rs: another GPU's client
+                check(fa_fill_uniform(p, cnt, wl->in, 0x5EED, (uint32_t)k, off, nullptr), "fa_fill_uniform");
+            }
     }
     for (int g = 0; g < gpus; ++g) {
         hip_check(hipSetDevice(g), "hipSetDevice");

@@ -3,9 +3,10 @@ MI355X (VERDICT r02 "next" #1 and #6).  The 8-GPU leg of C5 needs the driver's n
 runs whole on one GPU through the three paths the aggregator uses (the reduction replaced is
 aggregator.cpp:112-150):
 
-* the range context, device-resident (the phased kernel: 12 phases, 11 chip-wide meetings): sampled elements
-  against the oracle's chain, a chain split over two launches equal to the single launch in every bit, and
-  no meeting that gave up waiting;
+* the range context, device-resident: a GPU holding 128 GiB of slots cuts them into 8 pieces of 16 GiB
+  ("the address span") reduced one launch after another; sampled elements against the oracle's
+  chain, the chain split over two launches per piece equal to the context's result in every bit, and no
+  phased meeting that gave up waiting;
 * the rs context at one GPU (FA_SHARD_CLIENT_RS: per-piece reductions + a one-rank reduce-scatter, i.e. a
   copy), whose launches never take the phased grid: bit-exact at the sampled elements, no timeout;
 * host-inclusive: 128 fa_submit_pinned receipts (8 distinct host buckets, client k sends bucket k mod 8) and
@@ -34,8 +35,8 @@ def filled_ctx(fa, torch, rs):
     agg = fa.Aggregator(devices=[0], rs=rs)
     agg.define(1, N, fa.F32, fa.F32, D, fa.FEDAVG)
     for k in range(D):
-        ptr, cnt, off = agg.slot(1, 0, k)
-        fa.fill_uniform(ptr, cnt, fa.F32, SEED, k, idx0=off)
+        for ptr, cnt, off in agg.pieces(1, 0, k):
+            fa.fill_uniform(ptr, cnt, fa.F32, SEED, k, idx0=off)
     torch.cuda.synchronize()
     return agg
 
@@ -47,15 +48,18 @@ def test_c5_range_context_sampled_split_and_no_timeouts(fa, O, torch_gpu):
     ref = O.fedavg_at(SEED, w, idx)
     t0 = fa.phased_timeouts(0)
     with filled_ctx(fa, torch, rs=False) as agg:
-        assert fa.plan_chain(fa.F32, fa.F32, N, D, cus=torch.cuda.get_device_properties(0).multi_processor_count)[1] >= 12
+        pcs = agg.pieces(1, 0, 0)
+        assert len(pcs) == 8 and sum(c for _, c, _ in pcs) == N
         agg.reduce(1, w)
         out = agg.copy_output(1)  # waits for the reduction, D2H of the 1 GiB result
         assert_bits(out[idx], ref)
-        # the same chain in two launches (first 50 clients, then 78 continuing it): the same bits everywhere
-        cl = [agg.slot(1, 0, k)[0] for k in range(D)]
+        # per piece, the same chain in two launches (first 50 clients, then 78 continuing it): the same bits
         acc = torch.empty(N, dtype=torch.float32, device="cuda")
-        fa.reduce_device(cl[:50], w[:50], N, fa.F32, acc, fa.F32)
-        fa.reduce_device(cl[50:], w[50:], N, fa.F32, acc, fa.F32, init=acc)
+        for j, (_, cnt, off) in enumerate(pcs):
+            cl = [agg.pieces(1, 0, k)[j][0] for k in range(D)]
+            a = acc[off:off + cnt]
+            fa.reduce_device(cl[:50], w[:50], cnt, fa.F32, a, fa.F32)
+            fa.reduce_device(cl[50:], w[50:], cnt, fa.F32, a, fa.F32, init=a)
         torch.cuda.synchronize()
         assert np.array_equal(out.view(np.uint32), acc.cpu().numpy().view(np.uint32))
         del out, acc

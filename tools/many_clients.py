@@ -59,7 +59,9 @@ def main():
         D, n, *sub = CONFIGS[name]
         s = bench.Setup(fa, torch, D, n, "f32", "f32", 0, 0)
         torch.cuda.synchronize()
-        cl = s.clients(0)
+        # raw slot addresses only for the probe / split / sub legs (a pieced part has none: FA_PIECE_SPAN=0
+        # keeps C5's pool whole for them)
+        cl = s.clients(0) if sub or any(g != 0 for g in groups) else None
         out = s.agg.output(0)
         if sub:  # only the first sub[0] elements of every slot, through fa_reduce_device
             n = sub[0]
