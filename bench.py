@@ -54,6 +54,8 @@ WORKLOADS = {
     "c4": (64, 139_611_210, "f32", "f32", "VGG-19 full model buckets (reference build), 64 owners, fp32, on one GPU"),
     "c5": (128, 1 << 28, "f32", "f32", "synthetic 1 GiB fp32 bucket x 128 clients, all on one GPU (129 GiB resident)"),
     "c5r": (128, 1 << 25, "f32", "f32", "C5 one rank's share on 8 GPUs (range layout): 128 clients x 128 MiB slice"),
+    # C4 is a 4-GPU config: rank 0's range share of it (shard.range_bounds(139_611_210, 4, 0))
+    "c4r": (64, 34_902_848, "f32", "f32", "C4 one rank's share on 4 GPUs (range layout): 64 clients x 133 MiB slice"),
     # one rank's share of the strong-scaled north star (bench.py --gpus W): 32 clients x 256/W MiB
     "ns_w2": (32, 32 << 20, "f32", "f32", "north star, one rank's share at 2 GPUs (strong scaling): 32 x 128 MiB"),
     "ns_w4": (32, 16 << 20, "f32", "f32", "north star, one rank's share at 4 GPUs (strong scaling): 32 x 64 MiB"),

@@ -40,7 +40,7 @@ for s in $STEPS; do
             rc=$?; tail -2 "$OUT/pmc_$c.err"; ok_or_fail $rc pmc_$c
         done ;;
     pmcw)  # the same passes for the secondary workloads whose traffic bench.py reports
-        bash tools/pmc_workloads.sh "$TAG" ${PMC_WORKLOADS:-c2 c3 c4 c5 c5r ns_w2 ns_w4 ns_w8}
+        bash tools/pmc_workloads.sh "$TAG" ${PMC_WORKLOADS:-c2 c3 c4 c4r c5 c5r ns_w2 ns_w4 ns_w8}
         rc=$?; ok_or_fail $rc pmcw ;;
     layouts)
         for L in rs chain; do

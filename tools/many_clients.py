@@ -29,6 +29,7 @@ CONFIGS = {
     "d128": (128, 16 << 20),
     "c4": (64, 139_611_210),
     "c5r": (128, 1 << 25),
+    "c4r": (64, 34_902_848),  # C4's rank-0 range share at 4 GPUs
     "c5": (128, 1 << 28),
     # C4's slots (64 x 533 MiB), but every launch reduces only their first 32 M elements -- d64's launch on
     # C4's addresses: slow like C4 -> the slots' placement costs; fast like d64 -> the launch's length does
