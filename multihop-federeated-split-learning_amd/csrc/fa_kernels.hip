@@ -409,7 +409,7 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
                                                                        unsigned* sync, int slack, int rl_last,
                                                                        int skew, int skew_last, int last_meet,
                                                                        unsigned long long* tl, unsigned* claims,
-                                                                       int dyn_p, int fold_rows) {
+                                                                       int dyn_p) {
     constexpr int V = In<IN>::kVec, T = TH, RL = Phased<IN, REGS, TH, OUT>::RL, RR = Phased<IN, REGS, TH, OUT>::RR;
     constexpr int U = TH > 256 ? 8 : 16;  // loads in flight per wave (2 waves per SIMD at 512 threads)
     constexpr bool kPacked = std::is_same<LdsT<OUT>, uint16_t>::value;  // LDS rows hold bf16 output bits
@@ -433,9 +433,7 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
     // take `skew` fewer LDS rows than the even ones in every full phase, and 2 skew_last fewer in the last
     // (rl_last - skew_last against rl_last + skew_last) -- those XCDs read 5-10% slower (tools/timeline.py)
     const int64_t per_phase = G * T * (RL + RR) - (G / 2) * T * skew;
-    // fold_rows > 0: the bucket's remainder past its last full phase is not a short phase of its own but
-    // fold_rows rows per workgroup at the start of the last full phase, written straight out (phased_enqueue)
-    const int phases = fold_rows ? (int)(nvec / per_phase) : (int)((nvec + per_phase - 1) / per_phase);
+    const int phases = (int)((nvec + per_phase - 1) / per_phase);
     const bool odd = blockIdx.x & 1;
     // the meeting before phase p's writes: every workgroup's reads of the phase are done (all but `slack`)
     auto meet = [&](int p) {
@@ -577,26 +575,11 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
             }
             continue;
         }
-        // a folded remainder: its rows first (row i of workgroup b: block (i G + b) of T vectors after the last
-        // full phase), each written as soon as it is reduced; the phase itself is a full one, with its meeting
-        const bool short_last = last && !fold_rows;
-        if (last && fold_rows) {
-            const int64_t f0 = (int64_t)(p + 1) * per_phase + threadIdx.x;
-#pragma unroll 1
-            for (int i = 0; i < fold_rows; ++i) {
-                const int64_t v = f0 + ((int64_t)i * G + blockIdx.x) * T;
-                if (v < nvec) {
-                    float acc[V];
-                    chain_vec<IN, U, true, INIT>(t, nc, init, head + v * V, acc);
-                    put<OUT, V, SYNC>(t, nc, out, head + v * V, acc);
-                }
-            }
-        }
         // LDS vectors per lane in this phase: r_all rows every workgroup takes, then r_even more that only
         // the even XCDs' take.  Full phases: RL - skew and skew; the last phase is balanced by the host
         // (rl_last per lane on average, registers first: phased_rl_last)
-        const int r_all = short_last ? rl_last - skew_last : RL - skew;
-        const int r_even = short_last ? 2 * skew_last : skew;
+        const int r_all = last ? rl_last - skew_last : RL - skew;
+        const int r_even = last ? 2 * skew_last : skew;
         const int rl = r_all + (odd ? 0 : r_even);
         // LDS row i: block (i G + b) of T vectors for i < r_all, block (r_all G + (i - r_all) G/2 + b/2) after
         const int64_t p0 = (int64_t)p * per_phase + threadIdx.x;
@@ -638,7 +621,7 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
                 }
             }
         }
-        if (!short_last || last_meet) meet(p);
+        if (!last || last_meet) meet(p);
         else __syncthreads();
 #pragma unroll 1
         for (int i = 0; i < rl; ++i) {
@@ -1027,22 +1010,6 @@ inline int phased_rl_last(int64_t rem, int64_t lanes, int RL, int RR) {
 // 0.425-0.427 ms against 0.424, 4 rows 0.444-0.449; r02s26-s27), and its bf16 rows (20) keep none either.  FA_PHASED_SKEW overrides it (below RL / 2).
 std::atomic<uint64_t> g_dyn_launches{0};
 
-// FA_PHASED_FOLD = the largest remainder past a bucket's last full phase, in % of a phase, that is folded into
-// that phase (its rows reduced first and written straight out, no short phase of its own); 0: never.
-int phased_fold_pct() {
-    static const int v = [] {
-        const char* e = std::getenv("FA_PHASED_FOLD");
-        return e ? std::max(0, std::atoi(e)) : 0;
-    }();
-    return v;
-}
-// Rows per workgroup (of T vectors) of the folded remainder of a bucket of nvec vectors, or 0 (not folded).
-int phased_fold_rows(int64_t nvec, int64_t per_phase, int64_t groups, int T) {
-    const int64_t full = nvec / per_phase, rem = nvec - full * per_phase;
-    if (full < 1 || rem <= 0 || rem * 100 > (int64_t)phased_fold_pct() * per_phase) return 0;
-    return (int)((rem + groups * T - 1) / (groups * T));
-}
-
 // FA_PHASED_DYN = rows per workgroup in every phase's dynamic pool (0: the static form).
 int phased_dyn_rows() {
     static const int v = [] {
@@ -1080,12 +1047,10 @@ hipError_t phased_enqueue(PhasedDevice* d, Kern kern, Kern dyn_kern, int th, int
     // parity); a partition of the chip (fewer CUs per device) keeps the plain layout
     const int skew = d->cus >= 256 && d->cus % 16 == 0 ? phased_skew(RL) : 0;
     const int64_t per_phase = lanes * (RL + RR) - (int64_t)(d->cus / 2) * th * skew;
-    // a remainder of at most phased_fold_pct() % of a phase past the last full one is folded into it
-    const int fold_rows = dyn ? 0 : phased_fold_rows(nvec, per_phase, lanes / th, th);
-    const int64_t phases = fold_rows ? nvec / per_phase : (nvec + per_phase - 1) / per_phase;
+    const int64_t phases = (nvec + per_phase - 1) / per_phase;
     // the dynamic form: every phase's LDS part averages RL - skew / 2 rows, none skewed
-    const int rl_last = fold_rows ? RL : phased_rl_last(nvec - (phases - 1) * per_phase, lanes, dyn ? RL - skew / 2 : RL, RR);
-    const int skew_last = dyn || fold_rows ? 0 : std::min({(skew + 1) / 2, rl_last, RL - rl_last});
+    const int rl_last = phased_rl_last(nvec - (phases - 1) * per_phase, lanes, dyn ? RL - skew / 2 : RL, RR);
+    const int skew_last = dyn ? 0 : std::min({(skew + 1) / 2, rl_last, RL - rl_last});
     // The last phase writes without the meeting: each workgroup as soon as it has read its share, beside
     // the slower workgroups' last reads (one rank's share at 2 / 4 / 8 GPUs 0.664 / 0.344 / 0.173 ms
     // against 0.670 / 0.346 / 0.176 with the meeting, north star, C3 and C4 unchanged; gpurun_out r02s36).
@@ -1099,7 +1064,7 @@ hipError_t phased_enqueue(PhasedDevice* d, Kern kern, Kern dyn_kern, int th, int
     if (dyn) g_dyn_launches.fetch_add(1, std::memory_order_relaxed);
     hipLaunchKernelGGL(dyn ? dyn_kern : kern, dim3((unsigned)d->cus), dim3(th), 0, s, t, nc, init, out, head, nvec, n,
                        d->sync + slot * kSyncStride, slack, rl_last, skew, skew_last, last_meet, d->tl,
-                       dyn ? d->claims + (size_t)slot * kSyncRing * kDynPhases : nullptr, dyn, fold_rows);
+                       dyn ? d->claims + (size_t)slot * kSyncRing * kDynPhases : nullptr, dyn);
     return hipGetLastError();
 }
 
@@ -1251,9 +1216,7 @@ ChainPlan plan_chain(fa_dtype in, fa_dtype out, int64_t nvec, int nc, bool vecto
     }
     const int skew = cus >= 256 && cus % 16 == 0 ? phased_skew(rl) : 0;  // as phased_enqueue
     const int64_t per_phase = lanes * (rl + regs / V) - (int64_t)(cus / 2) * th * skew;
-    // a folded remainder (phased_enqueue; not in the dynamic form) adds no phase of its own
-    const bool fold = phased_dyn_rows() == 0 && phased_fold_rows(nvec, per_phase, cus, th) > 0;
-    return ChainPlan{kPlanPhased, regs, th, fold ? nvec / per_phase : (nvec + per_phase - 1) / per_phase};
+    return ChainPlan{kPlanPhased, regs, th, (nvec + per_phase - 1) / per_phase};
 }
 
 uint64_t dyn_launches() { return g_dyn_launches.load(std::memory_order_relaxed); }

@@ -1,6 +1,6 @@
-"""Child process of tests/test_phased_forms.py (GPU): the phased kernel's alternative forms -- the dynamic row
-pool (FA_PHASED_DYN) and the folded remainder (FA_PHASED_FOLD), knobs read once per process -- against the
-one-shot walk on the same device inputs, whole buckets bit for bit, plus sampled elements against the oracle.
+"""Child process of tests/test_phased_forms.py (GPU): the phased kernel's dynamic row pool (FA_PHASED_DYN, read
+once per process) against the one-shot walk on the same device inputs, whole buckets bit for bit, plus sampled
+elements against the oracle (the bf16 shapes run the static 512-thread form, which has no dynamic one).
 Prints one JSON line.
 
   FA_PHASED_DYN=8 python tests/phased_child.py
@@ -76,8 +76,7 @@ def main():
                         "oracle_sampled_ok": oracle_ok, "dyn_launches": fa.diag_dyn_launches() - d0})
         del clients, outs, init
         torch.cuda.empty_cache()
-    print(json.dumps({"dyn": int(os.environ.get("FA_PHASED_DYN", "0")),
-                      "fold": int(os.environ.get("FA_PHASED_FOLD", "0")), "cases": results}))
+    print(json.dumps({"dyn": int(os.environ.get("FA_PHASED_DYN", "0")), "cases": results}))
 
 
 if __name__ == "__main__":

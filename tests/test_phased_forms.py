@@ -1,7 +1,6 @@
-"""The phased kernel's alternative forms on the GPU, each against the one-shot walk (whole buckets, bit for bit)
-and the oracle (sampled elements): the dynamic row pool (FA_PHASED_DYN) at one row per workgroup, the
-measured size, every LDS row of a phase in the pool and more rows than a phase holds; and the folded remainder
-(FA_PHASED_FOLD) at C3's 28% and at every remainder.  Shapes: multi-phase f32 buckets, LDS-only and near-empty
+"""The phased kernel's dynamic row pool (FA_PHASED_DYN) on the GPU against the one-shot walk (whole buckets, bit
+for bit) and the oracle (sampled elements), at one row per workgroup, the measured size, every LDS row of a
+phase in the pool and more rows than a phase holds.  Shapes: multi-phase f32 buckets, LDS-only and near-empty
 remainders, 1 to 64 clients, a sized phase, a d_init continuation, and bf16 buckets of the 512-thread form
 (tests/phased_child.py).  Each setting runs in its own child process (the knobs are read once per process),
 one after another."""
@@ -31,17 +30,6 @@ def run_child(env_extra):
 
 @pytest.mark.parametrize("dyn", [1, 8, 38, 200])
 def test_dyn_pool_same_bits(dyn):
-    for c in run_child({"FA_PHASED_DYN": str(dyn), "FA_PHASED_FOLD": "0"}):
+    for c in run_child({"FA_PHASED_DYN": str(dyn)}):
         if not c["bf16"]:  # the f32 form has a dynamic instantiation: it must be what ran
             assert c["dyn_launches"] >= 1, c
-
-
-@pytest.mark.parametrize("fold", [30, 100])
-def test_folded_remainder_same_bits(fold):
-    cases = run_child({"FA_PHASED_FOLD": str(fold), "FA_PHASED_DYN": "0"})
-    # (clients, n) -> phases of the plan: a folded remainder adds none
-    by_shape = {(c["clients"], c["bf16"], c["n"]): c["plan"] for c in cases}
-    folded = [c for c in cases if c["plan"][0] == 2 and c["plan"][1] >= 1]
-    assert folded, by_shape
-    c3 = [c for c in cases if c["bf16"] and c["clients"] == 32][0]
-    assert c3["plan"][1] == 1, c3  # C3's shape: one phase and its 28% remainder folded
