@@ -400,7 +400,10 @@ __device__ __forceinline__ void put_bf16_bits(const ClientTable& t, int nc, void
 // 4 KiB block is still fetched in one burst.  Claimed rows go to the free LDS slots (the form gives one slot
 // to the claim broadcast); a workgroup whose slots are full writes further rows straight to the output.
 // Which workgroup reduces which row changes, never the chain of an element: same bits.  The counters are
-// per (counter slot, ring entry, phase); the last workgroup of a launch to leave zeroes its entry's.
+// per (counter slot, ring entry, phase); the last workgroup of a launch to leave zeroes its entry's.  A graph
+// that captured a dynamic-form launch keeps its capture stream's slot, so its replays must not overlap
+// launches of that stream (replays on the capture stream are serialized with them).  Off by default (§4 of
+// same speed as the static form).
 constexpr int kDynPhases = 64;  // phases of one launch that have a pool; later ones are all static rows
 
 template <typename IN, typename OUT, bool INIT, int REGS, bool SYNC, int TH, bool DYN = false>
