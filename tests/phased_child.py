@@ -76,7 +76,30 @@ def main():
                         "oracle_sampled_ok": oracle_ok, "dyn_launches": fa.diag_dyn_launches() - d0})
         del clients, outs, init
         torch.cuda.empty_cache()
-    print(json.dumps({"dyn": int(os.environ.get("FA_PHASED_DYN", "0")), "cases": results}))
+    # many streams at once: 52 launches of one two-phase bucket, each on a stream of its own, enqueued without a
+    # sync in between -- the first 48 streams own their counter slots (the dynamic form), the rest share hashed
+    # slots (the static form); grids that cannot all be resident meet late (bounded waits), never wrongly
+    n = 89 * cus * 256 * 4 - 5
+    D = 3
+    w = O.weights(D)
+    clients = []
+    for k in range(D):
+        t = torch.empty(n, dtype=torch.float32, device="cuda")
+        fa.fill_uniform(t, n, fa.F32, 77, k)
+        clients.append(t)
+    ref = torch.empty(n, dtype=torch.float32, device="cuda")
+    fa.reduce_device(clients, w, n, fa.F32, ref, fa.F32, fa.FEDAVG)
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream() for _ in range(52)]
+    outs = [torch.empty(n, dtype=torch.float32, device="cuda") for _ in streams]
+    d0 = fa.diag_dyn_launches()
+    for s, o in zip(streams, outs):
+        fa.reduce_device(clients, w, n, fa.F32, o, fa.F32, fa.FEDAVG, stream=s)
+    torch.cuda.synchronize()
+    bad = sum(0 if torch.equal(o.view(torch.int32), ref.view(torch.int32)) else 1 for o in outs)
+    print(json.dumps({"dyn": int(os.environ.get("FA_PHASED_DYN", "0")), "cases": results,
+                      "streams": {"launches": len(streams), "mismatched_outputs": bad,
+                                  "dyn_launches": fa.diag_dyn_launches() - d0}}))
 
 
 if __name__ == "__main__":

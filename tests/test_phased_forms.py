@@ -2,7 +2,8 @@
 for bit) and the oracle (sampled elements), at one row per workgroup, the measured size, every LDS row of a
 phase in the pool and more rows than a phase holds.  Shapes: multi-phase f32 buckets, LDS-only and near-empty
 remainders, 1 to 64 clients, a sized phase, a d_init continuation, and bf16 buckets of the 512-thread form
-(tests/phased_child.py).  Each setting runs in its own child process (the knobs are read once per process),
+(tests/phased_child.py); and 52 launches at once on as many streams, beyond the 48 stream-owned counter slots.
+Each setting runs in its own child process (the knobs are read once per process),
 one after another."""
 import json
 import os
@@ -25,11 +26,15 @@ def run_child(env_extra):
     for c in res["cases"]:
         assert c["same_bits"], c
         assert c["oracle_sampled_ok"] in (None, True), c
-    return res["cases"]
+    assert res["streams"]["mismatched_outputs"] == 0, res["streams"]
+    return res
 
 
 @pytest.mark.parametrize("dyn", [1, 8, 38, 200])
 def test_dyn_pool_same_bits(dyn):
-    for c in run_child({"FA_PHASED_DYN": str(dyn)}):
+    res = run_child({"FA_PHASED_DYN": str(dyn)})
+    for c in res["cases"]:
         if not c["bf16"]:  # the f32 form has a dynamic instantiation: it must be what ran
             assert c["dyn_launches"] >= 1, c
+    # concurrent launches on 52 streams: the streams that got a counter slot of their own took the dynamic form
+    assert res["streams"]["dyn_launches"] >= 1, res["streams"]
