@@ -93,7 +93,6 @@ def lib():
         "fa_diag_rs_plan": (I, [S, I, I, I, I, I, I, ctypes.POINTER(I), ctypes.POINTER(I),
                                 ctypes.POINTER(ctypes.c_longlong)]),
         "fa_diag_pieces": (I, [S, I, I, ctypes.POINTER(I), ctypes.POINTER(S)]),
-        "fa_diag_dyn_launches": (ctypes.c_longlong, []),
         "fa_set_tuning": (I, [ctypes.POINTER(_Tuning)]),
         "fa_get_tuning": (I, [ctypes.POINTER(_Tuning)]),
     }
@@ -167,11 +166,6 @@ def sync_device(clients, weights, n, dtype, stream=None, gpu=0, ctx=None):
 
 def fill_uniform(dst, n, dtype, seed, client, idx0=0, stream=None):
     check(lib().fa_fill_uniform(_addr(dst), n, dtype, seed, client, idx0, _stream(stream)))
-
-
-def diag_dyn_launches():
-    """fa_diag_dyn_launches (diagnostic): phased launches this process ran in the dynamic form (FA_PHASED_DYN)."""
-    return int(lib().fa_diag_dyn_launches())
 
 
 def diag_read_stream(buffers, n, stream=None):

@@ -1770,10 +1770,6 @@ extern "C" int fa_diag_phased_timeline(int device, unsigned long long* out, int 
     return out && cap > 0 ? fa::phased_timeline(device, out, cap) : -1;
 }
 
-// Diagnostic, not part of the ABI in fa.h: phased launches enqueued in the dynamic form (FA_PHASED_DYN) by
-// this process so far -- the parity tests check that the form they compare actually ran.
-extern "C" long long fa_diag_dyn_launches(void) { return (long long)fa::dyn_launches(); }
-
 // Diagnostic, not part of the ABI in fa.h: the kernel plan (fa::plan_chain) of one FedAvg chain launch of n
 // elements (16-byte aligned) and nc clients under fa_tuning.walk `walk` (0 = the process default) on a chip of
 // `cus` CUs: *kind 0 one-shot grid, 1 one element per lane, 2 phased persistent grid of *phases phases (more

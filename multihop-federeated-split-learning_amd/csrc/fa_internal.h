@@ -84,8 +84,6 @@ hipError_t launch_segargs(const SegArgs& a, fa_dtype in, fa_dtype out, int max_n
 bool phased_takes(fa_dtype in, fa_dtype out, int64_t nvec, int nc, const Tuning& tu);
 hipError_t launch_fill(void* dst, int64_t n, fa_dtype dt, uint64_t seed, uint32_t client, uint64_t idx0,
                        hipStream_t s);
-// Phased launches enqueued in the dynamic form (FA_PHASED_DYN) so far.
-uint64_t dyn_launches();
 // Read-stream probe over nc f32 buffers of nvec 16-byte vectors (16-byte aligned); nothing is written.
 hipError_t launch_read_probe(const ClientTable& t, int nc, int64_t nvec, float* sink, hipStream_t s);
 

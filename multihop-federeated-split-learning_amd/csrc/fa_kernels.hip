@@ -390,34 +390,16 @@ __device__ __forceinline__ void put_bf16_bits(const ClientTable& t, int nc, void
     }
 }
 
-// The dynamic row pool (DYN form, round 3).  A phase's LDS part is G * rl rows of T vectors (4 KiB of every
-// client bucket per row for f32).  Each workgroup reduces rl - dyn_p of them at fixed places (static rows),
-// then its register chunk, then claims rows of the phase's pool (dyn_p * G rows) one at a time from a
-// per-phase counter until the pool is empty: workgroups that read faster take more rows, so all of them
-// reach the meeting within about one row's time of each other instead of the 4-6% spread of a static split
-// (the per-CU read rates differ from CU to CU and launch to launch).  A claimed row is read by
-// the whole workgroup at once (its 4 waves take its 4 consecutive KiB, as a static row), so every client's
-// 4 KiB block is still fetched in one burst.  Claimed rows go to the free LDS slots (the form gives one slot
-// to the claim broadcast); a workgroup whose slots are full writes further rows straight to the output.
-// Which workgroup reduces which row changes, never the chain of an element: same bits.  The counters are
-// per (counter slot, ring entry, phase); the last workgroup of a launch to leave zeroes its entry's.  A graph
-// that captured a dynamic-form launch keeps its capture stream's slot, so its replays must not overlap
-// launches of that stream (replays on the capture stream are serialized with them).  Off by default (§4 of
-// same speed as the static form).
-constexpr int kDynPhases = 64;  // phases of one launch that have a pool; later ones are all static rows
-
-template <typename IN, typename OUT, bool INIT, int REGS, bool SYNC, int TH, bool DYN = false>
+template <typename IN, typename OUT, bool INIT, int REGS, bool SYNC, int TH>
 __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, int nc, const float* init,
                                                                        void* out, int64_t head, int64_t nvec, int64_t n,
                                                                        unsigned* sync, int slack, int rl_last,
                                                                        int skew, int skew_last, int last_meet,
-                                                                       unsigned long long* tl, unsigned* claims,
-                                                                       int dyn_p) {
+                                                                       unsigned long long* tl) {
     constexpr int V = In<IN>::kVec, T = TH, RL = Phased<IN, REGS, TH, OUT>::RL, RR = Phased<IN, REGS, TH, OUT>::RR;
     constexpr int U = TH > 256 ? 8 : 16;  // loads in flight per wave (2 waves per SIMD at 512 threads)
     constexpr bool kPacked = std::is_same<LdsT<OUT>, uint16_t>::value;  // LDS rows hold bf16 output bits
-    constexpr int RLS = DYN ? RL - 1 : RL;  // LDS row slots (the dynamic form: one row's room for its claim words)
-    __shared__ LdsT<OUT> buf[RLS * T * V + (DYN ? 16 : 0)];
+    __shared__ LdsT<OUT> buf[RL * T * V];
     // thread 0 takes the ticket; its value is first needed at the phase-0 meeting, so the atomic's
     // latency hides under the phase's loads
     unsigned long long ticket = 0;
@@ -466,118 +448,6 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
     };
     for (int p = 0; p < phases; ++p) {
         const bool last = p == phases - 1;
-        if constexpr (DYN) {
-            // rows per workgroup of this phase's LDS part (a full phase: RL - skew / 2, the static form's
-            // average), static_rows of them at fixed places, the rest of the part in the pool
-            const int rl_p = last ? rl_last : RL - skew / 2;
-            const int static_rows = (dyn_p > 0 && p < kDynPhases) ? max(0, rl_p - dyn_p) : rl_p;
-            const int pool = (rl_p - static_rows) * (int)G;
-            const int64_t p0 = (int64_t)p * per_phase + threadIdx.x;
-#pragma unroll 1
-            for (int i = 0; i < static_rows; ++i) {
-                const int64_t v = p0 + ((int64_t)i * G + blockIdx.x) * T;
-                if (v < nvec) {
-                    float acc[V];
-                    chain_vec<IN, U, true, INIT>(t, nc, init, head + v * V, acc);
-                    if constexpr (kPacked) pack_bf16<V>(reinterpret_cast<uint16_t*>(&buf[(i * T + threadIdx.x) * V]), acc);
-                    else {
-#pragma unroll
-                        for (int j = 0; j < V; ++j) buf[(i * T + threadIdx.x) * V + j] = acc[j];
-                    }
-                }
-            }
-            if (my_tl && p == 0) {
-                __syncthreads();
-                if (threadIdx.x == 0) my_tl[7] = (unsigned long long)wall_clock64();
-            }
-            const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-            const int64_t c0 = (int64_t)p * per_phase + (int64_t)rl_p * G * T + ((int64_t)blockIdx.x * (T / 64) + wave) * RR * 64;
-            float keep[RR][V];
-            const bool staged = stage_regs<IN, INIT, RR, U>(t, nc, init, head, c0, nvec, keep);
-            if (!staged) {
-                for (int r = 0; r < RR; ++r) {
-                    const int64_t v = c0 + r * 64 + (threadIdx.x & 63);
-                    if (v < nvec) {
-                        float acc[V];
-                        chain_vec<IN, U, true, INIT>(t, nc, init, head + v * V, acc);
-                        put<OUT, V, SYNC>(t, nc, out, head + v * V, acc);
-                    }
-                }
-            }
-            // the pool: thread 0 claims the next row while the workgroup reduces the current one
-            const int lane = threadIdx.x & 63;
-            int taken = 0, ids = 0;  // lane j of every wave: the pool row in LDS slot static_rows + j
-            if (pool > 0) {
-                int* ctl = reinterpret_cast<int*>(&buf[RLS * T * V]);
-                unsigned* ctr = nullptr;
-                if (threadIdx.x == 0) {
-                    ctr = claims + (size_t)((ticket / (unsigned long long)G) % kSyncRing) * kDynPhases + p;
-                    ctl[0] = (int)__hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                __syncthreads();
-                int c = __builtin_amdgcn_readfirstlane(ctl[0]);
-                int par = 1;
-                while (c < pool) {
-                    int nxt = 0;
-                    if (threadIdx.x == 0)
-                        nxt = (int)__hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const int64_t v = p0 + ((int64_t)static_rows * G + c) * T;
-                    if (v < nvec) {
-                        float acc[V];
-                        chain_vec<IN, U, true, INIT>(t, nc, init, head + v * V, acc);
-                        if (taken < RLS - static_rows) {
-                            const int i = static_rows + taken;
-                            if constexpr (kPacked) pack_bf16<V>(reinterpret_cast<uint16_t*>(&buf[(i * T + threadIdx.x) * V]), acc);
-                            else {
-#pragma unroll
-                                for (int j = 0; j < V; ++j) buf[(i * T + threadIdx.x) * V + j] = acc[j];
-                            }
-                        } else {
-                            put<OUT, V, SYNC>(t, nc, out, head + v * V, acc);  // no slot left: straight out
-                        }
-                    }
-                    if (lane == taken) ids = c;
-                    ++taken;
-                    if (threadIdx.x == 0) ctl[par] = nxt;
-                    __syncthreads();
-                    c = __builtin_amdgcn_readfirstlane(ctl[par]);
-                    par ^= 1;
-                }
-            }
-            if (!last || last_meet) meet(p);
-            else __syncthreads();
-#pragma unroll 1
-            for (int i = 0; i < static_rows; ++i) {
-                const int64_t v = p0 + ((int64_t)i * G + blockIdx.x) * T;
-                if (v < nvec) {
-                    if constexpr (kPacked)
-                        put_bf16_bits<V, SYNC>(t, nc, out, head + v * V,
-                                               reinterpret_cast<const uint16_t*>(&buf[(i * T + threadIdx.x) * V]));
-                    else
-                        put<OUT, V, SYNC>(t, nc, out, head + v * V, reinterpret_cast<const float*>(&buf[(i * T + threadIdx.x) * V]));
-                }
-            }
-            const int kept = min(taken, RLS - static_rows);
-#pragma unroll 1
-            for (int j = 0; j < kept; ++j) {
-                const int c = __builtin_amdgcn_readlane(ids, j);
-                const int64_t v = p0 + ((int64_t)static_rows * G + c) * T;
-                const int i = static_rows + j;
-                if (v < nvec) {
-                    if constexpr (kPacked)
-                        put_bf16_bits<V, SYNC>(t, nc, out, head + v * V,
-                                               reinterpret_cast<const uint16_t*>(&buf[(i * T + threadIdx.x) * V]));
-                    else
-                        put<OUT, V, SYNC>(t, nc, out, head + v * V, reinterpret_cast<const float*>(&buf[(i * T + threadIdx.x) * V]));
-                }
-            }
-            if (staged) {
-                const int64_t c = c0 + lane;
-#pragma unroll
-                for (int r = 0; r < RR; ++r) put<OUT, V, SYNC>(t, nc, out, head + (c + r * 64) * V, keep[r]);
-            }
-            continue;
-        }
         // LDS vectors per lane in this phase: r_all rows every workgroup takes, then r_even more that only
         // the even XCDs' take.  Full phases: RL - skew and skew; the last phase is balanced by the host
         // (rl_last per lane on average, registers first: phased_rl_last)
@@ -654,10 +524,6 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
             (unsigned)G - 1) {
             __hip_atomic_store(sync + 4 + e, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(sync + 4 + kSyncRing + e, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if constexpr (DYN) {  // every workgroup has left: no claim of this launch is still in flight
-                for (int p = 0; p < min(phases, kDynPhases); ++p)
-                    __hip_atomic_store(claims + (size_t)e * kDynPhases + p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
         }
     }
 }
@@ -938,16 +804,14 @@ hipError_t launch_chain_lnt(const ClientTable& t, int nc, const float* init, voi
 // slots (ticket + ring, fedavg_phased_kernel), one picked per stream, 256 B apart.
 constexpr int kMaxDevices = 64, kSyncSlots = 64, kSyncStride = 64;
 static_assert(4 + 2 * kSyncRing <= kSyncStride, "a counter slot holds the ticket and both rings");
-// Counter slots [0, kOwnedSlots) belong to one stream each (first come, for the life of the process): launches
-// on one stream are serialized, so every epoch of such a slot is exactly one launch -- what the dynamic form's
-// claim counters need (two launches sharing a counter would skip rows).  Further streams share the hashed
-// slots [kOwnedSlots, kSyncSlots) and take the static form.
+// Counter slots [0, kOwnedSlots) belong to one stream each (first come, for the life of the process), so
+// launches on two streams never mix their workgroups in one epoch; further streams share the hashed slots
+// [kOwnedSlots, kSyncSlots) (speed only, never results: see the ring above).
 constexpr int kOwnedSlots = 48;
 struct PhasedDevice {
     std::once_flag once;
     int cus = 0;
     unsigned* sync = nullptr;  // kSyncSlots slots, kSyncStride words apart
-    unsigned* claims = nullptr;  // kOwnedSlots x kSyncRing x kDynPhases claim counters of the dynamic form
     unsigned long long* tl = nullptr;  // FA_TIMELINE=1: the last phased launch's per-workgroup timeline
     std::mutex mu;
     hipStream_t owner[kOwnedSlots] = {};
@@ -974,18 +838,12 @@ PhasedDevice* phased_device() {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return;
         const size_t words = (size_t)kSyncStride * kSyncSlots;
         if (hipMalloc((void**)&p, sizeof(unsigned) * words) != hipSuccess) return;
-        unsigned* cl = nullptr;
-        const size_t cwords = (size_t)kOwnedSlots * kSyncRing * kDynPhases;
-        if (hipMalloc((void**)&cl, sizeof(unsigned) * cwords) != hipSuccess) cl = nullptr;
-        if (hipMemset(p, 0, sizeof(unsigned) * words) != hipSuccess ||
-            (cl && hipMemset(cl, 0, sizeof(unsigned) * cwords) != hipSuccess) || hipDeviceSynchronize() != hipSuccess) {
+        if (hipMemset(p, 0, sizeof(unsigned) * words) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
             (void)hipFree(p);
-            if (cl) (void)hipFree(cl);
             return;
         }
         d.cus = cus;
         d.sync = p;
-        d.claims = cl;
         const char* e = std::getenv("FA_TIMELINE");
         if (e && std::atoi(e) > 0 && hipMalloc((void**)&d.tl, sizeof(unsigned long long) * 8 * cus) == hipSuccess)
             (void)hipMemset(d.tl, 0, sizeof(unsigned long long) * 8 * cus);
@@ -1011,39 +869,20 @@ inline int phased_rl_last(int64_t rem, int64_t lanes, int RL, int RR) {
 // 5.30, one rank's share at 2 GPUs 0.668-0.673 against 0.677-0.684; gpurun_out r02s25-s26); more loses
 // again.  None in the 512-thread bf16 form: with fp32 rows (10) no step was small enough (C3: 1 row
 // 0.425-0.427 ms against 0.424, 4 rows 0.444-0.449; r02s26-s27), and its bf16 rows (20) keep none either.  FA_PHASED_SKEW overrides it (below RL / 2).
-std::atomic<uint64_t> g_dyn_launches{0};
-
-// FA_PHASED_DYN = rows per workgroup in every phase's dynamic pool (0: the static form).
-int phased_dyn_rows() {
-    static const int v = [] {
-        const char* e = std::getenv("FA_PHASED_DYN");
-        return e ? std::max(0, std::atoi(e)) : 0;
-    }();
-    return v;
-}
-// The instantiations built in the dynamic form: the f32 forms of walk 5 (the north star, C4, C5).
-template <typename IN, typename OUT, int REGS, int TH>
-struct HasDyn : std::integral_constant<bool, std::is_same<IN, float>::value && std::is_same<OUT, float>::value &&
-                                                 REGS == 192 && TH == 256> {};
-
 int phased_skew(int RL) {
     static const int v = [] {
         const char* e = std::getenv("FA_PHASED_SKEW");
         return e ? std::max(0, std::atoi(e)) : -1;
     }();
-    const int s = std::min(v >= 0 ? v : RL >= 40 ? RL / 10 : 0, RL / 2 - 1);  // the bf16 form (20 rows): none
-    return phased_dyn_rows() > 0 ? s & ~1 : s;  // the dynamic form's phase is RL - skew / 2 rows: even skews only
+    return std::min(v >= 0 ? v : RL >= 40 ? RL / 10 : 0, RL / 2 - 1);  // the bf16 form (20 rows): none
 }
 
-// Enqueue one phased launch on stream s, on the stream's counter slot.  dyn_kern (may be null): the dynamic
-// form of the same instantiation, taken when FA_PHASED_DYN > 0 and the slot is the stream's alone.
+// Enqueue one phased launch on stream s, on the stream's counter slot.
 template <typename Kern>
-hipError_t phased_enqueue(PhasedDevice* d, Kern kern, Kern dyn_kern, int th, int RL, int RR, hipStream_t s,
-                          const ClientTable& t, int nc, const float* init, void* out, int64_t head, int64_t nvec,
-                          int64_t n) {
+hipError_t phased_enqueue(PhasedDevice* d, Kern kern, int th, int RL, int RR, hipStream_t s, const ClientTable& t,
+                          int nc, const float* init, void* out, int64_t head, int64_t nvec, int64_t n) {
     bool own = false;
     const int slot = d->slot_of(s, &own);
-    const int dyn = dyn_kern && own && d->claims ? phased_dyn_rows() : 0;
     const int slack = d->cus / 32;  // the write part starts once all but ~3% of the workgroups have arrived
     const int64_t lanes = (int64_t)d->cus * th;
     // the skew follows the whole chip's round-robin of workgroups over its 8 XCDs (blockIdx parity = XCD
@@ -1051,9 +890,8 @@ hipError_t phased_enqueue(PhasedDevice* d, Kern kern, Kern dyn_kern, int th, int
     const int skew = d->cus >= 256 && d->cus % 16 == 0 ? phased_skew(RL) : 0;
     const int64_t per_phase = lanes * (RL + RR) - (int64_t)(d->cus / 2) * th * skew;
     const int64_t phases = (nvec + per_phase - 1) / per_phase;
-    // the dynamic form: every phase's LDS part averages RL - skew / 2 rows, none skewed
-    const int rl_last = phased_rl_last(nvec - (phases - 1) * per_phase, lanes, dyn ? RL - skew / 2 : RL, RR);
-    const int skew_last = dyn ? 0 : std::min({(skew + 1) / 2, rl_last, RL - rl_last});
+    const int rl_last = phased_rl_last(nvec - (phases - 1) * per_phase, lanes, RL, RR);
+    const int skew_last = std::min({(skew + 1) / 2, rl_last, RL - rl_last});
     // The last phase writes without the meeting: each workgroup as soon as it has read its share, beside
     // the slower workgroups' last reads (one rank's share at 2 / 4 / 8 GPUs 0.664 / 0.344 / 0.173 ms
     // against 0.670 / 0.346 / 0.176 with the meeting, north star, C3 and C4 unchanged; gpurun_out r02s36).
@@ -1064,10 +902,8 @@ hipError_t phased_enqueue(PhasedDevice* d, Kern kern, Kern dyn_kern, int th, int
     }();
     // FA_TIMELINE: a launch without meetings leaves their stamps alone, so clear the previous launch's
     if (d->tl) (void)hipMemsetAsync(d->tl, 0, sizeof(unsigned long long) * 8 * d->cus, s);
-    if (dyn) g_dyn_launches.fetch_add(1, std::memory_order_relaxed);
-    hipLaunchKernelGGL(dyn ? dyn_kern : kern, dim3((unsigned)d->cus), dim3(th), 0, s, t, nc, init, out, head, nvec, n,
-                       d->sync + slot * kSyncStride, slack, rl_last, skew, skew_last, last_meet, d->tl,
-                       dyn ? d->claims + (size_t)slot * kSyncRing * kDynPhases : nullptr, dyn);
+    hipLaunchKernelGGL(kern, dim3((unsigned)d->cus), dim3(th), 0, s, t, nc, init, out, head, nvec, n,
+                       d->sync + slot * kSyncStride, slack, rl_last, skew, skew_last, last_meet, d->tl);
     return hipGetLastError();
 }
 
@@ -1089,18 +925,10 @@ template <typename IN, typename OUT, int REGS, int TH>
 hipError_t launch_phased_r(PhasedDevice* d, const ClientTable& t, int nc, const float* init, void* out, int64_t head,
                            int64_t nvec, int64_t n, hipStream_t s) {
     constexpr int RL = Phased<IN, REGS, TH, OUT>::RL, RR = Phased<IN, REGS, TH, OUT>::RR;
-    static std::atomic<int> occ[4] = {-1, -1, -1, -1};  // per INIT variant, static and dynamic form
+    static std::atomic<int> occ[2] = {-1, -1};  // per INIT variant
     auto kern = init ? fedavg_phased_kernel<IN, OUT, true, REGS, false, TH> : fedavg_phased_kernel<IN, OUT, false, REGS, false, TH>;
     if (!phased_fits(occ[init ? 1 : 0], kern, TH)) return hipErrorNotSupported;
-    decltype(kern) dyn_kern = nullptr;
-    if constexpr (HasDyn<IN, OUT, REGS, TH>::value) {
-        if (phased_dyn_rows() > 0) {
-            dyn_kern = init ? fedavg_phased_kernel<IN, OUT, true, REGS, false, TH, true>
-                            : fedavg_phased_kernel<IN, OUT, false, REGS, false, TH, true>;
-            if (!phased_fits(occ[init ? 3 : 2], dyn_kern, TH)) dyn_kern = nullptr;
-        }
-    }
-    return phased_enqueue(d, kern, dyn_kern, TH, RL, RR, s, t, nc, init, out, head, nvec, n);
+    return phased_enqueue(d, kern, TH, RL, RR, s, t, nc, init, out, head, nvec, n);
 }
 
 // Clients from which a bucket smaller than one phase takes a phase sized to it (plan_chain); fewer
@@ -1222,8 +1050,6 @@ ChainPlan plan_chain(fa_dtype in, fa_dtype out, int64_t nvec, int nc, bool vecto
     return ChainPlan{kPlanPhased, regs, th, (nvec + per_phase - 1) / per_phase};
 }
 
-uint64_t dyn_launches() { return g_dyn_launches.load(std::memory_order_relaxed); }
-
 hipError_t phased_timeouts(int dev, uint64_t* count) {
     *count = 0;
     if (dev < 0 || dev >= kMaxDevices || !g_phased[dev].sync) return hipSuccess;  // no phased launch yet
@@ -1314,7 +1140,7 @@ hipError_t launch_sync_phased_r(const ClientTable& t, int nc, int64_t head, int6
     static std::atomic<int> occ{-1};
     auto kern = fedavg_phased_kernel<T, T, false, REGS, true, TH>;
     if (!phased_fits(occ, kern, TH)) return hipErrorNotSupported;
-    return phased_enqueue(d, kern, (decltype(kern))nullptr, TH, RL, RR, s, t, nc,
+    return phased_enqueue(d, kern, TH, RL, RR, s, t, nc,
                           (const float*)nullptr, (void*)nullptr, head, nvec, n);
 }
 
