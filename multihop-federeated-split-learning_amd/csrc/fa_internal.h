@@ -64,7 +64,6 @@ enum { kPlanOneShot = 0, kPlanScalar = 1, kPlanPhased = 2 };
 struct ChainPlan {
     int kind, regs, threads;
     int64_t phases;
-    int rows = 0;  // > 0: bf16 in and out, a register stage of `rows` packed bf16 rows per lane (regs 0)
 };
 // cus: the device's CU count (0 = no phased kernel).
 ChainPlan plan_chain(fa_dtype in, fa_dtype out, int64_t nvec, int nc, bool vector_ok, const Tuning& tu, int cus);

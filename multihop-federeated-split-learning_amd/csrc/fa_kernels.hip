@@ -276,10 +276,6 @@ constexpr int kSyncRing = 8;
 // instead of 23.1 M).
 template <typename OUT> using LdsT = typename std::conditional<std::is_same<OUT, uint16_t>::value, uint16_t, float>::type;
 
-// Packed register rows per lane of the bf16 -> bf16 RW form (fedavg_phased_kernel): with the 20 bf16 LDS rows
-// of the 512-thread form, 52 vectors per lane -- a phase of 54.5 M elements (C3's 42.7 M in one).
-constexpr int kBf16Rows = 32;
-
 template <typename IN, int REGS, int TH = kPhasedThreads, typename OUT = float>
 struct Phased {  // vectors per lane per phase: LDS (160 KiB per workgroup) + registers
     static constexpr int V = In<IN>::kVec;
@@ -394,21 +390,15 @@ __device__ __forceinline__ void put_bf16_bits(const ClientTable& t, int nc, void
     }
 }
 
-// RW > 0 (bf16 in and out, REGS 0): the register stage holds RW finished rows per lane as packed bf16 bits
-// (4 registers per 8 elements; a row is reduced like an LDS row -- one vector's chain at a time -- and packed
-// once done), instead of RR vectors of fp32 accumulators that the loop-swapped stage keeps live together (8
-// registers per 8 elements).  Register rows j < rw of a phase: block (lds_rows + j G + b) of T vectors, after
-// the LDS part; rw = RW in a full phase, rw_last in the last.
-template <typename IN, typename OUT, bool INIT, int REGS, bool SYNC, int TH, int RW = 0>
+template <typename IN, typename OUT, bool INIT, int REGS, bool SYNC, int TH>
 __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, int nc, const float* init,
                                                                        void* out, int64_t head, int64_t nvec, int64_t n,
                                                                        unsigned* sync, int slack, int rl_last,
                                                                        int skew, int skew_last, int last_meet,
-                                                                       unsigned long long* tl, int rw_last) {
+                                                                       unsigned long long* tl) {
     constexpr int V = In<IN>::kVec, T = TH, RL = Phased<IN, REGS, TH, OUT>::RL, RR = Phased<IN, REGS, TH, OUT>::RR;
     constexpr int U = TH > 256 ? 8 : 16;  // loads in flight per wave (2 waves per SIMD at 512 threads)
     constexpr bool kPacked = std::is_same<LdsT<OUT>, uint16_t>::value;  // LDS rows hold bf16 output bits
-    static_assert(RW == 0 || (kPacked && V == 8 && RR == 0 && !SYNC), "packed register rows: bf16 in and out, no fp32 stage");
     __shared__ LdsT<OUT> buf[RL * T * V];
     // thread 0 takes the ticket; its value is first needed at the phase-0 meeting, so the atomic's
     // latency hides under the phase's loads
@@ -427,7 +417,7 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
     // skew: the workgroups of the odd XCDs (blockIdx odd; blocks are dealt round-robin over the 8 XCDs)
     // take `skew` fewer LDS rows than the even ones in every full phase, and 2 skew_last fewer in the last
     // (rl_last - skew_last against rl_last + skew_last) -- those XCDs read 5-10% slower (tools/timeline.py)
-    const int64_t per_phase = G * T * (RL + RR + RW) - (G / 2) * T * skew;
+    const int64_t per_phase = G * T * (RL + RR) - (G / 2) * T * skew;
     const int phases = (int)((nvec + per_phase - 1) / per_phase);
     const bool odd = blockIdx.x & 1;
     // the meeting before phase p's writes: every workgroup's reads of the phase are done (all but `slack`)
@@ -489,36 +479,12 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
             __syncthreads();
             if (threadIdx.x == 0) my_tl[7] = (unsigned long long)wall_clock64();
         }
-        // packed register rows (RW form)
-        const int rw = RW > 0 ? (last ? rw_last : RW) : 0;
-        u32x4 packed[RW > 0 ? RW : 1];  // RW > 0 only
-        // rows reduced one at a time (a runtime loop: the chain's client loop inside it must not be unrolled 32
-        // times -- the kernel-argument client table then went to scratch), each packed row shifted into a register
-        // queue with constant indices: after rw rows, row j sits in packed[RW - rw + j]
-        const int64_t rv0 = p0 + (lds_rows + blockIdx.x) * T;
-        if constexpr (RW > 0) {
-#pragma unroll 1
-            for (int j = 0; j < rw; ++j) {
-                const int64_t v = rv0 + (int64_t)j * G * T;
-                u32x4 row = {0u, 0u, 0u, 0u};
-                if (v < nvec) {
-                    float acc[V];
-                    chain_vec<IN, U, true, INIT>(t, nc, init, head + v * V, acc);
-                    row = u32x4{f32_to_bf16(acc[0]) | (f32_to_bf16(acc[1]) << 16), f32_to_bf16(acc[2]) | (f32_to_bf16(acc[3]) << 16),
-                                f32_to_bf16(acc[4]) | (f32_to_bf16(acc[5]) << 16), f32_to_bf16(acc[6]) | (f32_to_bf16(acc[7]) << 16)};
-                }
-#pragma unroll
-                for (int i = 0; i + 1 < RW; ++i) packed[i] = packed[i + 1];
-                packed[RW - 1] = row;
-            }
-        }
         // register part: this wave's contiguous chunk after the phase's LDS part
         const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
         const int64_t c0 = (int64_t)p * per_phase + lds_rows * T + ((int64_t)blockIdx.x * (T / 64) + wave) * RR * 64;
-        float keep[RR > 0 ? RR : 1][V];
-        bool staged = false;
-        if constexpr (RR > 0) staged = stage_regs<IN, INIT, RR, U>(t, nc, init, head, c0, nvec, keep);
-        if (RR > 0 && !staged) {  // the chunk that holds the end of the bucket (or lies past it): no staging
+        float keep[RR][V];
+        const bool staged = stage_regs<IN, INIT, RR, U>(t, nc, init, head, c0, nvec, keep);
+        if (!staged) {  // the chunk that holds the end of the bucket (or lies past it): no staging
             for (int r = 0; r < RR; ++r) {
                 const int64_t v = c0 + r * 64 + (threadIdx.x & 63);
                 if (v < nvec) {
@@ -539,14 +505,6 @@ __global__ __launch_bounds__(TH) void fedavg_phased_kernel(const ClientTable t, 
                                            reinterpret_cast<const uint16_t*>(&buf[(i * T + threadIdx.x) * V]));
                 else
                     put<OUT, V, SYNC>(t, nc, out, head + v * V, reinterpret_cast<const float*>(&buf[(i * T + threadIdx.x) * V]));
-            }
-        }
-        if constexpr (RW > 0) {
-#pragma unroll
-            for (int i = 0; i < RW; ++i) {
-                const int j = i - (RW - rw);  // the register row packed[i] holds, if any
-                const int64_t v = rv0 + (int64_t)j * G * T;
-                if (j >= 0 && v < nvec) st16<kStSc1>(reinterpret_cast<uint16_t*>(out) + head + v * V, packed[i]);
             }
         }
         if (staged) {
@@ -922,7 +880,7 @@ int phased_skew(int RL) {
 // Enqueue one phased launch on stream s, on the stream's counter slot.
 template <typename Kern>
 hipError_t phased_enqueue(PhasedDevice* d, Kern kern, int th, int RL, int RR, hipStream_t s, const ClientTable& t,
-                          int nc, const float* init, void* out, int64_t head, int64_t nvec, int64_t n, int RW = 0) {
+                          int nc, const float* init, void* out, int64_t head, int64_t nvec, int64_t n) {
     bool own = false;
     const int slot = d->slot_of(s, &own);
     const int slack = d->cus / 32;  // the write part starts once all but ~3% of the workgroups have arrived
@@ -930,13 +888,9 @@ hipError_t phased_enqueue(PhasedDevice* d, Kern kern, int th, int RL, int RR, hi
     // the skew follows the whole chip's round-robin of workgroups over its 8 XCDs (blockIdx parity = XCD
     // parity); a partition of the chip (fewer CUs per device) keeps the plain layout
     const int skew = d->cus >= 256 && d->cus % 16 == 0 ? phased_skew(RL) : 0;
-    const int64_t per_phase = lanes * (RL + RR + RW) - (int64_t)(d->cus / 2) * th * skew;
+    const int64_t per_phase = lanes * (RL + RR) - (int64_t)(d->cus / 2) * th * skew;
     const int64_t phases = (nvec + per_phase - 1) / per_phase;
-    const int64_t rem = nvec - (phases - 1) * per_phase;
-    // packed register rows (RW form): q vectors per lane in the last phase, LDS rows first
-    const int64_t q = (rem + lanes - 1) / lanes;
-    const int rl_last = RW > 0 ? (int)std::min<int64_t>(q, RL) : phased_rl_last(rem, lanes, RL, RR);
-    const int rw_last = RW > 0 ? (int)(q - rl_last) : 0;
+    const int rl_last = phased_rl_last(nvec - (phases - 1) * per_phase, lanes, RL, RR);
     const int skew_last = std::min({(skew + 1) / 2, rl_last, RL - rl_last});
     // The last phase writes without the meeting: each workgroup as soon as it has read its share, beside
     // the slower workgroups' last reads (one rank's share at 2 / 4 / 8 GPUs 0.664 / 0.344 / 0.173 ms
@@ -949,7 +903,7 @@ hipError_t phased_enqueue(PhasedDevice* d, Kern kern, int th, int RL, int RR, hi
     // FA_TIMELINE: a launch without meetings leaves their stamps alone, so clear the previous launch's
     if (d->tl) (void)hipMemsetAsync(d->tl, 0, sizeof(unsigned long long) * 8 * d->cus, s);
     hipLaunchKernelGGL(kern, dim3((unsigned)d->cus), dim3(th), 0, s, t, nc, init, out, head, nvec, n,
-                       d->sync + slot * kSyncStride, slack, rl_last, skew, skew_last, last_meet, d->tl, rw_last);
+                       d->sync + slot * kSyncStride, slack, rl_last, skew, skew_last, last_meet, d->tl);
     return hipGetLastError();
 }
 
@@ -967,15 +921,14 @@ bool phased_fits(std::atomic<int>& occ, Kern kern, int th) {
 // The phased kernel launch of one instantiation (the plan, below, chose it and the bucket's size): one
 // workgroup per CU, all co-resident -- hipErrorNotSupported if not even one fits (the caller then takes the
 // one-shot grid).
-template <typename IN, typename OUT, int REGS, int TH, int RW = 0>
+template <typename IN, typename OUT, int REGS, int TH>
 hipError_t launch_phased_r(PhasedDevice* d, const ClientTable& t, int nc, const float* init, void* out, int64_t head,
                            int64_t nvec, int64_t n, hipStream_t s) {
     constexpr int RL = Phased<IN, REGS, TH, OUT>::RL, RR = Phased<IN, REGS, TH, OUT>::RR;
     static std::atomic<int> occ[2] = {-1, -1};  // per INIT variant
-    auto kern = init ? fedavg_phased_kernel<IN, OUT, true, REGS, false, TH, RW>
-                     : fedavg_phased_kernel<IN, OUT, false, REGS, false, TH, RW>;
+    auto kern = init ? fedavg_phased_kernel<IN, OUT, true, REGS, false, TH> : fedavg_phased_kernel<IN, OUT, false, REGS, false, TH>;
     if (!phased_fits(occ[init ? 1 : 0], kern, TH)) return hipErrorNotSupported;
-    return phased_enqueue(d, kern, TH, RL, RR, s, t, nc, init, out, head, nvec, n, RW);
+    return phased_enqueue(d, kern, TH, RL, RR, s, t, nc, init, out, head, nvec, n);
 }
 
 // Clients from which a bucket smaller than one phase takes a phase sized to it (plan_chain); fewer
@@ -985,15 +938,6 @@ int sized_min_clients() {
     static const int v = [] {
         const char* e = std::getenv("FA_SIZED_MIN_CLIENTS");
         return e ? std::atoi(e) : 16;
-    }();
-    return v;
-}
-
-// experiment knob: FA_BF16_ROWS=1 gives bf16 -> bf16 buckets the packed register-row form (kBf16Rows)
-bool bf16_rows_on() {
-    static const bool v = [] {
-        const char* e = std::getenv("FA_BF16_ROWS");
-        return e && std::atoi(e) > 0;
     }();
     return v;
 }
@@ -1016,9 +960,6 @@ template <typename IN, typename OUT>
 hipError_t launch_phased_plan(PhasedDevice* d, const ChainPlan& pl, const ClientTable& t, int nc, const float* init,
                               void* out, int64_t head, int64_t nvec, int64_t n, hipStream_t s) {
     constexpr bool bf = std::is_same<IN, uint16_t>::value;
-    if constexpr (bf && std::is_same<OUT, uint16_t>::value) {
-        if (pl.rows == kBf16Rows) return launch_phased_r<IN, OUT, 0, 512, kBf16Rows>(d, t, nc, init, out, head, nvec, n, s);
-    }
     switch (pl.threads * 1000 + pl.regs) {
         case 256128: return launch_phased_r<IN, OUT, 128, 256>(d, t, nc, init, out, head, nvec, n, s);
         case 512096: return launch_phased_r<IN, OUT, 96, 512>(d, t, nc, init, out, head, nvec, n, s);
@@ -1080,16 +1021,6 @@ ChainPlan plan_chain(fa_dtype in, fa_dtype out, int64_t nvec, int nc, bool vecto
     ChainPlan p{vector_ok ? kPlanOneShot : kPlanScalar, 0, 0, 0};
     if (!vector_ok || cus <= 0 || tu.walk < 3 || tu.walk > 5) return p;
     const bool bf = in == FA_BF16;
-    if (bf && out == FA_BF16 && tu.walk >= 4 && bf16_rows_on()) {  // the RW form: 20 LDS + 32 packed rows per lane
-        const int64_t lanes = (int64_t)cus * 512, per_phase = lanes * (20 + kBf16Rows);
-        const int64_t env = phased_min_vecs_env();
-        if (nvec < (env >= 0 ? env : per_phase)) {  // below one full phase: a phase sized to it, same rules
-            if (tu.walk != 4 || nc < sized_min_clients() || (nvec + lanes - 1) / lanes < 4) return p;
-        }
-        ChainPlan r{kPlanPhased, 0, 512, (nvec + per_phase - 1) / per_phase};
-        r.rows = kBf16Rows;
-        return r;
-    }
     const int V = bf ? 8 : 4;
     // walk 4 (fa_tuning.walk 5, the default): bf16 inputs take the 512-thread form (2 waves per SIMD hide
     // the widening VALU work of 8 elements per load: C3 0.430 vs 0.439 ms), f32 the 256-thread one (C4 5.43
