@@ -177,7 +177,9 @@ def traffic_from_profile(workload, n_gpus, strong_range=False):
     rec = d.get(workload)
     if not rec:
         return None, None
-    return rec.get("hbm_bytes_per_launch"), "%s, kernel %s" % (rec.get("source"), rec.get("kernel", "?").split("(")[0])
+    # per step (a step of C5's pieced layout is one launch per piece); older records hold one launch per step
+    return rec.get("hbm_bytes_per_step", rec.get("hbm_bytes_per_launch")), "%s, kernel %s" % (
+        rec.get("source"), rec.get("kernel", "?").split("(")[0])
 
 
 def under_profiler():

@@ -20,6 +20,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PER_LAUNCH_STEPS = 10  # bench.timed_loop(per_launch=10): steps timed one by one after the region
 
 
 def per_kernel(path, value_col=None, counter=None):
@@ -83,8 +84,17 @@ def main():
         wv = wg[fk]
         f_kib, w_kib = sum(fv) / len(fv), sum(wv) / len(wv)
         traffic = (2 * f_kib + w_kib) * 1024
+        # launches of the dominant kernel per bench step (C5's range pieces: one launch per piece): the pass ran
+        # warmup + steps timed steps + bench.timed_loop's per-launch loop (PER_LAUNCH_STEPS)
+        per_step = 1
+        bj = os.path.join(os.path.dirname(fetch), os.pardir, "pmc_%s_FETCH_SIZE.json" % workload)
+        if os.path.exists(bj) and os.path.getsize(bj):
+            line = json.loads(open(bj).read().strip().splitlines()[-1])
+            n_steps = int(line["warmup"]) + int(line["steps"]) + PER_LAUNCH_STEPS
+            per_step = max(1, round(len(fv) / n_steps))
         rec = {"kernel": fk[0], "grid": fk[1], "launches": len(fv), "FETCH_SIZE_KiB": f_kib,
-               "WRITE_SIZE_KiB": w_kib, "hbm_bytes_per_launch": round(traffic),
+               "WRITE_SIZE_KiB": w_kib, "hbm_bytes_per_launch": round(traffic), "launches_per_step": per_step,
+               "hbm_bytes_per_step": round(traffic * per_step),
                "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count correction)"}
         if workload == "northstar":
             summary["pmc"] = rec
@@ -92,7 +102,8 @@ def main():
             summary.setdefault("pmc_workloads", {})[workload] = rec
         tp = os.path.join(prof, "pmc_traffic.json")
         d = json.load(open(tp)) if os.path.exists(tp) else {}
-        d[workload] = {"hbm_bytes_per_launch": round(traffic), "kernel": fk[0], "grid": fk[1],
+        d[workload] = {"hbm_bytes_per_launch": round(traffic), "launches_per_step": per_step,
+                       "hbm_bytes_per_step": round(traffic * per_step), "kernel": fk[0], "grid": fk[1],
                        "FETCH_SIZE_KiB": f_kib, "WRITE_SIZE_KiB": w_kib, "round": rnd,
                        "source": "profiles/%s_summary.json (gpurun_out/%s)" % (rnd, os.path.basename(os.path.normpath(src)))}
         json.dump(d, open(tp, "w"), indent=1)
