@@ -78,12 +78,13 @@ def test_rs_layout_literal_and_errors(fa, O, torch_gpu):
 @pytest.mark.parametrize("G,D,chunks,bf16,out_bf16", [
     (2, 7, 8, False, False), (4, 7, 3, False, False), (3, 2, 5, False, False), (4, 9, 1, False, False),
     (2, 5, 4, True, False), (3, 6, 2, True, False), (3, 6, 2, True, True), (4, 7, 3, False, True)])
-def test_rs_layout_multi_gpu_tolerance(fa, O, torch_gpu, G, D, chunks, bf16, out_bf16):
+def test_rs_layout_multi_gpu_tolerance(fa, O, torch_gpu, record_property, G, D, chunks, bf16, out_bf16):
     """G shards: clients dealt to the GPUs (a GPU may hold none: D < G), every GPU's shard holds its
     cyclic blocks; the whole result within 1e-6 of sum_k |w_k x_k| of the oracle's ordered chain (the
     exchange adds per-GPU partials; bf16 inputs exchange fp32 partials too) -- for a bf16 output, plus
     the one bf16 rounding of that sum (half a bf16 ulp, 2^-8 relative); the device-resident round on the
-    same slots agrees bit for bit."""
+    same slots agrees bit for bit.  The largest error, relative to sum_k |w_k x_k| and as a fraction of the
+    bound, is reported ("parity by tolerance ... with the max error reported")."""
     n = 1_234_567
     w = O.weights(D)
     xs = host_clients(O, 71, D, n, bf16)
@@ -102,6 +103,19 @@ def test_rs_layout_multi_gpu_tolerance(fa, O, torch_gpu, G, D, chunks, bf16, out
     gotf = (O.bf16_to_f32(got) if out_bf16 else got).astype(np.float64)
     bound = 1e-6 * absw + (2.0 ** -8 * np.abs(ref.astype(np.float64)) if out_bf16 else 0.0) + 1e-30
     err = np.abs(gotf - ref) / bound
+    rel = float((np.abs(gotf - ref) / (absw + 1e-30)).max())
+    record_property("max_err_rel_to_sum_abs", rel)
+    record_property("max_err_fraction_of_bound", float(err.max()))
+    ulps = ""
+    if out_bf16:  # against the oracle's fp32 chain rounded once to bf16: bf16 ulps apart (ordered bit patterns)
+        def ordered(b):
+            b = b.astype(np.int64)
+            return np.where(b & 0x8000, 0x8000 - (b & 0x7FFF), 0x8000 + b)
+        du = int(np.abs(ordered(got.view(np.uint16)) - ordered(O.f32_to_bf16(ref))).max())
+        record_property("max_bf16_ulps_from_rounded_oracle", du)
+        ulps = ", max %d bf16 ulp(s) from the oracle's rounded chain" % du
+    print("rs tolerance G=%d D=%d chunks=%d bf16_in=%s bf16_out=%s: max |err| / sum|w x| = %.3g, "
+          "max fraction of the bound = %.3g%s" % (G, D, chunks, bf16, out_bf16, rel, float(err.max()), ulps))
     assert np.all(err <= 1.0), float(err.max())
 
 

@@ -81,7 +81,7 @@ def run(world, n, D, seed=17):
 
 
 @pytest.mark.parametrize("world,n,D", [(2, 10_000, 5), (3, 7_777, 7), (2, 4_099, 1), (3, 1_000, 2)])
-def test_layouts_match_single_gpu_chain(O, world, n, D):
+def test_layouts_match_single_gpu_chain(O, record_property, world, n, D):
     fa = load_pkg()
     import importlib
     shard = importlib.import_module("mhfsl_amd.shard")
@@ -101,6 +101,8 @@ def test_layouts_match_single_gpu_chain(O, world, n, D):
     for layout in ("rs", "rs_chunked"):  # chunked: reduce of chunk c+1 overlaps the reduce-scatter of chunk c
         got = np.concatenate([out[r][layout] for r in range(world)])[:n]
         ok, worst = shard.tolerance_ok(got, ref, absw)
+        record_property("max_err_fraction_of_bound_%s" % layout, worst)
+        print("%s world=%d n=%d D=%d: max |err| = %.3g of the bound 1e-6 sum|w x|" % (layout, world, n, D, worst))
         assert ok, (layout, worst)
     # block-cyclic rs: each rank's shard is its cyclic_bounds segments, concatenated
     npad = -(-n // (world * shard.UNIT)) * world * shard.UNIT
@@ -116,6 +118,8 @@ def test_layouts_match_single_gpu_chain(O, world, n, D):
                 off += b - a
         assert not np.isnan(got).any()  # the segments of all ranks cover the bucket
         ok, worst = shard.tolerance_ok(got[:n], ref, absw)
+        record_property("max_err_fraction_of_bound_rs_cyclic%d" % ch, worst)
+        print("rs_cyclic%d world=%d n=%d D=%d: max |err| = %.3g of the bound 1e-6 sum|w x|" % (ch, world, n, D, worst))
         assert ok, ("rs_cyclic", ch, worst)
         assert np.all(got[n:] == 0)  # padding stays zero
 
