@@ -94,6 +94,18 @@ def cpu_threads():
     return max(1, min(n, cap) if cap > 0 else n)
 
 
+def host_cpu():
+    """The host CPU model (the CPU baseline varies with the host a GPU box lands on)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(D, sample_elems, reps):
     """CPU baselines on the GPU box's host cores, before the GPU is initialised (child processes).
 
@@ -144,6 +156,7 @@ def cpu_baseline(D, sample_elems, reps):
             except Exception as e:  # noqa: BLE001 -- optional figures
                 print("cpu baseline: variant not timed (%s)" % e, file=sys.stderr)
             res.update(extra)
+            res["host_cpu"] = host_cpu()
             return res
         except Exception as e:  # noqa: BLE001 -- fall through to the port
             print("cpu baseline: ref_harness failed (%s), timing the oracle port" % e, file=sys.stderr)
@@ -157,7 +170,7 @@ def cpu_baseline(D, sample_elems, reps):
         oracle.fedavg(xs, w, threads=threads)
     dt = (time.perf_counter() - t0) / reps
     return {"value": round(D * sample_elems * 4 / dt / 2**30, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": sample + "; C oracle fmaf chain, %d threads" % threads}
+            "sample": sample + "; C oracle fmaf chain, %d threads" % threads, "host_cpu": host_cpu()}
 
 
 # ------------------------------------------------------------------ device measurement
