@@ -106,71 +106,262 @@ def host_cpu():
     return None
 
 
-def cpu_baseline(D, sample_elems, reps):
+# The reference's CPU path beside every config: the FedAvg chain restated in the
+# reference's own library (libtorch acc.add_(x_k, w_k), oracle/_ref/ref_harness bench-fedavg) at each
+# config's own shape.  name: (elements per client, clients, dtype, what the sample is)
+CPU_CONFIGS = {
+    "c2": (12_557_962, 8, "f32", "the whole config: 8 clients x ResNet-18's 12.6 M fp32 parameters"),
+    "c3": (42_737_546, 32, "bf16", "the whole config: 32 clients x ResNet-101's 42.7 M bf16 parameters "
+                                   "(fp32 accumulator, result rounded once to bf16)"),
+    "c4": (139_611_210, 64, "f32", "the whole config: 64 clients x VGG-19's 139.6 M fp32 parameters (35.7 GB)"),
+    "c5": (1 << 28, 16, "f32", "16 of the config's 128 clients x 1 GiB fp32 (16 GiB of host memory; the rate "
+                               "is per byte, the config's 128 GiB would take 8x as long)"),
+}
+# The reference's own receive loop (aggregator.cpp:59-93 / :112-150: torch::load of each receipt into the
+# global module + (p+p)/1000 + copy_), per round config: (secondary key, ref_harness model spec
+# name type start end nc, model_part, receipts, what it is)
+CPU_RECEIVE_LOOPS = [
+    ("round_c2", (1, 1, 9, 3, 10), 2, 8, "ResNet-18 (C2) model_part 2 (9.4 M fp32 parameters), 8 receipts"),
+    ("round_c4", (0, 6, 20, 3, 10), 3, 8, "VGG-19 (C4) model_part 3, the FC bucket (119.6 M fp32 parameters, a "
+                                          "478 MB blob per receipt; aggregator.cpp:112-150, torch::load at :118), "
+                                          "8 of the config's 64 receipts"),
+]
+
+
+CPU_MAX_SAMPLE_BYTES = 36 << 30  # host memory one CPU leg may fill (C4's whole config, 35.7 GB, fits)
+
+
+def cpu_baseline(D, n, reps, dt="f32", skip=None):
     """CPU baselines on the GPU box's host cores, before the GPU is initialised (child processes).
 
     oracle/_ref/ref_harness is built from the reference's own sources (model builders, State) linked with
     libtorch, the library the reference's arithmetic runs in -> kind "reference".  value = the FedAvg
-    metric restated in that library: acc.add_(x_k, w_k) in client order over a bounded sample of the
-    workload (the reference itself never computes FedAvg), all cores and one core.  Beside
-    it, the reference's own receive loop (aggregator.cpp:59-93: torch::load of each receipt into the
-    global module + (p+p)/1000 + copy_) on C2's largest bucket, with and without the torch::load decode.
-    Fallback without the harness: the C oracle ("port").
+    metric restated in that library: acc.add_(x_k, w_k) in client order over the WHOLE workload (D x n
+    fp32, inputs generated in host memory before the clock), all cores of the affinity mask; beside it one
+    core.  Returns (cpu_baseline object, {secondary key: figure}): every other config at its own shape
+    (CPU_CONFIGS) and the reference's own receive loop with torch::load on C2's and C4's largest buckets
+    (CPU_RECEIVE_LOOPS), each while the bench's time budget allows.  Fallback without the harness: the C
+    oracle ("port") on the same workload.
     """
     threads = cpu_threads()
+    cpu_model = host_cpu()
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
-    sample = "D=%d clients x %d fp32 elements (%.0f MiB per client), %d timed reps after 1 warm-up" % (
-        D, sample_elems, sample_elems * 4 / 2**20, reps)
+    s = 4 if dt == "f32" else 2
+    D0 = D
+    while D > 1 and D * n * s > CPU_MAX_SAMPLE_BYTES:  # C5 (128 GiB): a sample of its clients
+        D //= 2
+    sample = "%s: D=%d clients x %d %s elements (%.0f MiB per client, %.1f GiB in all), %d timed reps after 1 " \
+             "warm-up" % ("the whole workload" if D == D0 else "%d of the workload's %d clients" % (D, D0), D, n, dt,
+                          n * s / 2**20, D * n * s / 2**30, reps)
+    bf = ["bf16"] if dt == "bf16" else []
 
     def run(args, timeout=120):
         out = subprocess.run([harness] + [str(a) for a in args], capture_output=True, text=True, timeout=timeout,
                              check=True).stdout
         return json.loads(out.strip().splitlines()[-1])
+
+    def leg_timeout(cap=90):
+        left = budget_left() - 250
+        if left < 10:
+            raise TimeoutError("bench time budget (FA_BENCH_BUDGET_S): leg skipped")
+        return min(cap, left)
     if os.access(harness, os.X_OK):
         try:
-            r = run(["bench-fedavg", sample_elems, D, threads, reps])
+            r = run(["bench-fedavg", n, D, threads, reps] + bf)
             res = {"value": round(r["gib_s"], 3), "unit": "GiB/s", "cores": threads, "kind": "reference",
                    "path": "restatement in the reference's library: libtorch acc.add_(x_k, w_k) chain, "
                            "at::set_num_threads(%d)" % threads,
-                   "sample": sample}
-            extra = {}
-            try:
-                def variant_timeout():
-                    left = budget_left() - 250
-                    if left < 10:
-                        raise TimeoutError("bench time budget: variants skipped")
-                    return min(60, left)
-                r1 = run(["bench-fedavg", sample_elems, D, 1, max(2, reps // 4)], timeout=variant_timeout())
-                extra["fedavg_1_core"] = {"value": round(r1["gib_s"], 3), "unit": "GiB/s", "cores": 1}
-                for t in (threads, 1):
-                    for mode in ("", "arith"):
-                        lit = run(["bench-literal", 1, 1, 9, 3, 10, 8, t, 2] + ([mode] if mode else []),
-                                  timeout=variant_timeout())
-                        key = "reference_receive_loop" + ("_arith_only" if mode else "") + ("_1_core" if t == 1 else "")
-                        extra[key] = {
-                            "value": round(lit["gib_s"], 3), "unit": "GiB/s of parameters received", "cores": t,
-                            "path": "the reference's receive loop (aggregator.cpp:59-93): " +
-                                    ("(p+p)/1000 + copy_ on receipts decoded before the clock"
-                                     if mode else "torch::load of each receipt + (p+p)/1000 + copy_"),
-                            "sample": "ResNet-18 (C2) model_part 2 (%d fp32 params), 8 receipts" % lit["numel"]}
-            except Exception as e:  # noqa: BLE001 -- optional figures
-                print("cpu baseline: variant not timed (%s)" % e, file=sys.stderr)
-            res.update(extra)
-            res["host_cpu"] = host_cpu()
-            return res
+                   "sample": sample, "host_cpu": cpu_model}
         except Exception as e:  # noqa: BLE001 -- fall through to the port
             print("cpu baseline: ref_harness failed (%s), timing the oracle port" % e, file=sys.stderr)
+            res = None
+        if res is not None:
+            per = {}
+            try:
+                r1 = run(["bench-fedavg", n, D, 1, 2] + bf, timeout=leg_timeout(120))
+                res["fedavg_1_core"] = {"value": round(r1["gib_s"], 3), "unit": "GiB/s", "cores": 1,
+                                        "sample": "the whole workload, 2 timed reps"}
+            except Exception as e:  # noqa: BLE001 -- optional figures
+                print("cpu baseline: one-core leg not timed (%s)" % e, file=sys.stderr)
+            for key, (cn, cD, cdt, what) in CPU_CONFIGS.items():
+                if key == skip:  # the main line's own workload: `value` above
+                    continue
+                try:
+                    rc = run(["bench-fedavg", cn, cD, threads, 3] + (["bf16"] if cdt == "bf16" else []),
+                             timeout=leg_timeout())
+                    per[key] = {"cpu_gib_s": round(rc["gib_s"], 3), "cpu_cores": threads, "host_cpu": cpu_model,
+                                "cpu_kind": "reference", "cpu_path": "libtorch acc.add_(x_k, w_k) chain (%s)" % cdt,
+                                "cpu_sample": what + ", 3 timed reps", "cpu_ms_per_round": round(rc["avg_s"] * 1e3, 2)}
+                except Exception as e:  # noqa: BLE001
+                    per[key] = {"cpu_error": repr(e)[:200]}
+            for key, spec, mp, receipts, what in CPU_RECEIVE_LOOPS:
+                try:
+                    lit = run(["bench-literal"] + list(spec) + [receipts, threads, mp], timeout=leg_timeout(120))
+                    per[key] = {"cpu_gib_s": round(lit["gib_s"], 3), "cpu_cores": threads, "host_cpu": cpu_model,
+                                "cpu_kind": "reference",
+                                "cpu_path": "the reference's receive loop: torch::load of each receipt + (p+p)/1000 "
+                                            "+ copy_ (GiB/s of parameters received)",
+                                "cpu_sample": what}
+                except Exception as e:  # noqa: BLE001
+                    per[key] = {"cpu_error": repr(e)[:200]}
+            # the C2 receive loop also without the decode, and on one core (the reference's own shape)
+            for t in (threads, 1):
+                for mode in ("", "arith"):
+                    if t == threads and not mode:
+                        continue  # = per["round_c2"]
+                    try:
+                        lit = run(["bench-literal", 1, 1, 9, 3, 10, 8, t, 2] + ([mode] if mode else []),
+                                  timeout=leg_timeout(60))
+                        k = "reference_receive_loop" + ("_arith_only" if mode else "") + ("_1_core" if t == 1 else "")
+                        res[k] = {"value": round(lit["gib_s"], 3), "unit": "GiB/s of parameters received", "cores": t,
+                                  "path": "the reference's receive loop (aggregator.cpp:59-93): " +
+                                          ("(p+p)/1000 + copy_ on receipts decoded before the clock"
+                                           if mode else "torch::load of each receipt + (p+p)/1000 + copy_"),
+                                  "sample": "ResNet-18 (C2) model_part 2 (%d fp32 params), 8 receipts" % lit["numel"]}
+                    except Exception as e:  # noqa: BLE001
+                        print("cpu baseline: receive-loop variant not timed (%s)" % e, file=sys.stderr)
+            if "round_c2" in per and "cpu_gib_s" in per["round_c2"]:
+                res["reference_receive_loop"] = {"value": per["round_c2"]["cpu_gib_s"],
+                                                 "unit": "GiB/s of parameters received", "cores": threads,
+                                                 "path": "the reference's receive loop (aggregator.cpp:59-93): "
+                                                         "torch::load of each receipt + (p+p)/1000 + copy_",
+                                                 "sample": per["round_c2"]["cpu_sample"]}
+            return res, per
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    xs = [oracle.gen(0x5EED, k, sample_elems) for k in range(D)]
     w = oracle.weights(D)
+    xs = [oracle.gen(0x5EED, k, n, dtype=dt) for k in range(D)]
     oracle.fedavg(xs, w, threads=threads)
     t0 = time.perf_counter()
     for _ in range(reps):
         oracle.fedavg(xs, w, threads=threads)
-    dt = (time.perf_counter() - t0) / reps
-    return {"value": round(D * sample_elems * 4 / dt / 2**30, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": sample + "; C oracle fmaf chain, %d threads" % threads, "host_cpu": host_cpu()}
+    per_rep = (time.perf_counter() - t0) / reps
+    return {"value": round(D * n * s / per_rep / 2**30, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": sample + "; C oracle fmaf chain, %d threads" % threads, "host_cpu": cpu_model}, {}
+
+
+# ------------------------------------------------------------------ parity (the checker, outside every timed region)
+#
+# Every leg that times a reduction checks what it computed afterwards: sampled elements of its result
+# against the ordered chain (aggregator.cpp:59-93 / :112-150 with FedAvg semantics) evaluated by the C
+# oracle at those indices only.  The oracle is the checker here, as in smoke(): it runs after the timed
+# region has closed, never inside it, and nothing it computes feeds the measured path.  Range and chain
+# layouts must be bit-exact; the client-sharded reduce-scatter (rs) sums in RCCL's order, so it is held to
+# |err| <= 1e-6 * sum_k |w_k x_k| (BASELINE.json north_star: "within 1e-6 relative fp32").
+
+PARITY_SAMPLES = 1024
+RS_REL_TOL = 1e-6
+
+
+def load_checker():
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    return oracle
+
+
+def sample_positions(segments, k=PARITY_SAMPLES, salt=0):
+    """Positions to check in a result that holds the bucket segments [lo, hi) concatenated in the order
+    given: both ends of every segment plus `k` positions spread uniformly (fixed seed) over the rest.
+    Returns (positions in the result, global element indices), both int64 / uint64 arrays."""
+    import numpy as np
+    segs = [(int(a), int(b)) for a, b in segments if b > a]
+    if not segs:
+        return np.zeros(0, np.int64), np.zeros(0, np.uint64)
+    lens = np.array([b - a for a, b in segs], np.int64)
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    total = int(lens.sum())
+    if total <= k:  # a small result: every element
+        pos = np.arange(total, dtype=np.int64)
+    else:
+        rng = np.random.default_rng(0xC0FFEE ^ salt)
+        draw = np.unique(rng.integers(0, total, size=2 * k))
+        while draw.size < k:  # only when k is close to total
+            draw = np.unique(np.concatenate([draw, rng.integers(0, total, size=k)]))
+        pos = np.unique(np.concatenate([starts, starts + lens - 1, rng.permutation(draw)[:k]]))
+    seg = np.searchsorted(starts, pos, side="right") - 1
+    lo = np.array([a for a, _ in segs], np.int64)
+    return pos, (lo[seg] + (pos - starts[seg])).astype(np.uint64)
+
+
+def parity_check(got, pos, idx, seed, w, exact=True, clients=None, bf16_in=False, literal=False):
+    """Sampled parity of one result (host array `got`, fp32 or bf16 bits as uint16) against the oracle.
+
+    exact: bit equality with the oracle's chain (rounded once to bf16 for a bf16 result); otherwise
+    |got - ref| <= RS_REL_TOL * sum_k |w_k x_k| per element.  literal: the reference's own arithmetic
+    fl(fl(x + x) / 1000) of the last client (`w` only gives the client count)."""
+    import numpy as np
+    O = load_checker()
+    if literal:
+        last = O.gen_at(seed, len(w) - 1 if clients is None else clients[-1], idx)
+        if bf16_in:
+            last = O.f32_to_bf16(last)
+        ref = O.literal(last, out_dtype="bf16" if np.asarray(got).dtype == np.uint16 else "f32")
+        sabs = None
+    else:
+        ref, sabs = O.sampled_chain(seed, w, idx, clients, bf16_in)
+    g = np.asarray(got)[pos]
+    if g.dtype == np.uint16:  # a bf16 result
+        if not literal:
+            ref = O.f32_to_bf16(ref)
+        gf, rf = O.bf16_to_f32(g).astype(np.float64), O.bf16_to_f32(ref).astype(np.float64)
+        gb, rb = g, ref
+    else:
+        gf, rf = g.astype(np.float64), ref.astype(np.float64)
+        gb, rb = g.view(np.uint32), ref.view(np.uint32)
+    err = np.abs(gf - rf)
+    res = {"samples": int(pos.size), "max_abs_err": float(err.max()) if err.size else 0.0}
+    if exact:
+        bad = int(np.count_nonzero(gb != rb))
+        res.update({"check": "bit-exact vs the oracle's ordered chain" if not literal else
+                    "bit-exact vs the oracle's fl(fl(x+x)/1000) of the last client", "mismatches": bad})
+    else:
+        bound = RS_REL_TOL * sabs + 1e-30
+        ratio = err / bound
+        res.update({"check": "|err| <= %g * sum_k |w_k x_k|" % RS_REL_TOL,
+                    "mismatches": int(np.count_nonzero(ratio > 1.0)),
+                    "max_err_over_bound": float(ratio.max()) if ratio.size else 0.0})
+    res["ok"] = res["mismatches"] == 0 and res["samples"] > 0
+    return res
+
+
+def parity_merge(parts):
+    """One parity object from several (GPUs of one context, buckets of one round)."""
+    parts = [p for p in parts if p]
+    if not parts:
+        return None
+    out = {"check": parts[0]["check"], "samples": sum(p["samples"] for p in parts),
+           "mismatches": sum(p["mismatches"] for p in parts),
+           "max_abs_err": max(p["max_abs_err"] for p in parts)}
+    if any("max_err_over_bound" in p for p in parts):
+        out["max_err_over_bound"] = max(p.get("max_err_over_bound", 0.0) for p in parts)
+    out["ok"] = all(p["ok"] for p in parts)
+    return out
+
+
+def parity_over_ranks(torch, dist, world, backend, p):
+    """Rank-local parity summed (samples, mismatches) and maxed (errors) over the ranks; every rank gets it."""
+    if world == 1 or p is None:
+        return p
+    dev = "cuda" if backend == "nccl" else "cpu"
+    s = torch.tensor([p["samples"], p["mismatches"], 0 if p["ok"] else 1], dtype=torch.float64, device=dev)
+    m = torch.tensor([p["max_abs_err"], p.get("max_err_over_bound", 0.0)], dtype=torch.float64, device=dev)
+    dist.all_reduce(s, op=dist.ReduceOp.SUM)
+    dist.all_reduce(m, op=dist.ReduceOp.MAX)
+    s, m = s.tolist(), m.tolist()
+    out = dict(p, samples=int(s[0]), mismatches=int(s[1]), max_abs_err=m[0], ranks=world, ok=s[2] == 0 and s[1] == 0)
+    if "max_err_over_bound" in p:
+        out["max_err_over_bound"] = m[1]
+    return out
+
+
+def parity_guarded(fn):
+    """A parity check that fails to run is reported as such (ok false), never fatal to the bench line."""
+    try:
+        return fn()
+    except Exception as e:  # noqa: BLE001
+        traceback.print_exc()
+        return {"ok": False, "error": repr(e)[:300], "samples": 0, "mismatches": 0, "max_abs_err": 0.0,
+                "check": "not run"}
 
 
 # ------------------------------------------------------------------ device measurement
@@ -271,9 +462,11 @@ class Setup:
     """
 
     def __init__(self, fa, torch, D, n, in_dt, out_dt, elem0, device, client0=0, seed=0x5EED,
-                 min_rotate_bytes=ROTATE_MIN_BYTES, mode=None):
+                 min_rotate_bytes=ROTATE_MIN_BYTES, mode=None, contiguous=False):
         self.fa, self.torch = fa, torch
         self.D, self.n = D, n
+        self.elem0, self.client0, self.seed = elem0, client0, seed
+        self.literal = mode is not None and mode == fa.LITERAL
         self.in_dt = fa.F32 if in_dt == "f32" else fa.BF16
         self.out_dt = fa.F32 if out_dt == "f32" else fa.BF16
         self.s_in = 4 if in_dt == "f32" else 2
@@ -281,12 +474,24 @@ class Setup:
         set_bytes = D * n * self.s_in
         self.nsets = max(1, -(-min_rotate_bytes // set_bytes))
         self.agg = fa.Aggregator(devices=[device])
-        for s in range(self.nsets):
-            self.agg.define(s, n, self.in_dt, self.out_dt, D, fa.FEDAVG if mode is None else mode)
-            for k in range(D):
-                for ptr, cnt, off in self.agg.pieces(s, 0, k):
-                    # global client id and element offset: ranks hold disjoint clients or slices of one bucket
-                    fa.fill_uniform(ptr, cnt, self.in_dt, seed + s, client0 + k, idx0=elem0 + off)
+        # contiguous: every client slot one range of device memory (the client-sharded legs hand raw slot
+        # addresses to fa_reduce_device), i.e. no range pieces (FA_PIECE_SPAN=0 while the parts are defined)
+        span0 = os.environ.get("FA_PIECE_SPAN")
+        if contiguous:
+            os.environ["FA_PIECE_SPAN"] = "0"
+        try:
+            for s in range(self.nsets):
+                self.agg.define(s, n, self.in_dt, self.out_dt, D, fa.FEDAVG if mode is None else mode)
+                for k in range(D):
+                    for ptr, cnt, off in self.agg.pieces(s, 0, k):
+                        # global client id and element offset: ranks hold disjoint clients or slices of one bucket
+                        fa.fill_uniform(ptr, cnt, self.in_dt, seed + s, client0 + k, idx0=elem0 + off)
+        finally:
+            if contiguous:
+                if span0 is None:
+                    os.environ.pop("FA_PIECE_SPAN", None)
+                else:
+                    os.environ["FA_PIECE_SPAN"] = span0
         self.w = self._weights(D)
 
     @staticmethod
@@ -308,8 +513,24 @@ class Setup:
     def launch(self, step, stream):
         self.agg.reduce(step % self.nsets, self.w, stream=stream)
 
+    def pieced(self, s=0):
+        return len(self.agg.pieces(s, 0, 0)) > 1
+
     def clients(self, s=0):
+        """Device addresses of the D client slots of set s (each one contiguous range)."""
+        if self.pieced(s):
+            raise RuntimeError("bucket set %d is held in range pieces (fa_bucket_pieces): its client slots are not "
+                               "contiguous; build the Setup with contiguous=True" % s)
         return [self.agg.slot(s, 0, k)[0] for k in range(self.D)]
+
+    def parity(self, s=0):
+        """Sampled parity of input set s's reduced bucket (read back after the timed region): the oracle's
+        chain over global clients client0.. at global elements elem0.. (literal mode: the last client)."""
+        got = self.agg.copy_output(s)
+        pos, idx = sample_positions([(self.elem0, self.elem0 + self.n)], salt=s)
+        return parity_check(got, pos, idx, self.seed + s, self.w,
+                            clients=[self.client0 + k for k in range(self.D)],
+                            bf16_in=self.in_dt == self.fa.BF16, literal=self.literal)
 
     def close(self):
         self.agg.close()
@@ -354,6 +575,15 @@ class RoundSetup:
                     fa.fill_uniform(ptr, cnt, self.in_dt, 0x5EED + 100 * st + j, k)
         self.w = Setup._weights(D)
 
+    def parity(self, st=0):
+        """Sampled parity of every bucket of input set st (phase 1 and the batched phase 2), merged."""
+        res = []
+        for j, n in enumerate(self.sizes):
+            got = self.agg.copy_output(10 * st + j + 1)
+            pos, idx = sample_positions([(0, n)], salt=j)
+            res.append(parity_check(got, pos, idx, 0x5EED + 100 * st + j, self.w, bf16_in=self.in_dt == self.fa.BF16))
+        return parity_merge(res)
+
     def launch(self, step, stream):
         base = 10 * (step % self.nsets)
         self.agg.reduce(base + 1, self.w, stream=stream)  # phase 1
@@ -392,18 +622,25 @@ def read_stream_peak(fa, torch, setup, stream, reps=7):
     read; frac_of_read_stream = achieved / this, i.e. what the output stream costs on top of the reads."""
     if setup.in_dt != fa.F32:
         return None
-    n = setup.n - setup.n % 4
-    ptrs = setup.clients(0)
-    ms = []
-    for i in range(reps + 2):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        fa.diag_read_stream(ptrs, n, stream=stream)
-        b.record(stream)
-        b.synchronize()
-        if i >= 2:
-            ms.append(a.elapsed_time(b))
-    return round(setup.D * n * 4 / (statistics.median(ms) * 1e-3) / 1e9, 1)
+    # one read-only launch per range piece (a bucket set held in pieces, e.g. C5 on one GPU, is reduced one
+    # launch per piece too): bytes of all pieces / the sum of their median times
+    per_client = [setup.agg.pieces(0, 0, k) for k in range(setup.D)]
+    nbytes, t_ms = 0, 0.0
+    for j in range(len(per_client[0])):
+        ptrs = [pc[j][0] for pc in per_client]
+        n = per_client[0][j][1] - per_client[0][j][1] % 4
+        ms = []
+        for i in range(reps + 2):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            fa.diag_read_stream(ptrs, n, stream=stream)
+            b.record(stream)
+            b.synchronize()
+            if i >= 2:
+                ms.append(a.elapsed_time(b))
+        nbytes += setup.D * n * 4
+        t_ms += statistics.median(ms)
+    return round(nbytes / (t_ms * 1e-3) / 1e9, 1)
 
 
 def timed_loop(torch, setup, steps, warmup, stream, dist, barrier, per_launch=10):
@@ -463,11 +700,27 @@ def time_client_sharded(torch, dist, shard, setup, layout, n, world, device, str
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        step()
+        res = step()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
-    return time.perf_counter() - t0
+    return time.perf_counter() - t0, res
+
+
+def client_sharded_parity(shard, setup, layout, res, n, world, rank, chunks, D):
+    """Sampled parity of a client-sharded round's result `res` (this rank's part, read back after the timed
+    region): "rs" holds the block-cyclic segments of shard.cyclic_bounds (RCCL's summation order: the 1e-6
+    tolerance); "chain" this rank's range of the ordered chain (bit-exact); one rank: the whole chain."""
+    got = res.cpu().numpy()
+    if world == 1:
+        segs, exact = [(0, n)], True
+    elif layout == "rs":
+        segs, exact = shard.cyclic_bounds(n, world, rank, chunks), False
+    else:
+        segs, exact = [shard.range_bounds(n, world, rank)], True
+    pos, idx = sample_positions(segs, salt=rank)
+    return parity_check(got, pos, idx, setup.seed, Setup._weights(D), exact=exact,
+                        bf16_in=setup.in_dt == setup.fa.BF16)
 
 
 def layout_desc_of(layout, D, world, chunks):
@@ -610,9 +863,9 @@ def main():
         if live[0] is None:
             print("bench: %s; using the committed profile" % live[1], file=sys.stderr)
 
-    cpu = None
+    cpu, cpu_per = None, {}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(D, 16 << 20, 10)
+        cpu, cpu_per = cpu_baseline(D, n, 5, in_dt, skip=args.workload)
 
     import torch
     import torch.distributed as dist
@@ -663,7 +916,7 @@ def main():
     else:
         # client-sharded: strong: the D clients are dealt to the ranks; weak: every rank holds D clients
         c0, c1 = shard.client_bounds(D, world, rank) if strong else (rank * D, (rank + 1) * D)
-        setup = Setup(fa, torch, c1 - c0, n, in_dt, out_dt, 0, device, client0=c0)
+        setup = Setup(fa, torch, c1 - c0, n, in_dt, out_dt, 0, device, client0=c0, contiguous=True)
         setup.w = Setup._weights(D if strong else D * world)[c0:c1]
         total_bytes = D * n * s_in * (1 if strong else world)
         layout_desc = layout_desc_of(args.layout, c1 - c0, world, args.chunks)
@@ -680,12 +933,20 @@ def main():
         if world > 1:  # one rank runs no collective
             fa.set_tuning(walk=shard.OVERLAP_WALK)
         try:
-            wall = time_client_sharded(torch, dist, shard, setup, args.layout, n, world, device, stream,
-                                       args.steps, args.warmup, args.chunks, barrier)
+            wall, res = time_client_sharded(torch, dist, shard, setup, args.layout, n, world, device, stream,
+                                            args.steps, args.warmup, args.chunks, barrier)
         finally:
             fa.set_tuning(walk=walk0)
         timeouts += fa.phased_timeouts(device) - timeouts0 - timeouts
     wall = max_over_ranks(wall)
+    # parity of what was timed, read back and checked now that the timed region is closed
+    if args.layout == "range":
+        par = parity_guarded(lambda: setup.parity(0))
+    else:
+        par = parity_guarded(lambda: client_sharded_parity(shard, setup, args.layout, res, n, world, rank,
+                                                           args.chunks, D if strong else D * world))
+        res = None
+    par = parity_over_ranks(torch, dist, world, backend, par)
 
     achieved = setup.algo_bytes() / (kavg * 1e-3) / 1e9
     read_peak = read_stream_peak(fa, torch, setup, stream) if args.layout == "range" and not under_profiler() \
@@ -731,6 +992,7 @@ def main():
                      "read_stream_peak": read_peak, "frac_of_read_stream":
                          round(achieved / read_peak, 4) if read_peak else None},
         "cpu_baseline": cpu,
+        "parity": par,
     }
     if world > 1:
         line["roofline"]["kernel_ms_avg_max_over_ranks"] = round(max_over_ranks(kavg), 4)
@@ -738,6 +1000,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_secondary:
         setup.close()
         line["secondary"] = single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier)
+        for key, fig in cpu_per.items():  # the reference's CPU path beside each config's device figure
+            line["secondary"].setdefault(key, {}).update(fig)
         if n_dev >= 2:
             line["secondary"].update(ctx_multi_secondaries(n_dev, T_START + BUDGET_S))
 
@@ -770,25 +1034,29 @@ def main():
                     w2, _, _ = timed_loop(torch, s2, steps2, 3, stream, dist, barrier)
                     tb, desc2 = D * n * s_in * world, "weak scaling: every rank reduces its own %d-element slice " \
                                                        "of %d buckets, no collective" % (n, D)
+                    p2 = parity_guarded(lambda: s2.parity(0))
                 else:
                     c0, c1 = shard.client_bounds(D, world, rank)
-                    s2 = Setup(fa, torch, c1 - c0, n, in_dt, out_dt, 0, device, client0=c0)
+                    s2 = Setup(fa, torch, c1 - c0, n, in_dt, out_dt, 0, device, client0=c0, contiguous=True)
                     s2.w = Setup._weights(D)[c0:c1]
                     torch.cuda.synchronize()
                     # the local reductions run beside RCCL's kernels: the one-shot walk (shard.py, "Overlap")
                     walk0 = fa.get_tuning()["walk"]
                     fa.set_tuning(walk=shard.OVERLAP_WALK)
                     try:
-                        w2 = time_client_sharded(torch, dist, shard, s2, L, n, world, device, stream, steps2, 3,
-                                                 args.chunks, barrier)
+                        w2, r2 = time_client_sharded(torch, dist, shard, s2, L, n, world, device, stream, steps2,
+                                                     3, args.chunks, barrier)
                     finally:
                         fa.set_tuning(walk=walk0)
                     tb, desc2 = D * n * s_in, layout_desc_of(L, c1 - c0, world, args.chunks)
+                    p2 = parity_guarded(lambda: client_sharded_parity(shard, s2, L, r2, n, world, rank, args.chunks, D))
+                    r2 = None
                 t2 = fa.phased_timeouts(device) - timeouts0 - timeouts
                 w2 = max_over_ranks(w2)
                 sec[L] = {"description": desc2, "clients": D, "steps": steps2,
                           "ms_per_step": round(w2 / steps2 * 1e3, 4), "gib_s": round(tb * steps2 / w2 / 2**30, 1),
-                          "phased_meeting_timeouts": int(max_over_ranks(t2))}
+                          "phased_meeting_timeouts": int(max_over_ranks(t2)),
+                          "parity": parity_over_ranks(torch, dist, world, backend, p2)}
                 timeouts += t2
                 s2.close()
             except Exception as e:  # noqa: BLE001 -- the ranks may now disagree: report and leave
@@ -833,13 +1101,20 @@ def ctx_multi(args):
     for g in range(G):
         torch.cuda.synchronize(g)
     w = Setup._weights(D)
+    import numpy as np
+    clients = None  # chain position k holds generator client k
     if args.h2d:
-        # client buckets in pinned host memory (8 distinct buffers, client k uses k % 8: timing does not depend on
-        # values and C5 stays at 8 GiB of host memory), submitted each round; the result lands in host memory
-        import numpy as np
+        # client buckets in pinned host memory (8 distinct buffers, client k uses k % 8, so C5 stays at 8 GiB of
+        # host memory), submitted each round; the result lands in host memory.  Buffer i holds generator client
+        # i (filled on the device, copied once, outside the timed region), so the result can be checked.
         hosts = [fa.PinnedBuffer(n * s_in) for _ in range(min(D, 8))]
+        tmp = torch.empty(n * s_in // 4, dtype=torch.float32, device="cuda:0")
         for i, h in enumerate(hosts):
-            h.view(np.float32)[:] = 0.25 * (i + 1)  # any finite values: the timing does not depend on them
+            fa.fill_uniform(tmp, n, idt, 0x5EED, i)
+            torch.from_numpy(h.view(np.float32, count=n * s_in // 4)).copy_(tmp)
+        del tmp
+        torch.cuda.synchronize(0)
+        clients = [k % len(hosts) for k in range(D)]
         res = np.empty(n, np.float32)
 
         def step():
@@ -860,10 +1135,30 @@ def ctx_multi(args):
     dt = (time.perf_counter() - t0) / args.steps
     # > 0: a phased launch's grid was not co-resident on some GPU (the rs layout never takes that kernel)
     timeouts = sum(fa.phased_timeouts(g) - t_before[g] for g in range(G))
+    tuning = agg.get_tuning()
+    # parity of the last round, read back now that the timed region is closed: >= 1024 sampled elements of
+    # every GPU's share of the result (range: its element range, pieces included; rs: its block-cyclic
+    # segments after the RCCL reduce-scatter, held to the 1e-6 tolerance)
+    def check():
+        got = res if args.h2d else agg.copy_output(1)
+        per_gpu = []
+        for g in range(G):
+            if rs:
+                segs = [(lo, min(hi, n)) for lo, hi in fa.rs_segments(n, G, tuning["rs_chunks"], g) if lo < n]
+            else:
+                segs = [(off, off + cnt) for _, cnt, off in agg.pieces(1, g, 0)]
+            pos, idx = sample_positions(segs, salt=g)
+            # the whole result is on the host: position = element index
+            per_gpu.append(parity_check(got, idx.astype(np.int64), idx, 0x5EED, w, exact=not rs or G == 1,
+                                        clients=clients, bf16_in=idt == fa.BF16))
+        p = parity_merge(per_gpu)
+        p["per_gpu_samples"] = [q["samples"] for q in per_gpu]
+        return p
+    parity = parity_guarded(check)
     out = {"layout": args.ctx_multi, "gpus": G, "workload": args.workload, "description": desc, "clients": D,
            "elems_per_client": n, "host_inclusive": args.h2d, "ms_per_round": round(dt * 1e3, 4),
            "gib_s": round(D * n * s_in / dt / 2**30, 1), "steps": args.steps,
-           "phased_meeting_timeouts": timeouts, "tuning": agg.get_tuning()}
+           "phased_meeting_timeouts": timeouts, "parity": parity, "tuning": tuning}
     agg.close()
     print(json.dumps(out), flush=True)
 
@@ -914,7 +1209,7 @@ def single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier):
                      "algorithmic_bytes_per_launch": s.algo_bytes(),
                      "traffic": traffic_from_profile(name, 1)[0],
                      "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                     "input_sets_rotated": s.nsets}
+                     "input_sets_rotated": s.nsets, "parity": parity_guarded(lambda: s.parity(0))}
         s.close()
 
     # the buckets of one aggregator round as it forms them: per-round device time and roofline fraction,
@@ -929,16 +1224,19 @@ def single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier):
                                (" (phase 2 batched: fa_reduce_parts)" if batched else " (one launch per part)"),
                 "round_ms_avg": round(ka, 4), "algorithmic_bytes_per_round": s.algo_bytes(),
                 "achieved_GBs": round(s.algo_bytes() / (ka * 1e-3) / 1e9, 1),
-                "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "input_sets_rotated": s.nsets}
+                "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "input_sets_rotated": s.nsets,
+                "parity": parity_guarded(lambda: s.parity())}
             s.close()
 
-    def one(key, s, desc):
+    def one(key, s, desc, check=False):
         torch.cuda.synchronize()
         _, ka, _ = timed_loop(torch, s, max(10, args.steps), 3, stream, dist, barrier)
         sec[key] = {"description": desc, "kernel_ms_avg": round(ka, 4),
                     "achieved_GBs": round(s.algo_bytes() / (ka * 1e-3) / 1e9, 1),
                     "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                     "input_sets_rotated": s.nsets}
+        if check:
+            sec[key]["parity"] = parity_guarded(lambda: s.parity(0))
         s.close()
     # compute-node aggregation on the C2 shape: 8 client copies synced in place
     sD, sn, si, so, _ = WORKLOADS["c2"]
@@ -951,7 +1249,8 @@ def single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier):
     # the reference's own semantics (aggregator.cpp:72-88, literal mode): fl(fl(x+x)/1000) of the last
     # receipt, on its largest bucket (VGG-19's FC part); per element one read + one write
     one("literal_vgg_fc", Setup(fa, torch, 1, 119_586_826, "f32", "f32", 0, device, mode=fa.LITERAL),
-        "reference-literal mode fl(fl(x+x)/1000) of the last receipt, VGG-19's FC part (119.6 M fp32 parameters)")
+        "reference-literal mode fl(fl(x+x)/1000) of the last receipt, VGG-19's FC part (119.6 M fp32 parameters)",
+        check=True)
     return sec
 
 

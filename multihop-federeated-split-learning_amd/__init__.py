@@ -93,6 +93,8 @@ def lib():
         "fa_diag_rs_plan": (I, [S, I, I, I, I, I, I, ctypes.POINTER(I), ctypes.POINTER(I),
                                 ctypes.POINTER(ctypes.c_longlong)]),
         "fa_diag_pieces": (I, [S, I, I, ctypes.POINTER(I), ctypes.POINTER(S)]),
+        "fa_diag_phased_slot": (I, [I, P, ctypes.POINTER(I)]),
+        "fa_diag_phased_owned": (I, [I]),
         "fa_set_tuning": (I, [ctypes.POINTER(_Tuning)]),
         "fa_get_tuning": (I, [ctypes.POINTER(_Tuning)]),
     }
@@ -233,6 +235,25 @@ def phased_timeouts(device=0):
     c = ctypes.c_uint64()
     check(lib().fa_phased_timeouts(device, ctypes.byref(c)))
     return c.value
+
+
+def phased_slot(stream, device=0):
+    """fa_diag_phased_slot (diagnostic): (counter slot, owned) of the phased kernel for `stream` on `device`,
+    assigned now if the stream has none yet -- owned: the slot is the stream's alone (the first 48 streams,
+    until their context is destroyed), else a hashed slot shared with other streams."""
+    own = ctypes.c_int()
+    slot = lib().fa_diag_phased_slot(device, _stream(stream), ctypes.byref(own))
+    if slot < 0:
+        check(slot)
+    return slot, bool(own.value)
+
+
+def phased_owned_slots(device=0):
+    """fa_diag_phased_owned (diagnostic): how many of the 48 owned counter slots are taken on `device`."""
+    n = lib().fa_diag_phased_owned(device)
+    if n < 0:
+        check(n)
+    return n
 
 
 def rs_segments(n, n_gpus, chunks, gpu):

@@ -1126,11 +1126,21 @@ int reduce_parts_impl(fa_ctx* ctx, int n_parts, const int* ids, const float* con
                         ti = (r.seg_last + 1) % kSegRing;
                         GpuRes::SegTable& t = r.seg[ti];
                         if (!t.host) {
-                            if (hipHostMalloc((void**)&t.host, sizeof(fa::SegDesc) * kMaxSegments, hipHostMallocDefault) !=
+                            // all three or none: a ring entry is either fully usable or allocated afresh next time
+                            fa::SegDesc *h = nullptr, *d = nullptr;
+                            hipEvent_t ev = nullptr;
+                            if (hipHostMalloc((void**)&h, sizeof(fa::SegDesc) * kMaxSegments, hipHostMallocDefault) !=
                                     hipSuccess ||
-                                hipMalloc((void**)&t.dev, sizeof(fa::SegDesc) * kMaxSegments) != hipSuccess ||
-                                hipEventCreateWithFlags(&t.ev, hipEventDisableTiming) != hipSuccess)
+                                hipMalloc((void**)&d, sizeof(fa::SegDesc) * kMaxSegments) != hipSuccess ||
+                                hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+                                if (h) (void)hipHostFree(h);
+                                if (d) (void)hipFree(d);
+                                (void)hipGetLastError();
                                 return fail(FA_ERR_NOMEM, "segment table allocation failed");
+                            }
+                            t.host = h;
+                            t.dev = d;
+                            t.ev = ev;
                         } else {
                             // the slot's last launch (on any stream) has read the device table, and its upload
                             // the pinned one, before either is rewritten
@@ -1358,7 +1368,10 @@ void fa_destroy(fa_ctx* ctx) {
             if (e) (void)hipEventDestroy(e);
         if (r.scratch) (void)hipFree(r.scratch);
         for (hipStream_t s : {r.compute, r.copy, r.comm})
-            if (s) (void)hipStreamDestroy(s);
+            if (s) {
+                fa::phased_release_stream(r.dev, s);  // its phased counter slot goes to the next new stream
+                (void)hipStreamDestroy(s);
+            }
         r.pool.reset();
     }
     ctx->workers.reset();
@@ -1768,6 +1781,26 @@ extern "C" int fa_diag_read_stream(const void* const* d_bufs, int nc, size_t n, 
 // when the process runs with FA_TIMELINE=1 (tools/timeline.py).
 extern "C" int fa_diag_phased_timeline(int device, unsigned long long* out, int cap) {
     return out && cap > 0 ? fa::phased_timeline(device, out, cap) : -1;
+}
+
+// Diagnostic, not part of the ABI in fa.h: the phased kernel's counter slot of `hip_stream` on `device`
+// (assigned now if the stream has none, exactly as its first phased launch would); *own = 1 when the slot is
+// the stream's alone, 0 for a hashed slot shared with other streams (tests/test_gpu_parity.py).
+extern "C" int fa_diag_phased_slot(int device, void* hip_stream, int* own) {
+    g_err.clear();
+    bool o = false;
+    const int slot = fa::phased_slot(device, static_cast<hipStream_t>(hip_stream), &o);
+    if (slot < 0) return fail(FA_ERR_ARG, "device %d", device);
+    if (own) *own = o ? 1 : 0;
+    return slot;
+}
+
+// Diagnostic, not part of the ABI in fa.h: how many of the owned counter slots are taken on `device` (a
+// destroyed context gives its streams' slots back).
+extern "C" int fa_diag_phased_owned(int device) {
+    g_err.clear();
+    const int n = fa::phased_owned_slots(device);
+    return n < 0 ? fail(FA_ERR_ARG, "device %d", device) : n;
 }
 
 // Diagnostic, not part of the ABI in fa.h: the kernel plan (fa::plan_chain) of one FedAvg chain launch of n

@@ -57,6 +57,11 @@ hipError_t phased_timeouts(int dev, uint64_t* count);
 // FA_TIMELINE=1 diagnostic: copies the last phased launch's per-workgroup timeline (8 words each) on device
 // dev into out; returns the words copied (0: no timeline, -1: HIP error).
 int phased_timeline(int dev, unsigned long long* out, int cap);
+// The phased kernel's counter slot of stream s on device dev (assigned on first use, as a launch would;
+// *own: the slot is the stream's alone), and the release of a stream's owned slot (fa_destroy).
+int phased_slot(int dev, hipStream_t s, bool* own);
+void phased_release_stream(int dev, hipStream_t s);
+int phased_owned_slots(int dev);  // owned slots currently taken on dev
 // What one FedAvg chain launch runs (plan_chain, host-only): the one-shot vector grid, the one-element-per-
 // lane kernel (mixed 16-byte phases), or the phased persistent grid (`threads` per workgroup, `regs` bytes of
 // register stage per lane, `phases` phases; phases > 1 means chip-wide meetings).

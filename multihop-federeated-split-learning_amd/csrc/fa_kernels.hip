@@ -804,9 +804,11 @@ hipError_t launch_chain_lnt(const ClientTable& t, int nc, const float* init, voi
 // slots (ticket + ring, fedavg_phased_kernel), one picked per stream, 256 B apart.
 constexpr int kMaxDevices = 64, kSyncSlots = 64, kSyncStride = 64;
 static_assert(4 + 2 * kSyncRing <= kSyncStride, "a counter slot holds the ticket and both rings");
-// Counter slots [0, kOwnedSlots) belong to one stream each (first come, for the life of the process), so
-// launches on two streams never mix their workgroups in one epoch; further streams share the hashed slots
-// [kOwnedSlots, kSyncSlots) (speed only, never results: see the ring above).
+// Counter slots [0, kOwnedSlots) belong to one stream each (first come, until the stream is released:
+// fa_destroy releases its context's streams), so launches on two streams never mix their workgroups in one
+// epoch; further streams share the hashed slots [kOwnedSlots, kSyncSlots) (speed only, never results: see
+// the ring above).  A released slot is handed to the next new stream; it needs no reset, since a slot's
+// ticket and ring already serve any sequence of launches from any streams (the hashed slots rely on it).
 constexpr int kOwnedSlots = 48;
 struct PhasedDevice {
     std::once_flag once;
@@ -815,15 +817,33 @@ struct PhasedDevice {
     unsigned long long* tl = nullptr;  // FA_TIMELINE=1: the last phased launch's per-workgroup timeline
     std::mutex mu;
     hipStream_t owner[kOwnedSlots] = {};
-    int owned = 0;
+    bool taken[kOwnedSlots] = {};  // owner[i] is valid (the null stream may own a slot too)
     // this stream's counter slot; *own: the slot is the stream's alone
     int slot_of(hipStream_t s, bool* own) {
         std::lock_guard<std::mutex> g(mu);
-        for (int i = 0; i < owned; ++i)
-            if (owner[i] == s) return *own = true, i;
-        if (owned < kOwnedSlots) return owner[owned] = s, *own = true, owned++;
+        int free_slot = -1;
+        for (int i = 0; i < kOwnedSlots; ++i) {
+            if (taken[i] && owner[i] == s) return *own = true, i;
+            if (!taken[i] && free_slot < 0) free_slot = i;
+        }
+        if (free_slot >= 0) {
+            owner[free_slot] = s;
+            taken[free_slot] = true;
+            return *own = true, free_slot;
+        }
         *own = false;
         return kOwnedSlots + (int)(((uintptr_t)s >> 4) % (kSyncSlots - kOwnedSlots));
+    }
+    int taken_count() {
+        std::lock_guard<std::mutex> g(mu);
+        int c = 0;
+        for (int i = 0; i < kOwnedSlots; ++i) c += taken[i] ? 1 : 0;
+        return c;
+    }
+    void release(hipStream_t s) {
+        std::lock_guard<std::mutex> g(mu);
+        for (int i = 0; i < kOwnedSlots; ++i)
+            if (taken[i] && owner[i] == s) taken[i] = false;
     }
 };
 PhasedDevice g_phased[kMaxDevices];
@@ -1071,11 +1091,27 @@ hipError_t phased_timeouts(int dev, uint64_t* count) {
 int phased_timeline(int dev, unsigned long long* out, int cap) {
     if (dev < 0 || dev >= kMaxDevices || !g_phased[dev].tl) return 0;
     const int n = std::min(cap, g_phased[dev].cus * 8);
-    if (hipDeviceSynchronize() != hipSuccess ||
-        hipMemcpy(out, g_phased[dev].tl, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost) != hipSuccess)
-        return -1;
-    return n;
+    // on that device, after its launches in flight (as phased_timeouts): the caller's current one may differ
+    int prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    hipError_t e = hipSetDevice(dev);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess)
+        e = hipMemcpy(out, g_phased[dev].tl, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost);
+    if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
+    return e == hipSuccess ? n : -1;
 }
+
+void phased_release_stream(int dev, hipStream_t s) {
+    if (dev >= 0 && dev < kMaxDevices) g_phased[dev].release(s);
+}
+
+int phased_slot(int dev, hipStream_t s, bool* own) {
+    if (dev < 0 || dev >= kMaxDevices) return -1;
+    return g_phased[dev].slot_of(s, own);
+}
+
+int phased_owned_slots(int dev) { return dev >= 0 && dev < kMaxDevices ? g_phased[dev].taken_count() : -1; }
 
 hipError_t launch_chain(const ClientTable& t, int nc, fa_dtype in, fa_dtype outdt, const float* init, void* out,
                         int64_t head, int64_t nvec, int64_t n, bool vector_ok, const Tuning& tu, hipStream_t s) {

@@ -29,6 +29,10 @@ void fa_oracle_fill_f32(uint64_t seed, uint32_t client, uint64_t idx0, size_t n,
     for (size_t i = 0; i < n; ++i) out[i] = fa_oracle_gen_value(seed, client, idx0 + i);
 }
 
+void fa_oracle_gen_at(uint64_t seed, uint32_t client, const uint64_t* idx, size_t n, float* out) {
+    for (size_t i = 0; i < n; ++i) out[i] = fa_oracle_gen_value(seed, client, idx[i]);
+}
+
 uint16_t fa_oracle_f32_to_bf16(float f) {
     uint32_t u;
     memcpy(&u, &f, 4);

@@ -40,6 +40,8 @@ uint64_t fa_oracle_splitmix64(uint64_t z);
 float fa_oracle_gen_value(uint64_t seed, uint32_t client, uint64_t idx);
 void fa_oracle_fill_f32(uint64_t seed, uint32_t client, uint64_t idx0, size_t n, float* out);
 void fa_oracle_fill_bf16(uint64_t seed, uint32_t client, uint64_t idx0, size_t n, uint16_t* out);
+/* The generator at n arbitrary indices (sampled parity checks at full size). */
+void fa_oracle_gen_at(uint64_t seed, uint32_t client, const uint64_t* idx, size_t n, float* out);
 /* FedAvg weights w_k = n_k / sum(n), n_k uniform in [500,1500]. */
 void fa_oracle_weights(uint64_t seed, int n_clients, float* w);
 

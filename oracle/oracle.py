@@ -42,6 +42,7 @@ def lib():
         L.fa_oracle_gen_value.argtypes = [U64, U32, U64]
         L.fa_oracle_fill_f32.argtypes = [U64, U32, U64, S, P]
         L.fa_oracle_fill_bf16.argtypes = [U64, U32, U64, S, P]
+        L.fa_oracle_gen_at.argtypes = [U64, U32, P, S, P]
         L.fa_oracle_weights.argtypes = [U64, I, P]
         L.fa_oracle_fedavg_f32.argtypes = [P, P, I, S, P, P, I]
         L.fa_oracle_fedavg_bf16.argtypes = [P, P, I, S, P, P, I, I]
@@ -68,8 +69,10 @@ def gen(seed, client, n, idx0=0, dtype="f32"):
 
 def gen_at(seed, client, idx):
     """Generator values at arbitrary indices (for sampled checks at full size)."""
-    L = lib()
-    return np.array([L.fa_oracle_gen_value(seed, client, int(i)) for i in idx], np.float32)
+    idx = np.ascontiguousarray(idx, np.uint64)
+    out = np.empty(idx.size, np.float32)
+    lib().fa_oracle_gen_at(seed, client, _ptr(idx), idx.size, _ptr(out))
+    return out
 
 
 def weights(n_clients, seed=WSEED):
@@ -119,6 +122,21 @@ def fedavg_at(seed, w, idx, bf16=False):
             v = bf16_to_f32(f32_to_bf16(v))
         xs.append(v)
     return fedavg(xs, w)
+
+
+def sampled_chain(seed, w, idx, clients=None, bf16=False):
+    """The FedAvg chain at the indices `idx` only, for parity checks of full-size results: chain position k
+    holds generator client clients[k] (default k) of `seed`, rounded to bf16 first when `bf16`.
+    Returns (ref fp32, sum_k |w_k x_k| in fp64 -- the scale of the rs layout's 1e-6 tolerance)."""
+    idx = np.asarray(idx, np.uint64)
+    xs, sabs = [], np.zeros(idx.size, np.float64)
+    for k in range(len(w)):
+        v = gen_at(seed, k if clients is None else clients[k], idx)
+        if bf16:
+            v = bf16_to_f32(f32_to_bf16(v))
+        xs.append(v)
+        sabs += np.abs(np.float64(w[k]) * v.astype(np.float64))
+    return fedavg(xs, w), sabs
 
 
 def f32_to_bf16(a):

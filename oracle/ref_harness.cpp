@@ -18,7 +18,7 @@
 // Modes (all write JSON to stdout):
 //   layout  <name> <type> <start> <end> <nc>
 //   golden  <name> <type> <start> <end> <nc> <D> <seed> <wseed> <outdir> [blob_mp; -1 = every bucket <= 200k]
-//   bench-fedavg <n> <D> <threads> <reps>
+//   bench-fedavg <n> <D> <threads> <reps> [bf16]
 //   bench-literal <name> <type> <start> <end> <nc> <D> <threads> <model_part> [arith]
 #include <chrono>
 #include <cstdio>
@@ -27,6 +27,7 @@
 #include <fstream>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <torch/torch.h>
@@ -234,33 +235,53 @@ int cmd_golden(int argc, char** argv) {
 }
 
 // libtorch CPU FedAvg (acc.add_(x_k, w_k) in client order) over D synthetic
-// buckets of n fp32: the reference's arithmetic library doing the intended op.
-int cmd_bench_fedavg(char** argv) {
+// buckets of n fp32 (or bf16 with `bf16`: the fp32 accumulator takes the bf16
+// receipts as they are, type promotion widening them, and the result is rounded
+// once to bf16 inside the timed region): the reference's arithmetic library doing
+// the intended op.  The inputs are generated on all threads (a C4-sized sample is
+// 36 GB), outside the clock.
+int cmd_bench_fedavg(int argc, char** argv) {
     int64_t n = atoll(argv[2]);
     int D = atoi(argv[3]), threads = atoi(argv[4]), reps = atoi(argv[5]);
+    const bool bf16 = argc > 6 && std::string(argv[6]) == "bf16";
     at::set_num_threads(threads);
     std::vector<torch::Tensor> x(D);
     std::vector<float> w(D);
     fa_oracle_weights(7, D, w.data());
+    const double t_fill = now_s();
     for (int k = 0; k < D; ++k) {
-        x[k] = torch::empty({n}, torch::kFloat32);
-        fa_oracle_fill_f32(0x5EED, (uint32_t)k, 0, (size_t)n, x[k].data_ptr<float>());
+        x[k] = torch::empty({n}, bf16 ? torch::kBFloat16 : torch::kFloat32);
+        char* base = (char*)x[k].data_ptr();
+        std::vector<std::thread> pool;
+        for (int t = 0; t < threads; ++t)
+            pool.emplace_back([=] {
+                const int64_t a = n * t / threads, b = n * (t + 1) / threads;
+                if (bf16)
+                    fa_oracle_fill_bf16(0x5EED, (uint32_t)k, (uint64_t)a, (size_t)(b - a), (uint16_t*)base + a);
+                else
+                    fa_oracle_fill_f32(0x5EED, (uint32_t)k, (uint64_t)a, (size_t)(b - a), (float*)base + a);
+            });
+        for (auto& th : pool) th.join();
     }
+    const double fill_s = now_s() - t_fill;
     auto acc = torch::zeros({n}, torch::kFloat32);
+    torch::Tensor out;
     double best = 1e30, total = 0;
     for (int r = 0; r < reps + 1; ++r) {
         double t0 = now_s();
         acc.zero_();
         for (int k = 0; k < D; ++k) acc.add_(x[k], w[k]);
+        if (bf16) out = acc.to(torch::kBFloat16);
         double dt = now_s() - t0;
         if (r == 0) continue;  // warm-up
         total += dt;
         if (dt < best) best = dt;
     }
-    double avg = total / reps, bytes = (double)D * n * 4;
-    printf("{\"mode\":\"fedavg\",\"n\":%lld,\"D\":%d,\"threads\":%d,\"reps\":%d,\"avg_s\":%.6f,\"best_s\":%.6f,"
-           "\"gib_s\":%.4f,\"checksum\":%.9g}\n",
-           (long long)n, D, threads, reps, avg, best, bytes / avg / (1ull << 30), acc.sum().item<double>());
+    double avg = total / reps, bytes = (double)D * n * (bf16 ? 2 : 4);
+    printf("{\"mode\":\"fedavg\",\"dtype\":\"%s\",\"n\":%lld,\"D\":%d,\"threads\":%d,\"reps\":%d,\"avg_s\":%.6f,"
+           "\"best_s\":%.6f,\"gib_s\":%.4f,\"fill_s\":%.3f,\"checksum\":%.9g}\n",
+           bf16 ? "bf16" : "f32", (long long)n, D, threads, reps, avg, best, bytes / avg / (1ull << 30), fill_s,
+           acc.sum().item<double>());
     return 0;
 }
 
@@ -321,7 +342,7 @@ int main(int argc, char** argv) {
     } else if (mode == "golden" && argc >= 11) {
         rc = cmd_golden(argc, argv);
     } else if (mode == "bench-fedavg" && argc >= 6) {
-        rc = cmd_bench_fedavg(argv);
+        rc = cmd_bench_fedavg(argc, argv);
     } else if (mode == "bench-literal" && argc >= 10) {
         rc = cmd_bench_literal(argc, argv);
     } else {

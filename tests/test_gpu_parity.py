@@ -14,7 +14,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN
+from conftest import GOLDEN, ROOT
 
 pytestmark = pytest.mark.gpu
 
@@ -705,64 +705,178 @@ def test_buckets_past_32bit_indices(fa, O, torch_gpu, in_bf16, n, D, walk):
         torch.cuda.empty_cache()
 
 
-def test_phased_streams_sharing_a_counter(fa, O, torch_gpu):
-    """Two streams whose phased launches count on the same counter slot (stream handles are hashed onto
-    64 slots), launched so they overlap: every result stays bit-exact, and a later launch on either
-    stream runs as fast as before (no counter is left skewed)."""
-    torch = torch_gpu
-    before = fa.get_tuning()
-    try:
-        fa.set_tuning(walk=5)
-        n, D = 30_000_005, 4  # 1.3 phases of the default f32 form
-        w = O.weights(D)
-        sets = []
-        for s in range(2):
-            clients = [filled(fa, torch, n, False, 0x5EED + s, k) for k in range(D)]
-            sets.append((clients, torch.empty(n, dtype=torch.float32, device="cuda")))
-        ref = []
-        for clients, out in sets:
-            fa.reduce_device(clients, w, n, fa.F32, out, fa.F32)
-            torch.cuda.synchronize()
-            ref.append(out.clone())
-        by_slot = {}
-        streams = []
-        pair = None
-        for _ in range(65):  # pigeonhole: two of 65 streams share one of the 64 slots
-            st = torch.cuda.Stream()
-            streams.append(st)
-            slot = (st.cuda_stream >> 4) % 64
-            if slot in by_slot:
-                pair = (by_slot[slot], st)
-                break
-            by_slot[slot] = st
-        assert pair is not None
+# Run in a fresh child process, so that which counter slot a stream gets does not depend on what earlier tests
+# left: the first 48 streams that launch the phased kernel in a process own a slot each (until their context is
+# destroyed), later ones share the 16 hashed slots (fa_kernels.hip, PhasedDevice::slot_of).
+_SHARED_SLOT_CHILD = r"""
+import json, sys
+import numpy as np
+import torch
+sys.path.insert(0, %(tests)r)
+sys.path.insert(0, %(oracle)r)
+from conftest import load_pkg
+import oracle as O
+fa = load_pkg()
+fa.lib()
+fa.set_tuning(walk=5)
+n, D = 30_000_005, 4  # 1.3 phases of the default f32 form: a meeting, so both streams count on the slot
+assert fa.plan_chain(fa.F32, fa.F32, n, D)[0] == fa.PLAN_PHASED
+assert fa.phased_owned_slots(0) == 0
+w = O.weights(D)
+sets = []
+for s in range(2):
+    clients = []
+    for k in range(D):
+        t = torch.empty(n, dtype=torch.float32, device="cuda")
+        fa.fill_uniform(t, n, fa.F32, 0x5EED + s, k)
+        clients.append(t)
+    sets.append((clients, torch.empty(n, dtype=torch.float32, device="cuda")))
+# distinct HIP streams: torch.cuda.Stream() hands out its pool's 32 streams round-robin, so it cannot give 65
+import ctypes
+hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime torch already loaded
 
-        def median_ms(st):
-            evs = []
-            clients, out = sets[0]
-            for _ in range(7):
-                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                a.record(st)
-                fa.reduce_device(clients, w, n, fa.F32, out, fa.F32, stream=st)
-                b.record(st)
-                evs.append((a, b))
-            torch.cuda.synchronize()
-            return float(np.median([a.elapsed_time(b) for a, b in evs[2:]]))
 
-        t0 = median_ms(pair[0])
-        for _ in range(6):  # overlapping launches on the two streams
-            for k in range(2):
-                clients, out = sets[k]
-                with torch.cuda.stream(pair[k]):
-                    out.zero_()
-                fa.reduce_device(clients, w, n, fa.F32, out, fa.F32, stream=pair[k])
-        torch.cuda.synchronize()
-        for k in range(2):
-            assert torch.equal(sets[k][1].view(torch.int32), ref[k].view(torch.int32))
-        t1, t2 = median_ms(pair[0]), median_ms(pair[1])
-        assert max(t1, t2) < 1.5 * t0 + 0.05, (t0, t1, t2)
-    finally:
-        fa.set_tuning(walk=before["walk"])
+def new_stream():
+    p = ctypes.c_void_p()
+    assert hip.hipStreamCreateWithFlags(ctypes.byref(p), 1) == 0  # hipStreamNonBlocking
+    return torch.cuda.ExternalStream(p.value)
+
+
+streams, hashed, pair = [], {}, None
+while pair is None:  # 48 owned, then pigeonhole: two of 17 more streams share one of the 16 hashed slots
+    st = new_stream()
+    streams.append(st)
+    slot, own = fa.phased_slot(st)
+    assert own == (len(streams) <= 48) and (slot < 48) == own, (len(streams), slot, own)
+    if not own:
+        if slot in hashed:
+            pair = (hashed[slot], st)
+        hashed[slot] = st
+    assert len(streams) <= 48 + 17
+assert fa.phased_owned_slots(0) == 48 and fa.phased_slot(pair[0]) == fa.phased_slot(pair[1])
+ref = []
+for clients, out in sets:  # each set alone, on an owned stream
+    with torch.cuda.stream(streams[0]):
+        fa.reduce_device(clients, w, n, fa.F32, out, fa.F32, stream=streams[0])
+    torch.cuda.synchronize()
+    ref.append(out.clone())
+idx = np.unique(np.concatenate([[0, n - 1], np.random.default_rng(1).integers(0, n, 1024)]))
+for s in range(2):  # the lone results against the oracle
+    assert np.array_equal(ref[s].cpu().numpy()[idx].view(np.uint32),
+                          O.sampled_chain(0x5EED + s, w, idx)[0].view(np.uint32))
+
+def median_ms(st):
+    evs = []
+    clients, out = sets[0]
+    for _ in range(7):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        fa.reduce_device(clients, w, n, fa.F32, out, fa.F32, stream=st)
+        b.record(st)
+        evs.append((a, b))
+    torch.cuda.synchronize()
+    return float(np.median([a.elapsed_time(b) for a, b in evs[2:]]))
+
+t0 = median_ms(pair[0])
+for _ in range(6):  # overlapping launches of the two sets on the two streams that share the slot
+    for k in range(2):
+        clients, out = sets[k]
+        with torch.cuda.stream(pair[k]):
+            out.zero_()
+        fa.reduce_device(clients, w, n, fa.F32, out, fa.F32, stream=pair[k])
+torch.cuda.synchronize()
+same = [bool(torch.equal(sets[k][1].view(torch.int32), ref[k].view(torch.int32))) for k in range(2)]
+t1, t2 = median_ms(pair[0]), median_ms(pair[1])
+print(json.dumps({"same": same, "t0": t0, "t1": t1, "t2": t2, "streams": len(streams),
+                  "timeouts": fa.phased_timeouts(0)}))
+"""
+
+
+def _child(script, timeout=180, env=None):
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, "-c", script % {"tests": os.path.join(ROOT, "tests"),
+                                                        "oracle": os.path.join(ROOT, "oracle")}],
+                       capture_output=True, text=True, timeout=timeout, env=dict(os.environ, **(env or {})))
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_phased_streams_sharing_a_counter(fa, torch_gpu):
+    """Two streams forced onto one hashed counter slot (a fresh process: 48 streams take the owned slots, then
+    two of the next 17 share one of the 16 hashed ones), launched so they overlap: both results stay bit-exact
+    with each set reduced alone (itself checked against the oracle), and a later launch on either stream runs
+    as fast as before (no counter is left skewed)."""
+    r = _child(_SHARED_SLOT_CHILD)
+    assert r["same"] == [True, True], r
+    assert max(r["t1"], r["t2"]) < 1.5 * r["t0"] + 0.05, r
+    assert r["streams"] <= 65
+
+
+_RELEASE_CHILD = r"""
+import json, sys
+import numpy as np
+import torch
+sys.path.insert(0, %(tests)r)
+from conftest import load_pkg
+fa = load_pkg()
+fa.lib()
+n, D = 4 << 20, 16  # below one phase with 16 clients: one sized phase of the phased kernel
+assert fa.plan_chain(fa.F32, fa.F32, n, D)[0] == fa.PLAN_PHASED
+w = np.full(D, 1.0 / D, np.float32)
+counts = []
+for i in range(60):  # more contexts than owned slots
+    with fa.Aggregator(1) as agg:
+        agg.define(1, n, fa.F32, fa.F32, D, fa.FEDAVG)
+        for k in range(D):
+            fa.fill_uniform(agg.slot(1, 0, k)[0], n, fa.F32, 0x5EED, k)
+        agg.reduce(1, w)  # on the context's compute stream: it takes an owned slot
+        agg.sync()
+        during = fa.phased_owned_slots(0)
+    counts.append((during, fa.phased_owned_slots(0)))
+import ctypes
+p = ctypes.c_void_p()
+assert ctypes.CDLL("libamdhip64.so.7").hipStreamCreateWithFlags(ctypes.byref(p), 1) == 0  # a new HIP stream
+print(json.dumps({"counts": counts, "fresh_stream_owns": fa.phased_slot(p.value)[1]}))
+"""
+
+
+def test_destroyed_context_releases_its_counter_slot(fa, torch_gpu):
+    """fa_destroy gives its streams' owned counter slots back: 60 contexts one after another each hold one
+    owned slot while alive and none after, so a stream created after them still gets a slot of its own."""
+    r = _child(_RELEASE_CHILD)
+    assert all(c == [1, 0] for c in r["counts"]), r["counts"]
+    assert r["fresh_stream_owns"]
+
+
+_TIMELINE_CHILD = r"""
+import ctypes, json, sys
+import numpy as np
+import torch
+sys.path.insert(0, %(tests)r)
+from conftest import load_pkg
+fa = load_pkg()
+fa.lib()
+n, D = 30_000_005, 4
+assert fa.plan_chain(fa.F32, fa.F32, n, D)[0] == fa.PLAN_PHASED
+clients = [torch.zeros(n, dtype=torch.float32, device="cuda:0") for _ in range(D)]
+out = torch.empty(n, dtype=torch.float32, device="cuda:0")
+fa.reduce_device(clients, np.full(D, 0.25, np.float32), n, fa.F32, out, fa.F32)  # enqueued, not synchronized
+buf = (ctypes.c_ulonglong * 4096)()
+L = fa.lib()
+got = L.fa_diag_phased_timeline(0, buf, 4096)  # synchronizes device 0 itself before the copy
+starts = [buf[8 * i] for i in range(max(0, got) // 8)]
+print(json.dumps({"words": got, "stamped": sum(1 for x in starts if x), "none": L.fa_diag_phased_timeline(63, buf, 8)}))
+"""
+
+
+def test_phased_timeline_reads_its_own_device(fa, torch_gpu):
+    """fa_diag_phased_timeline (FA_TIMELINE=1, tools/timeline.py) synchronizes and copies on the device it is
+    asked about, not the caller's current one: right after an enqueued phased launch on device 0 every
+    workgroup's start stamp is there (8 words per CU); a device that never ran one reports 0 words."""
+    r = _child(_TIMELINE_CHILD, env={"FA_TIMELINE": "1"})
+    assert r["words"] > 0 and r["words"] % 8 == 0 and r["stamped"] == r["words"] // 8, r
+    assert r["none"] == 0
 
 
 def test_phased_meeting_timeouts_counter(fa, O, torch_gpu):

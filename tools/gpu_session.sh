@@ -23,6 +23,16 @@ for s in $STEPS; do
     test)
         timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rfs --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
         rc=$?; tail -5 "$OUT/pytest_gpu.log"; ok_or_fail $rc test ;;
+    tk)  # a subset of the GPU suite: TK = a -k expression, TKPATH = test files (default tests)
+        timeout -k 10 600 python -u -m pytest -m gpu -x -v -rfs --timeout 240 --timeout-method thread -k "${TK:-}" ${TKPATH:-tests} > "$OUT/pytest_tk.log" 2>&1
+        rc=$?; tail -8 "$OUT/pytest_tk.log"; ok_or_fail $rc tk ;;
+    ctx)  # the in-process multi-GPU children at the GPUs this box has, each with its parity object
+        for A in "range northstar" "rs northstar" "rs c4" "range c5 --h2d"; do
+            set -- $A
+            H=""; [ "${3:-}" = "--h2d" ] && H="--h2d --steps 2 --warmup 1"
+            timeout -k 10 240 python bench.py --ctx-multi $1 --workload $2 $H >> "$OUT/ctx.jsonl" 2>> "$OUT/ctx.err"
+            rc=$?; tail -c 700 "$OUT/ctx.jsonl"; echo; ok_or_fail $rc "ctx $A"
+        done ;;
     smoke)
         timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
         rc=$?; tail -3 "$OUT/smoke.log"; ok_or_fail $rc smoke ;;
