@@ -183,6 +183,39 @@ def test_retransmitted_receipts_count_once(torch_gpu, extra):
             agg.kill()
 
 
+@pytest.mark.parametrize("extra", [[], ["--eager"], ["--mode", "literal"]])
+def test_late_duplicates_of_earlier_rounds_are_dropped(torch_gpu, extra):
+    """Owner 2 re-sends its previous round's receipts during the next round, once before and once after the
+    current ones (fake_owners --retransmit-late).  The wire has no round number; fa_aggregator tells them
+    apart by t_start (stamped when the owner sends, network_layer.cpp:761) and by content, so a late copy
+    neither counts as the owner's receipt nor replaces the newer one: every reply of every round stays
+    bit-exact against the oracle over THIS round's values, and the log names the dropped copies
+    (aggregator.cpp:59-92 would reduce the stale parameters without a word)."""
+    D, rounds, base = 4, 3, pick_base()
+    agg = subprocess.Popen([AGG, "-i", "-1", "-d", str(D), "-c", "1", "--rounds", str(rounds), "--port-base",
+                            str(base), "--stall-report", "5", "--receipt-timeout", "30"] + extra,
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        time.sleep(0.5)
+        r = subprocess.run([OWNERS, "--blobs", os.path.join(GOLDEN, "lenet5_c1"), "--parts", "1,2,3", "-d", str(D),
+                            "-c", "1", "--rounds", str(rounds), "--port-base", str(base), "--model-name", "2",
+                            "--start", "6", "--end", "1", "--retransmit-late", "2", "--reply-timeout", "60"]
+                           + (["--mode", "literal"] if "literal" in extra else []),
+                           capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res = json.loads(r.stdout.strip().splitlines()[-1])
+        assert res["ok"] and res["rounds"] == rounds
+        out, err = agg.communicate(timeout=60)
+        assert agg.returncode == 0, err[-2000:]
+        lines = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+        assert len(lines) == rounds
+        assert lines[-1]["stale_dropped"] >= 1 and "stale part" in err, err[-2000:]
+        assert lines[0]["stale_dropped"] == 0  # round 0 has no earlier round to be late from
+    finally:
+        if agg.poll() is None:
+            agg.kill()
+
+
 @pytest.mark.parametrize("extra", [[], ["--eager"], ["--mode", "literal"], ["--layout", "rs", "--rs-chunks", "3"]])
 def test_bf16_parts_over_tcp(torch_gpu, tmp_path, extra):
     """BASELINE config C3's dtype through the drop-in process: owners send bf16 model parts

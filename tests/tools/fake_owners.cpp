@@ -8,7 +8,8 @@
 //
 //   fa_fake_owners --blobs DIR --parts 1,2,3 -d D -c C [--rounds R] [--mode fedavg|literal]
 //                  [--port-base P] [--model-name N --model-type T --start S --end E] [--seed X]
-//                  [--drop-owner K [--drop-phase P]] [--retransmit K] [--reply-timeout S]
+//                  [--drop-owner K [--drop-phase P]] [--retransmit K] [--retransmit-late K]
+//                  [--reply-timeout S]
 //                  [--sequential]   (owners send at once, one connection each, unless --sequential
 //                                    or --mode literal, whose result depends on the arrival order)
 // Prints one JSON line: {"ok": bool, "rounds": R, "checked_elems": ..., "round_ms": [...]}.
@@ -69,6 +70,7 @@ int main(int argc, char** argv) {
     bool concurrent = true;
     int drop_owner = -1, drop_phase = 1;  // failure injection: owner K never sends its phase-P receipts
     int retransmit = -1;                  // owner K sends every receipt twice (a retransmission)
+    int retransmit_late = -1;             // owner K re-sends its previous round's receipts during this round
     long reply_timeout_ms = 600000;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
@@ -90,6 +92,7 @@ int main(int argc, char** argv) {
         else if (a == "--drop-owner") drop_owner = std::atoi(v), ++i;
         else if (a == "--drop-phase") drop_phase = std::atoi(v), ++i;
         else if (a == "--retransmit") retransmit = std::atoi(v), ++i;
+        else if (a == "--retransmit-late") retransmit_late = std::atoi(v), ++i;
         else if (a == "--reply-timeout") reply_timeout_ms = (long)(std::atof(v) * 1000), ++i;
         else {
             std::cerr << "unknown argument " << a << "\n";
@@ -161,6 +164,7 @@ int main(int argc, char** argv) {
     bool ok = true;
     size_t checked = 0;
     std::vector<long> round_ms;
+    std::map<int, std::vector<std::shared_ptr<const Bytes>>> prev_frames;  // the previous round's, per mp
     auto collect = [&](int want, std::vector<Receipt>* got) {
         const long t_end = now_ms() + reply_timeout_ms;
         while ((int)got->size() < want && now_ms() < t_end) {
@@ -222,8 +226,14 @@ int main(int argc, char** argv) {
                 for (auto& p : parts) {
                     if ((phase == 1) != (p.mp == 1)) continue;
                     if (k == drop_owner && phase == drop_phase) continue;  // this owner "died"
+                    // --retransmit-late: the previous round's receipt of this bucket arrives late, once before
+                    // and once after this round's (a delayed duplicate; the aggregator must drop both copies,
+                    // whichever order they land in)
+                    const bool late = k == retransmit_late && prev_frames.count(p.mp);
+                    if (late) by_owner[k].push_back(prev_frames[p.mp][k]);
                     by_owner[k].push_back(frames[p.mp][k]);
                     if (k == retransmit) by_owner[k].push_back(frames[p.mp][k]);  // the same receipt again
+                    if (late) by_owner[k].push_back(prev_frames[p.mp][k]);
                     ++sent;  // one reply per bucket and destination, retransmission or not
                 }
             if (concurrent) {  // every owner is its own process in the reference: they send at once
@@ -254,6 +264,7 @@ int main(int argc, char** argv) {
             }
             for (auto& r : got) replies.push_back(std::move(r));
         }
+        prev_frames = frames;
         round_ms.push_back((long)std::llround(
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count()));
         for (auto& r : replies) {

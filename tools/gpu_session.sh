@@ -82,9 +82,12 @@ for s in $STEPS; do
             python3 tools/rounds.py 20 round_c2,round_c3 > "$OUT/rounds_prof.jsonl" 2> "$OUT/rounds_prof.err"
         rc=$?; tail -2 "$OUT/rounds_prof.err"; ok_or_fail $rc rounds_prof ;;
     markers)  # roctx ranges of the host entries (fa_submit / fa_finalize / fa_copy_output) beside kernels and copies
-        timeout -k 10 300 rocprofv3 --marker-trace --kernel-trace --memory-copy-trace --stats --output-format csv \
-            -d "$OUT/markers" -o run -- python3 tools/h2d_rate.py 8 24 1 > "$OUT/markers.jsonl" 2> "$OUT/markers.err"
-        rc=$?; tail -2 "$OUT/markers.err"; ok_or_fail $rc markers ;;
+        # D2H copies are HIP blit kernels here (kernel trace: __amd_rocclr_copyBuffer), H2D copies SDMA
+        # (memory-copy trace); tools/copy_stats.py puts both directions in one table
+        H2D_MODES=${H2D_MODES:-pinned_io} timeout -k 10 300 rocprofv3 --marker-trace --kernel-trace --memory-copy-trace \
+            --stats --output-format csv -d "$OUT/markers" -o run -- python3 tools/h2d_rate.py 8 24 3 > "$OUT/markers.jsonl" 2> "$OUT/markers.err"
+        rc=$?; tail -2 "$OUT/markers.err"; ok_or_fail $rc markers
+        python3 tools/copy_stats.py "$OUT/markers" "$OUT/markers_copy_stats.csv" > "$OUT/markers_breakdown.json" ;;
     e2e)
         timeout -k 10 900 python tools/e2e_bench.py 4 3 > "$OUT/e2e_bench.json" 2> "$OUT/e2e_bench.err"
         rc=$?; cat "$OUT/e2e_bench.json"; tail -3 "$OUT/e2e_bench.err"; ok_or_fail $rc e2e ;;

@@ -42,6 +42,11 @@ def main():
         t.numpy()[:] = x
         pinned.append(t)
     out = np.empty(n, np.float32)
+    # modes: pageable (fa_submit / fa_finalize of numpy arrays), pinned (fa_submit_pinned, pageable result),
+    # pinned_io (pinned receipts and the result DMA'd straight into pinned memory: fa_finalize_gather with
+    # FA_HOST_PINNED, the drop-in aggregator's own path, host/aggregator_main.cpp)
+    modes = os.environ.get("H2D_MODES", "pageable,pinned").split(",")
+    out_pinned = fa.PinnedBuffer(n * 4) if "pinned_io" in modes else None
     res = {"D": D, "n": n, "bytes_per_client": n * 4, "distinct_host_buffers": len(pageable), "shards": shards}
     if shards == 1:
         ctx = fa.Aggregator(1)
@@ -52,16 +57,19 @@ def main():
         res["shared_device"] = True
     with ctx as agg:
         agg.define(1, n, fa.F32, fa.F32, D, fa.FEDAVG)
-        for mode in ("pageable", "pinned"):
+        for mode in modes:
             times = []
             for r in range(rounds + 1):
                 t0 = time.perf_counter()
                 for k in range(D):
-                    if mode == "pinned":
+                    if mode in ("pinned", "pinned_io"):
                         agg.submit(1, k, pinned[k % len(pinned)].numpy(), w[k], pinned=True)
                     else:
                         agg.submit(1, k, pageable[k % len(pageable)], w[k])
-                agg.finalize(1, out)
+                if mode == "pinned_io":
+                    agg.finalize_gather(1, [out_pinned.view(np.float32, count=n)], pinned=True)
+                else:
+                    agg.finalize(1, out)
                 times.append(time.perf_counter() - t0)
             t = min(times[1:])
             res[mode] = {"round_s": round(t, 4), "GiB_s_input": round(D * n * 4 / t / 2**30, 2),
@@ -79,6 +87,14 @@ def main():
         torch.cuda.synchronize()
         ms = min(a.elapsed_time(b) for a, b in ev[1:])
         res["device_resident"] = {"round_ms": round(ms, 4), "GiB_s_input": round(D * n * 4 / ms / 1e-3 / 2**30, 1)}
+        agg.sync()
+    # Drain before exit: the context is destroyed (fa_destroy synchronizes its streams), then the whole device,
+    # and the profiler gets a moment to deliver its last copy records (a marker trace of this tool lost its
+    # DEVICE_TO_HOST rows to "completion callbacks were not delivered" at exit, gpurun_out r03s46).
+    torch.cuda.synchronize()
+    if out_pinned is not None:
+        out_pinned.close()
+    time.sleep(float(os.environ.get("H2D_EXIT_DRAIN_S", "2")))
     print(json.dumps(res))
 
 
