@@ -1,0 +1,77 @@
+"""GPU: bench.py's own legs on the one-GPU box, each ending with its parity object (verdict r03 #1).
+
+* A workload held in range pieces (forced small with FA_PIECE_SPLIT / FA_PIECE_SPAN, as C5's 128 x 1 GiB
+  is on one GPU) prints its line: read_stream_peak walks the pieces instead of asking fa_bucket_slot for a
+  contiguous slot, and the client-sharded layout builds contiguous slots.
+* `--ctx-multi range|rs` (the in-process multi-GPU children the N = 1 run starts on a node with several
+  GPUs) and `--gpus 2` (two ranks sharing the GPU over gloo: the driver's N > 1 launch, rehearsed) carry
+  a passing parity object on the main line and on every secondary, so the first run on an 8-GPU node is
+  also the first parity test of its reduce-scatter and range legs.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def run_bench(args, env=None, timeout=240):
+    r = subprocess.run([sys.executable, BENCH] + args, capture_output=True, text=True, timeout=timeout, cwd=ROOT,
+                       env=dict(os.environ, **(env or {})))
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def ok(p, samples=1024):
+    assert p and p["ok"] and p["mismatches"] == 0 and p["samples"] >= samples, p
+
+
+PIECES = {"FA_PIECE_SPLIT": "0", "FA_PIECE_SPAN": str(256 << 20)}  # ns_w8's 1 GiB of slots -> 4 pieces
+
+
+@pytest.mark.parametrize("layout", ["range", "rs"])
+def test_pieced_workload_prints_its_line(fa, torch_gpu, layout):
+    line = run_bench(["--workload", "ns_w8", "--layout", layout, "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
+                      "--no-secondary", "--no-live-pmc"], env=PIECES)
+    ok(line["parity"])
+    assert line["value"] > 0 and line["roofline"]["phased_meeting_timeouts"] == 0
+    if layout == "range":
+        assert line["roofline"]["read_stream_peak"] > 0
+        assert line["parity"]["check"].startswith("bit-exact")
+
+
+@pytest.mark.parametrize("layout", ["range", "rs"])
+def test_ctx_multi_child_carries_parity(fa, torch_gpu, layout):
+    res = run_bench(["--ctx-multi", layout, "--workload", "ns_w8", "--steps", "3", "--warmup", "1"])
+    ok(res["parity"])
+    assert res["gpus"] >= 1 and len(res["parity"]["per_gpu_samples"]) == res["gpus"]
+    assert all(s >= 1024 for s in res["parity"]["per_gpu_samples"])
+
+
+def test_ctx_multi_host_inclusive_parity(fa, torch_gpu):
+    """--h2d: every client submitted from pinned host memory (client k from buffer k % 8) and the result
+    finalized into host memory; checked against the oracle's chain with that client map."""
+    res = run_bench(["--ctx-multi", "range", "--workload", "ns_w8", "--h2d", "--steps", "2", "--warmup", "1"])
+    ok(res["parity"])
+    assert res["host_inclusive"]
+
+
+def test_two_rank_rehearsal_parity_everywhere(fa, torch_gpu):
+    """The driver's N > 1 launch rehearsed on one GPU (bench.py spawns 2 ranks, gloo): the main range line
+    and the weak-range, rs and chain secondaries each carry a parity object summed over both ranks."""
+    line = run_bench(["--gpus", "2", "--workload", "ns_w8", "--steps", "3", "--warmup", "1", "--no-live-pmc"],
+                     timeout=300)
+    assert line["n_gpus"] == 2
+    ok(line["parity"], 2 * 1024)
+    assert line["parity"]["ranks"] == 2
+    for leg in ("weak_range", "rs", "chain"):
+        p = line["secondary"][leg]["parity"]
+        ok(p, 2 * 1024)
+        assert p["ranks"] == 2
+    assert line["secondary"]["rs"]["parity"]["max_err_over_bound"] < 1.0
