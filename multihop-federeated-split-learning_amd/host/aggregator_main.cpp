@@ -38,6 +38,7 @@
 #include "archive.h"
 #include "fedavg/fa.h"
 #include "net.h"
+#include "receipts.h"
 
 using namespace fahost;
 
@@ -178,84 +179,17 @@ public:
     }
     ~Aggregator() { fa_destroy(ctx_); }
 
-    // Stale receipts across rounds.  The wire carries no round number, but every receipt carries t_start,
-    // stamped on its owner's clock when the owner's sender thread sends it (network_layer.cpp:761), and an
-    // owner's sends follow the protocol's order: its part 1 of round r+1 only after the phase-2 replies of
-    // round r, which go out after its phase-2 receipts of round r arrived; its phase-2 receipts only after the
-    // phase-1 reply, i.e. after its part 1 (data_owner.cpp:224-253).  So, per owner:
-    //   * the floor of a phase = the newest t_start among the owner's receipts the previous phase reduced;
-    //     a receipt sent before it (t_start < floor) belongs to an earlier phase: stale;
-    //   * t_start == floor (one millisecond) is decided by content: a byte-for-byte copy of a receipt the
-    //     last two phases already reduced (fingerprint below) is stale, anything else is new;
-    //   * within a phase, a second receipt of (owner, bucket) sent before the one already taken does not
-    //     replace it (the newest wins, whichever arrives last).
-    // A stale receipt is dropped and named in the log; it never counts and never touches a slot.  (A sender
-    // clock stepped backwards by more than a round could make a genuine receipt look stale: the stall report
-    // then names its owner.)
-    static uint64_t fingerprint(const Receipt& r) {
-        // FNV-1a over the length and 1024 evenly spaced 8-byte words of the archive: two rounds' receipts of
-        // a bucket differ in (nearly) every parameter, so sampled words tell them apart; a copy matches.
-        uint64_t h = 1469598103934665603ull ^ (uint64_t)r.blob_len;
-        const uint8_t* b = r.blob();
-        const size_t words = r.blob_len / 8;
-        const size_t step = std::max<size_t>(1, words / 1024);
-        for (size_t i = 0; i < words; i += step) {
-            uint64_t v;
-            std::memcpy(&v, b + i * 8, 8);
-            h = (h ^ v) * 1099511628211ull;
-        }
-        for (size_t i = words * 8; i < r.blob_len; ++i) h = (h ^ b[i]) * 1099511628211ull;
-        return h;
-    }
-
-    // Empty when the receipt is current; else why it is stale.
-    std::string stale(const Receipt& r, uint64_t fp) const {
-        auto fl = floor_.find(r.client_id);
-        if (fl != floor_.end()) {
-            if (r.t_start < fl->second)
-                return "sent at " + std::to_string(r.t_start) + ", before its owner's receipts of the previous phase (" +
-                       std::to_string(fl->second) + ")";
-            auto c = consumed_.find(r.client_id);
-            if (r.t_start == fl->second && c != consumed_.end() &&
-                std::find(c->second.begin(), c->second.end(), fp) != c->second.end())
-                return "a copy of a receipt an earlier phase already reduced";
-        }
-        auto a = accepted_.find({r.client_id, r.model_part});
-        if (a != accepted_.end() && r.t_start < a->second.first)
-            return "sent at " + std::to_string(r.t_start) + ", before the receipt already taken (" +
-                   std::to_string(a->second.first) + ")";
-        return std::string();
-    }
-
-    // A phase's buckets are reduced: its receipts set every owner's floor for the next phase, and their
-    // fingerprints join the last two phases' (what a late copy is matched against).
-    void end_phase() {
-        std::map<int, long> fl;
-        std::map<int, std::vector<uint64_t>> fps;
-        for (auto& kv : accepted_) {
-            const int owner = kv.first.first;
-            auto it = fl.find(owner);
-            fl[owner] = it == fl.end() ? kv.second.first : std::max(it->second, kv.second.first);
-            fps[owner].push_back(kv.second.second);
-        }
-        for (auto& kv : fl) floor_[kv.first] = kv.second;
-        for (auto& kv : fps) {
-            auto& prev = last_phase_fps_[kv.first];
-            std::vector<uint64_t> both = prev;
-            both.insert(both.end(), kv.second.begin(), kv.second.end());
-            consumed_[kv.first] = both;
-            prev = kv.second;
-        }
-        accepted_.clear();
-    }
+    // Stale receipts across rounds (host/receipts.h): a receipt its owner sent before its receipts of the
+    // previous phase, or a copy of one already reduced, is dropped -- never counted, never in a slot.
+    void end_phase() { ledger_.end_phase(); }
 
     // Consumes one receipt of bucket `mp` into its client slot.  Returns whether it is the first receipt of
     // this (owner, bucket) in the round: a retransmission replaces the slot's contents (the newest one wins,
     // as a second torch::load would) but is not another receipt -- the phase waits for D distinct owners.
     // A stale receipt (above) is dropped: returns false without touching the slot.
     bool absorb(const Receipt& r) {
-        const uint64_t fp = fingerprint(r);
-        const std::string why = stale(r, fp);
+        const uint64_t fp = archive_fingerprint(r.blob(), r.blob_len);
+        const std::string why = ledger_.stale(r.client_id, r.model_part, r.t_start, fp);
         if (!why.empty()) {
             std::cerr << "[aggregator] stale part " << r.model_part << " from owner " << r.client_id << " (" << why
                       << "): dropped\n";
@@ -306,7 +240,7 @@ public:
             FA_CHECK(fa_submit(ctx_, r.model_part, slot, flat.data(), weight_of(r.client_id)));
         }
         b.bytes_in += r.blob_len;
-        accepted_[{r.client_id, r.model_part}] = {r.t_start, fp};
+        ledger_.accept(r.client_id, r.model_part, r.t_start, fp);
         const bool first = b.arrived.insert(r.client_id).second;
         b.last = r;  // template of the reply: the last receipt (its buffers travel back, as in the reference)
         st_.absorb_s += secs_since(t0);
@@ -448,12 +382,7 @@ private:
     std::vector<char> claimed_;  // slot -> an arrived client holds it
     std::vector<int> expected_;  // the data owners' ids in slot order
     Stats st_;
-    // stale-receipt state (stale() above): per owner the t_start floor of the current phase, the
-    // fingerprints of the last two phases' receipts and of the last phase's alone, and this phase's
-    // accepted (t_start, fingerprint) per (owner, bucket)
-    std::map<int, long> floor_;
-    std::map<int, std::vector<uint64_t>> consumed_, last_phase_fps_;
-    std::map<std::pair<int, int>, std::pair<long, uint64_t>> accepted_;
+    ReceiptLedger ledger_;
     unsigned long long stale_dropped_ = 0;
 };
 
@@ -528,8 +457,8 @@ int main(int argc, char** argv) {
         // (data_owner.cpp:228-245), which goes out after phase 1 ends, and its next part 1 only after every
         // phase-2 reply, which goes out after phase 2 ends.  So it is ignored (named in the log), never carried
         // into a later phase, where it would stand for a receipt its owner has not sent yet.  A late copy of
-        // the SAME phase's bucket from an earlier round is caught by its t_start (Aggregator::stale) and
-        // dropped; the round line counts them (stale_dropped).
+        // the SAME phase's bucket from an earlier round is caught by its t_start (ReceiptLedger) and
+        // dropped (host/receipts.h); the round line counts them (stale_dropped).
         auto t0 = std::chrono::steady_clock::now();
         int received = 0;
         while (received < o.data_owners) {

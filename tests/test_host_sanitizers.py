@@ -59,3 +59,18 @@ def test_network_layer_under_tsan():
                            capture_output=True, text=True, timeout=300, env=env)
         assert r.returncode == 0, r.stderr[-4000:]
         assert json.loads(r.stdout.strip().splitlines()[-1])["ok"]
+
+
+def test_receipt_ledger_under_asan_ubsan():
+    """fa_aggregator's receipt ledger (host/receipts.h): late copies of earlier rounds, before and after the
+    current receipt, in both phases, dropped; copies at the floor's millisecond decided by content; a frozen
+    part resent later and a retransmission of the current receipt kept (tests/tools/receipts_selftest.cpp)."""
+    for exe in ("receipts_selftest", "receipts_selftest_asan"):
+        if exe == "receipts_selftest":
+            subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "tools")], capture_output=True, timeout=600,
+                           check=True)
+        r = subprocess.run([os.path.join(BIN, exe)], capture_output=True, text=True, timeout=60,
+                           env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1"))
+        assert r.returncode == 0, r.stderr[-2000:]
+        res = json.loads(r.stdout.strip().splitlines()[-1])
+        assert res["failed"] == 0 and res["checks"] >= 50
