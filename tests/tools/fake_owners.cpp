@@ -100,6 +100,10 @@ int main(int argc, char** argv) {
         }
     }
     if (mode == "literal") concurrent = false;
+    if (retransmit_late >= D || retransmit >= D || drop_owner >= D) {
+        std::cerr << "owner index out of range (-d " << D << ")\n";
+        return 2;
+    }
     // template archives
     std::vector<Part> parts;
     {
@@ -264,7 +268,14 @@ int main(int argc, char** argv) {
             }
             for (auto& r : got) replies.push_back(std::move(r));
         }
-        prev_frames = frames;
+        // only owner K's frames are kept for the next round (keeping every frame would hold a round of
+        // receipts -- 31 GB at C4 -- out of the recycled buffer pool)
+        prev_frames.clear();
+        if (retransmit_late >= 0)
+            for (auto& kv : frames) {
+                prev_frames[kv.first].assign(kv.second.size(), nullptr);
+                prev_frames[kv.first][retransmit_late] = kv.second[retransmit_late];
+            }
         round_ms.push_back((long)std::llround(
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count()));
         for (auto& r : replies) {
