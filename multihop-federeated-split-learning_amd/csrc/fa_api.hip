@@ -626,9 +626,12 @@ fa::Tuning rs_launch_tuning(const fa::Tuning& tu) {
 
 // FA_TEST_SHARED_DEVICE with FA_SHARD_CLIENT_RS: RCCL refuses two ranks on one device, so the
 // reduce-scatter of piece [a, a + G q) is replaced by its definition -- shard g block [off, off + q) :=
-// sum over h of partial_h[a + g q, a + (g + 1) q) in rank order, one launch per shard on its exchange
-// stream after every shard's piece reduction -- so that the rest of the layout (client dealing, pieces,
-// padding, shard offsets, copy-out runs) runs on a one-GPU box.  Never used with distinct devices.
+// sum over h of partial_h[a + g q, a + (g + 1) q), one launch per shard on its exchange stream after every
+// shard's piece reduction -- so that the rest of the layout (client dealing, pieces, padding, shard
+// offsets, copy-out runs) runs on a one-GPU box.  The sum runs in ring order, as a ring reduce-scatter
+// accumulates block g (it starts at rank g + 1 and ends at rank g), not rank order; RCCL's channels may
+// still order it otherwise, which is why the layout's parity is a tolerance.  Never used with distinct
+// devices.
 int emulated_reduce_scatter(fa_ctx* ctx, Part& p, size_t a, size_t q, size_t off) {
     const int G = ctx->G;
     for (int g = 0; g < G; ++g)
@@ -638,7 +641,7 @@ int emulated_reduce_scatter(fa_ctx* ctx, Part& p, size_t a, size_t q, size_t off
     for (int g = 0; g < G; ++g) {
         GpuRes& r = ctx->gpu[(size_t)g];
         DeviceGuard dg(r.dev);
-        for (int h = 0; h < G; ++h) ptrs[(size_t)h] = p.partial[(size_t)h] + a + (size_t)g * q;
+        for (int i = 0; i < G; ++i) ptrs[(size_t)i] = p.partial[(size_t)((g + 1 + i) % G)] + a + (size_t)g * q;
         int rc = reduce_on(ctx, g, rs_launch_tuning(ctx->tuning.tu), ptrs.data(), ones.data(), G, q, FA_F32,
                            static_cast<float*>(p.dout[(size_t)g]) + off, FA_F32, FA_FEDAVG, 1.0f, nullptr, r.comm);
         if (rc) return rc;
