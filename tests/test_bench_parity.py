@@ -173,3 +173,22 @@ def test_client_sharded_parity_over_gloo_ranks():
     bad = _run(2, n, D, corrupt=True)
     for layout in ("rs", "chain"):
         assert not bad[0][layout]["ok"] and bad[0][layout]["mismatches"] >= 1
+
+
+def test_committed_round4_bench_line_has_every_field():
+    """profiles/r04_bench.json (the full N = 1 bench of the round-4 tree, r04s07): the main line and every
+    secondary that reduces carry a passing parity object; the CPU baseline is the whole north-star workload,
+    and the other configs carry the reference's CPU path beside their device figure (verdict r03 #1, #3)."""
+    import json
+    with open(os.path.join(ROOT, "profiles", "r04_bench.json")) as f:
+        line = json.load(f)
+    assert line["parity"]["ok"] and line["parity"]["samples"] >= 1024
+    cpu = line["cpu_baseline"]
+    assert cpu["kind"] == "reference" and cpu["sample"].startswith("the whole workload") and cpu["cores"] >= 1
+    sec = line["secondary"]
+    for key, v in sec.items():
+        if key.startswith("sync_"):  # in-place state sync: slots hold sync-of-sync after the timed loop
+            continue
+        assert v["parity"]["ok"] and v["parity"]["samples"] >= 1024, key
+    for key in ("c2", "c3", "c4", "c5", "round_c2", "round_c4"):
+        assert sec[key]["cpu_gib_s"] > 0 and sec[key]["cpu_cores"] >= 1 and sec[key]["host_cpu"], key
