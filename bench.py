@@ -309,7 +309,10 @@ def parity_check(got, pos, idx, seed, w, exact=True, clients=None, bf16_in=False
         gf, rf = g.astype(np.float64), ref.astype(np.float64)
         gb, rb = g.view(np.uint32), ref.view(np.uint32)
     err = np.abs(gf - rf)
-    res = {"samples": int(pos.size), "max_abs_err": float(err.max()) if err.size else 0.0}
+    # a NaN where the oracle has a number is an error of unbounded size; the JSON line stays standard JSON
+    # (no NaN / Infinity literals): non-finite maxima are reported as null and always count as mismatches
+    fin = lambda x: float(x) if np.isfinite(x) else None  # noqa: E731
+    res = {"samples": int(pos.size), "max_abs_err": fin(err.max()) if err.size else 0.0}
     if exact:
         bad = int(np.count_nonzero(gb != rb))
         res.update({"check": "bit-exact vs the oracle's ordered chain" if not literal else
@@ -318,8 +321,8 @@ def parity_check(got, pos, idx, seed, w, exact=True, clients=None, bf16_in=False
         bound = RS_REL_TOL * sabs + 1e-30
         ratio = err / bound
         res.update({"check": "|err| <= %g * sum_k |w_k x_k|" % RS_REL_TOL,
-                    "mismatches": int(np.count_nonzero(ratio > 1.0)),
-                    "max_err_over_bound": float(ratio.max()) if ratio.size else 0.0})
+                    "mismatches": int(np.count_nonzero(~(ratio <= 1.0))),  # NaN counts
+                    "max_err_over_bound": fin(ratio.max()) if ratio.size else 0.0})
     res["ok"] = res["mismatches"] == 0 and res["samples"] > 0
     return res
 
@@ -329,25 +332,31 @@ def parity_merge(parts):
     parts = [p for p in parts if p]
     if not parts:
         return None
+    def worst(key):
+        vals = [p.get(key, 0.0) for p in parts]
+        return None if any(v is None for v in vals) else max(vals)
     out = {"check": parts[0]["check"], "samples": sum(p["samples"] for p in parts),
-           "mismatches": sum(p["mismatches"] for p in parts),
-           "max_abs_err": max(p["max_abs_err"] for p in parts)}
+           "mismatches": sum(p["mismatches"] for p in parts), "max_abs_err": worst("max_abs_err")}
     if any("max_err_over_bound" in p for p in parts):
-        out["max_err_over_bound"] = max(p.get("max_err_over_bound", 0.0) for p in parts)
+        out["max_err_over_bound"] = worst("max_err_over_bound")
     out["ok"] = all(p["ok"] for p in parts)
     return out
 
 
 def parity_over_ranks(torch, dist, world, backend, p):
     """Rank-local parity summed (samples, mismatches) and maxed (errors) over the ranks; every rank gets it."""
-    if world == 1 or p is None:
+    if world == 1:
         return p
+    # every rank takes part in both reductions, whatever its own check did (a collective per rank)
+    p = p or {"check": "not run", "samples": 0, "mismatches": 0, "max_abs_err": 0.0, "ok": False}
+    inf = float("inf")
+    enc = lambda v: inf if v is None else float(v)  # noqa: E731 -- None (a non-finite error) travels as inf
     dev = "cuda" if backend == "nccl" else "cpu"
     s = torch.tensor([p["samples"], p["mismatches"], 0 if p["ok"] else 1], dtype=torch.float64, device=dev)
-    m = torch.tensor([p["max_abs_err"], p.get("max_err_over_bound", 0.0)], dtype=torch.float64, device=dev)
+    m = torch.tensor([enc(p["max_abs_err"]), enc(p.get("max_err_over_bound", 0.0))], dtype=torch.float64, device=dev)
     dist.all_reduce(s, op=dist.ReduceOp.SUM)
     dist.all_reduce(m, op=dist.ReduceOp.MAX)
-    s, m = s.tolist(), m.tolist()
+    s, m = s.tolist(), [None if v == inf else v for v in m.tolist()]
     out = dict(p, samples=int(s[0]), mismatches=int(s[1]), max_abs_err=m[0], ranks=world, ok=s[2] == 0 and s[1] == 0)
     if "max_err_over_bound" in p:
         out["max_err_over_bound"] = m[1]

@@ -192,3 +192,20 @@ def test_committed_round4_bench_line_has_every_field():
         assert v["parity"]["ok"] and v["parity"]["samples"] >= 1024, key
     for key in ("c2", "c3", "c4", "c5", "round_c2", "round_c4"):
         assert sec[key]["cpu_gib_s"] > 0 and sec[key]["cpu_cores"] >= 1 and sec[key]["host_cpu"], key
+
+
+def test_parity_nan_is_a_mismatch_and_json_stays_standard(O):
+    """A NaN where the oracle has a number fails both checks, and the parity object serializes as standard
+    JSON (no NaN / Infinity literals the driver's parser would refuse)."""
+    import json
+    w, _, out = _full(O, 0x5EED, 4, 5_000)
+    pos, idx = bench.sample_positions([(0, 5_000)])
+    bad = out.copy()
+    bad[pos[7]] = np.nan
+    for exact in (True, False):
+        p = bench.parity_check(bad, pos, idx, 0x5EED, w, exact=exact)
+        assert not p["ok"] and p["mismatches"] == 1, p
+        json.loads(json.dumps(p, allow_nan=False))
+    m = bench.parity_merge([bench.parity_check(out, pos, idx, 0x5EED, w, exact=False),
+                            bench.parity_check(bad, pos, idx, 0x5EED, w, exact=False)])
+    assert not m["ok"] and m["max_err_over_bound"] is None
