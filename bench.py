@@ -632,6 +632,7 @@ class SyncSetup(Setup):
         for k in range(self.D):
             for ptr, cnt, off in self.agg.pieces(s, 0, k):
                 fa.fill_uniform(ptr, cnt, self.in_dt, self.seed + s, self.client0 + k, idx0=self.elem0 + off)
+        torch.cuda.synchronize()  # the fills ran on the null stream; the context's streams do not wait for it
         self.agg.sync_states(s, self.w)
         self.agg.sync()
         torch.cuda.synchronize()
