@@ -880,6 +880,9 @@ def main():
     ap.add_argument("--ctx-multi", default="", choices=["", "range", "rs"],
                     help="one process over every visible GPU through the C ABI: FA_SHARD_RANGE or FA_SHARD_CLIENT_RS "
                          "(RCCL reduce-scatter); prints one JSON object (a secondary of the N = 1 run)")
+    ap.add_argument("--ctx-shared", type=int, default=0,
+                    help="with --ctx-multi: rehearse K shards on GPU 0 (FA_TEST_SHARED_DEVICE: the layout's code path "
+                         "at K GPUs, the rs exchange replaced by its definition); for one-GPU boxes, not a timing")
     ap.add_argument("--ctx-gpus", type=int, default=0,
                     help="with --ctx-multi: use the first K visible GPUs (default all)")
     ap.add_argument("--h2d", action="store_true",
@@ -1136,14 +1139,21 @@ def ctx_multi(args):
     G = torch.cuda.device_count()
     if args.ctx_gpus > 0:
         G = min(G, args.ctx_gpus)
+    shared = args.ctx_shared > 0
+    if shared:  # K shards of GPU 0: the K-GPU code path rehearsed on a one-GPU box
+        G = args.ctx_shared
+        # the shards' launches share the GPU's CUs, and the phased kernel's persistent grid needs all of them:
+        # the one-shot walk, as for ranks sharing a GPU
+        fa.set_tuning(walk=2)
+    dev_of = (lambda g: 0) if shared else (lambda g: g)  # noqa: E731
     D, n, in_dt, _, desc = WORKLOADS[args.workload]
     idt = fa.F32 if in_dt == "f32" else fa.BF16
     s_in = 4 if in_dt == "f32" else 2
     rs = args.ctx_multi == "rs"
-    agg = fa.Aggregator(devices=list(range(G)), rs=rs)
+    agg = fa.Aggregator(devices=[dev_of(g) for g in range(G)], rs=rs, shared_device=shared)
     agg.define(1, n, idt, fa.F32, D, fa.FEDAVG)
     for g in range(G):
-        with torch.cuda.device(g):
+        with torch.cuda.device(dev_of(g)):
             for k in range(D):
                 try:
                     pcs = agg.pieces(1, g, k)
@@ -1152,7 +1162,7 @@ def ctx_multi(args):
                 for ptr, cnt, off in pcs:
                     fa.fill_uniform(ptr, cnt, idt, 0x5EED, k, idx0=off)
     for g in range(G):
-        torch.cuda.synchronize(g)
+        torch.cuda.synchronize(dev_of(g))
     w = Setup._weights(D)
     import numpy as np
     clients = None  # chain position k holds generator client k
@@ -1177,7 +1187,8 @@ def ctx_multi(args):
     else:
         def step():
             agg.reduce(1, w)
-    t_before = [fa.phased_timeouts(g) for g in range(G)]
+    devs = sorted({dev_of(g) for g in range(G)})
+    t_before = {d: fa.phased_timeouts(d) for d in devs}
     for _ in range(args.warmup):
         step()
     agg.sync()
@@ -1187,7 +1198,7 @@ def ctx_multi(args):
     agg.sync()
     dt = (time.perf_counter() - t0) / args.steps
     # > 0: a phased launch's grid was not co-resident on some GPU (the rs layout never takes that kernel)
-    timeouts = sum(fa.phased_timeouts(g) - t_before[g] for g in range(G))
+    timeouts = sum(fa.phased_timeouts(d) - t_before[d] for d in devs)
     tuning = agg.get_tuning()
     # parity of the last round, read back now that the timed region is closed: >= 1024 sampled elements of
     # every GPU's share of the result (range: its element range, pieces included; rs: its block-cyclic
@@ -1208,7 +1219,8 @@ def ctx_multi(args):
         p["per_gpu_samples"] = [q["samples"] for q in per_gpu]
         return p
     parity = parity_guarded(check)
-    out = {"layout": args.ctx_multi, "gpus": G, "workload": args.workload, "description": desc, "clients": D,
+    out = {"layout": args.ctx_multi, "gpus": G, "shared_device_rehearsal": shared, "workload": args.workload,
+           "description": desc, "clients": D,
            "elems_per_client": n, "host_inclusive": args.h2d, "ms_per_round": round(dt * 1e3, 4),
            "gib_s": round(D * n * s_in / dt / 2**30, 1), "steps": args.steps,
            "phased_meeting_timeouts": timeouts, "parity": parity, "tuning": tuning}

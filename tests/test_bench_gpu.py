@@ -75,3 +75,18 @@ def test_two_rank_rehearsal_parity_everywhere(fa, torch_gpu):
         ok(p, 2 * 1024)
         assert p["ranks"] == 2
     assert line["secondary"]["rs"]["parity"]["max_err_over_bound"] < 1.0
+
+
+@pytest.mark.parametrize("args", [["--ctx-multi", "rs", "--workload", "c4"],
+                                  ["--ctx-multi", "range", "--workload", "c5r", "--h2d"]])
+def test_eight_gpu_children_rehearsed_on_one_gpu(fa, torch_gpu, args):
+    """The N = 1 run's children on the driver's 8-GPU node (ctx_rs_c4_8gpu; ctx_range_c5_h2d_8gpu with C5's
+    per-GPU share, so that 128 clients fit the box's host budget) rehearsed as 8 shards of GPU 0
+    (FA_TEST_SHARED_DEVICE: the same dealing, pieces, shard offsets and copy-out; the exchange replaced by its
+    definition in ring order): the parity object covers all 8 shards, >= 1024 samples each."""
+    res = run_bench(args + ["--ctx-shared", "8", "--steps", "2", "--warmup", "1"], timeout=300)
+    assert res["gpus"] == 8 and res["shared_device_rehearsal"]
+    ok(res["parity"], 8 * 1024)
+    assert len(res["parity"]["per_gpu_samples"]) == 8 and min(res["parity"]["per_gpu_samples"]) >= 1024
+    if "rs" in args:
+        assert res["parity"]["max_err_over_bound"] < 1.0
