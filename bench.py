@@ -1058,8 +1058,7 @@ def main():
         line["secondary"] = single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier)
         for key, fig in cpu_per.items():  # the reference's CPU path beside each config's device figure
             line["secondary"].setdefault(key, {}).update(fig)
-        if n_dev >= 2:
-            line["secondary"].update(ctx_multi_secondaries(n_dev, T_START + BUDGET_S))
+        line["secondary"].update(ctx_multi_secondaries(n_dev, T_START + BUDGET_S))
 
     printer = LinePrinter(rank, line_out)
     if world > 1 and not args.no_secondary and args.layout == "range":
@@ -1232,25 +1231,33 @@ def ctx_multi_secondaries(n_dev, deadline, timeout=120):
     """On a node with several visible GPUs, the N = 1 run also times the in-process multi-GPU layouts over
     all of them (child processes, time-limited: a stalled collective cannot take the main line with it).
     Every child gets min(timeout, what is left before `deadline` - a 30 s margin); once less than 20 s is left
-    the rest are skipped (reported as such), so the line is printed before the driver's limit (600 s)."""
-    res = {}
+    the rest are skipped (reported as such), so the line is printed before the driver's limit (600 s).
+    On a one-GPU box the 8-GPU children are rehearsed instead as 8 shards of the one GPU (--ctx-shared 8:
+    the layouts' code paths with the exchange replaced by its definition; a parity check, not a timing)."""
     # BASELINE C4 is quoted on 4 GPUs (RCCL reduce-scatter), C5 on 8 (128 x 1 GiB buckets arriving from host
     # memory, H2D overlapped over every GPU's link); the north star on all of them
-    for layout, workload, h2d, gpus in (("range", "northstar", False, n_dev), ("rs", "northstar", False, n_dev),
-                                        ("rs", "c4", False, min(4, n_dev)), ("rs", "c4", False, n_dev),
-                                        ("range", "c5", True, min(8, n_dev))):
-        key = "ctx_%s_%s%s_%dgpu" % (layout, workload, "_h2d" if h2d else "", gpus)
+    if n_dev >= 2:
+        legs = [("range", "northstar", False, n_dev, 0), ("rs", "northstar", False, n_dev, 0),
+                ("rs", "c4", False, min(4, n_dev), 0), ("rs", "c4", False, n_dev, 0),
+                ("range", "c5", True, min(8, n_dev), 0)]
+    else:  # C5's per-GPU share (c5r) keeps the host-inclusive rehearsal at 16 GiB of input per round
+        legs = [("rs", "c4", False, 8, 8), ("range", "c5r", True, 8, 8)]
+    res = {}
+    for layout, workload, h2d, gpus, shared in legs:
+        key = "ctx_%s_%s%s_%d%s" % (layout, workload, "_h2d" if h2d else "", gpus,
+                                   "shard_rehearsal_on_one_gpu" if shared else "gpu")
         if key in res:
             continue
         left = deadline - time.monotonic() - 30  # deadline = T_START + BUDGET_S
         if left < 20:
             res[key] = {"skipped": "the bench's time budget is spent (FA_BENCH_BUDGET_S)"}
             continue
+        cmd = [sys.executable, os.path.abspath(__file__), "--ctx-multi", layout, "--workload", workload]
+        cmd += ["--ctx-shared", str(shared)] if shared else ["--ctx-gpus", str(gpus)]
+        cmd += ["--h2d", "--steps", "3", "--warmup", "1"] if h2d else ["--steps", "3" if shared else "10", "--warmup",
+                                                                        "1" if shared else "2"]
         try:
-            r = subprocess.run([sys.executable, os.path.abspath(__file__), "--ctx-multi", layout, "--workload",
-                                workload, "--ctx-gpus", str(gpus)] + (["--h2d", "--steps", "3", "--warmup", "1"] if h2d
-                                                                      else ["--steps", "10", "--warmup", "2"]),
-                               capture_output=True, text=True, timeout=min(timeout, left))
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=min(timeout, left))
             res[key] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
                 {"error": "rc %d: %s" % (r.returncode, r.stderr[-300:])}
         except Exception as e:  # noqa: BLE001 -- reported, never fatal
