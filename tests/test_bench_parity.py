@@ -209,3 +209,39 @@ def test_parity_nan_is_a_mismatch_and_json_stays_standard(O):
     m = bench.parity_merge([bench.parity_check(out, pos, idx, 0x5EED, w, exact=False),
                             bench.parity_check(bad, pos, idx, 0x5EED, w, exact=False)])
     assert not m["ok"] and m["max_err_over_bound"] is None
+
+
+def test_ctx_children_the_n1_run_starts(monkeypatch):
+    """Which --ctx-multi children the N = 1 bench starts: on the driver's 8-GPU node the real multi-GPU legs
+    (C4's reduce-scatter on 4 and 8 GPUs, C5 host-inclusive on 8), on a one-GPU box the 8-GPU legs rehearsed
+    as 8 shards of the one GPU; every child's JSON (with its parity object) lands under its key."""
+    import json
+    import subprocess
+    calls = []
+
+    class R:
+        returncode = 0
+        stderr = ""
+
+        def __init__(self, cmd):
+            self.stdout = json.dumps({"cmd": cmd, "parity": {"ok": True}}) + "\n"
+
+    def fake_run(cmd, **kw):
+        calls.append(cmd)
+        return R(cmd)
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    import time
+    res = bench.ctx_multi_secondaries(8, time.monotonic() + 1000)
+    assert {"ctx_range_northstar_8gpu", "ctx_rs_northstar_8gpu", "ctx_rs_c4_4gpu", "ctx_rs_c4_8gpu",
+            "ctx_range_c5_h2d_8gpu"} == set(res)
+    assert all(r["parity"]["ok"] for r in res.values())
+    c4 = [c for c in calls if "c4" in c and c[c.index("--ctx-gpus") + 1] == "4"]
+    assert c4 and c4[0][c4[0].index("--ctx-multi") + 1] == "rs"
+    calls.clear()
+    res = bench.ctx_multi_secondaries(1, time.monotonic() + 1000)
+    assert set(res) == {"ctx_rs_c4_8shard_rehearsal_on_one_gpu", "ctx_range_c5r_h2d_8shard_rehearsal_on_one_gpu"}
+    assert all("--ctx-shared" in c and c[c.index("--ctx-shared") + 1] == "8" for c in calls)
+    # no time left: skipped, never started
+    calls.clear()
+    res = bench.ctx_multi_secondaries(8, time.monotonic() + 10)
+    assert not calls and all("skipped" in r for r in res.values())
