@@ -52,6 +52,9 @@ struct Options {
     bool discover = false, pinned = true;
     bool rs = false;     // --layout rs: clients dealt to the GPUs, RCCL reduce-scatter of fp32 partials
     bool eager = false;  // --eager: accumulate on arrival (the chain advances with the in-order receipts)
+    // --test-shared-device: the --gpus G shards all on GPU 0 (FA_TEST_SHARED_DEVICE; the rs exchange replaced
+    // by its definition), so the multi-GPU layouts run end to end on a one-GPU box (tests only)
+    bool shared_device = false;
     int rs_chunks = 0;
     double link_mbps = 0;
     // failure detection: after stall_report_s without a receipt, name the data owners still missing;
@@ -70,7 +73,7 @@ void usage() {
                  "       [--rounds R] [--port-base P] [--discover] [--link-mbps M] [--samples id:n,...]\n"
                  "       [--divisor K] [--last-layers L] [--no-pinned] [--layout range|rs] [--rs-chunks C]\n"
                  "       [--eager] [--stall-report S] [--receipt-timeout S] [--rx-concurrency K]\n"
-                 "       [--senders S]\n";
+                 "       [--senders S] [--test-shared-device]\n";
 }
 
 bool parse_args(int argc, char** argv, Options* o) {
@@ -94,6 +97,7 @@ bool parse_args(int argc, char** argv, Options* o) {
         else if (a == "--discover") o->discover = true;
         else if (a == "--no-pinned") o->pinned = false;
         else if (a == "--eager") o->eager = true;
+        else if (a == "--test-shared-device") o->shared_device = true;
         else if (a == "--rs-chunks") o->rs_chunks = std::atoi(val("--rs-chunks"));
         else if (a == "--stall-report") o->stall_report_s = std::atof(val("--stall-report"));
         else if (a == "--receipt-timeout") o->receipt_timeout_s = std::atof(val("--receipt-timeout"));
@@ -161,7 +165,12 @@ public:
     Aggregator(const Options& o, NetLayer* net, const std::vector<int>& owners) : o_(o), net_(net) {
         int flags = o.rs ? FA_SHARD_CLIENT_RS : o.gpus > 1 ? FA_SHARD_RANGE : 0;
         if (o.eager) flags |= FA_ACCUMULATE_ON_ARRIVAL;
-        FA_CHECK(fa_create(&ctx_, o.gpus, flags));
+        if (o.shared_device) {
+            const std::vector<int> zeros((size_t)std::max(1, o.gpus), 0);
+            FA_CHECK(fa_create_ex(&ctx_, zeros.data(), o.gpus, flags | FA_TEST_SHARED_DEVICE));
+        } else {
+            FA_CHECK(fa_create(&ctx_, o.gpus, flags));
+        }
         FA_CHECK(fa_set_literal_divisor(ctx_, -1, o.divisor));
         if (o.rs_chunks > 0) {
             fa_tuning t{};

@@ -126,6 +126,43 @@ def test_multi_mb_parts_concurrent_owners(torch_gpu, tmp_path, pinned, sequentia
             agg.kill()
 
 
+@pytest.mark.parametrize("extra,tol", [
+    (["--gpus", "2"], 0),                                            # range shards: bit-exact
+    (["--gpus", "3", "--eager"], 0),                                 # range shards, accumulate on arrival
+    (["--gpus", "3", "--layout", "rs", "--rs-chunks", "3"], 1e-6),   # client shards + the exchange: tolerance
+    (["--gpus", "4", "--layout", "rs"], 1e-6),                       # a GPU holds 1-2 of the 6 clients
+])
+def test_multi_gpu_layouts_through_the_process(torch_gpu, tmp_path, extra, tol):
+    """fa_aggregator --gpus G, the drop-in process's multi-GPU layouts end to end, rehearsed as G shards of
+    the box's one GPU (--test-shared-device: FA_TEST_SHARED_DEVICE; the rs exchange replaced by its
+    definition in ring order): receipts split over the shards from the frames they arrived in, the replies
+    gathered back from every shard into one frame.  Range shards must be bit-exact; the client-sharded rs
+    layout is held to 1e-6 * sum_k |w_k x_k| element by element (fake_owners --rel-tol)."""
+    sizes = _large_parts(str(tmp_path))
+    D, rounds = 6, 2
+    base = pick_base()
+    agg = subprocess.Popen([AGG, "-i", "-1", "-d", str(D), "-c", "1", "--rounds", str(rounds), "--port-base",
+                            str(base), "--test-shared-device"] + extra,
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        time.sleep(0.5)
+        r = subprocess.run([OWNERS, "--blobs", str(tmp_path), "--parts", "1,2,3", "-d", str(D), "-c", "1",
+                            "--rounds", str(rounds), "--port-base", str(base), "--model-name", "1", "--start", "9",
+                            "--end", "3"] + (["--rel-tol", str(tol)] if tol else []),
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res = json.loads(r.stdout.strip().splitlines()[-1])
+        assert res["ok"] and res["checked_elems"] == rounds * D * sum(sizes.values())
+        if tol:
+            assert 0 <= res["max_err_over_bound"] < 1.0
+        out, err = agg.communicate(timeout=60)
+        assert agg.returncode == 0, err[-2000:]
+        assert len([l for l in out.splitlines() if l.startswith("{")]) == rounds
+    finally:
+        if agg.poll() is None:
+            agg.kill()
+
+
 @pytest.mark.parametrize("drop_phase", [1, 2])
 def test_missing_owner_is_reported_and_times_out(torch_gpu, drop_phase):
     """Failure detection: one data owner never sends its phase-1 (or phase-2) receipts.  The

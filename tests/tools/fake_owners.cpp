@@ -9,7 +9,7 @@
 //   fa_fake_owners --blobs DIR --parts 1,2,3 -d D -c C [--rounds R] [--mode fedavg|literal]
 //                  [--port-base P] [--model-name N --model-type T --start S --end E] [--seed X]
 //                  [--drop-owner K [--drop-phase P]] [--retransmit K] [--retransmit-late K]
-//                  [--reply-timeout S]
+//                  [--reply-timeout S] [--rel-tol X]
 //                  [--sequential]   (owners send at once, one connection each, unless --sequential
 //                                    or --mode literal, whose result depends on the arrival order)
 // Prints one JSON line: {"ok": bool, "rounds": R, "checked_elems": ..., "round_ms": [...]}.
@@ -71,6 +71,7 @@ int main(int argc, char** argv) {
     int drop_owner = -1, drop_phase = 1;  // failure injection: owner K never sends its phase-P receipts
     int retransmit = -1;                  // owner K sends every receipt twice (a retransmission)
     int retransmit_late = -1;             // owner K re-sends its previous round's receipts during this round
+    double rel_tol = 0;                   // > 0: fp32 replies within rel_tol * sum_k |w_k x_k| (the rs layout)
     long reply_timeout_ms = 600000;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
@@ -93,6 +94,7 @@ int main(int argc, char** argv) {
         else if (a == "--drop-phase") drop_phase = std::atoi(v), ++i;
         else if (a == "--retransmit") retransmit = std::atoi(v), ++i;
         else if (a == "--retransmit-late") retransmit_late = std::atoi(v), ++i;
+        else if (a == "--rel-tol") rel_tol = std::atof(v), ++i;
         else if (a == "--reply-timeout") reply_timeout_ms = (long)(std::atof(v) * 1000), ++i;
         else {
             std::cerr << "unknown argument " << a << "\n";
@@ -168,6 +170,7 @@ int main(int argc, char** argv) {
     bool ok = true;
     size_t checked = 0;
     std::vector<long> round_ms;
+    double max_err_over_bound = 0;  // --rel-tol: the worst element against its bound
     std::map<int, std::vector<std::shared_ptr<const Bytes>>> prev_frames;  // the previous round's, per mp
     auto collect = [&](int want, std::vector<Receipt>* got) {
         const long t_end = now_ms() + reply_timeout_ms;
@@ -309,7 +312,26 @@ int main(int argc, char** argv) {
                 for (auto& x : xs) ptrs.push_back((const uint16_t*)x.data());
                 fa_oracle_fedavg_bf16(ptrs.data(), w.data(), D, p->n, nullptr, want.data(), 1, threads);
             }
-            if (std::memcmp(got.data(), want.data(), p->n * es) != 0) {
+            if (rel_tol > 0 && es == 4 && mode != "literal") {
+                // the client-sharded layout sums in the exchange's order: |got - want| <= tol * sum_k |w_k x_k|
+                const float* g = (const float*)got.data();
+                const float* h = (const float*)want.data();
+                size_t bad = 0;
+                double worst = 0;
+                for (size_t i = 0; i < p->n; ++i) {
+                    double sabs = 0;
+                    for (int k = 0; k < D; ++k) sabs += std::fabs((double)w[k] * ((const float*)xs[k].data())[i]);
+                    const double r = std::fabs((double)g[i] - (double)h[i]) / (rel_tol * sabs + 1e-30);
+                    if (!(r <= 1.0)) ++bad;
+                    if (r > worst) worst = r;
+                }
+                if (bad) {
+                    std::cerr << "part " << p->mp << ": " << bad << " elements beyond the tolerance (worst " << worst
+                              << " of the bound)\n";
+                    ok = false;
+                }
+                max_err_over_bound = std::max(max_err_over_bound, worst);
+            } else if (std::memcmp(got.data(), want.data(), p->n * es) != 0) {
                 size_t bad = 0;
                 while (bad < p->n && std::memcmp(&got[bad * es], &want[bad * es], es) == 0) ++bad;
                 std::cerr << "part " << p->mp << " mismatch at element " << bad << " (" << es << "-byte elements)\n";
@@ -323,7 +345,7 @@ int main(int argc, char** argv) {
     printf("{\"ok\": %s, \"rounds\": %d, \"data_owners\": %d, \"checked_elems\": %zu, \"round_ms\": [", ok ? "true" : "false",
            rounds, D, checked);
     for (size_t i = 0; i < round_ms.size(); ++i) printf("%s%ld", i ? ", " : "", round_ms[i]);
-    printf("]}\n");
+    printf("], \"max_err_over_bound\": %.6g}\n", max_err_over_bound);
     for (auto& kv : listeners) kv.second->stop();
     return ok ? 0 : 1;
 }
