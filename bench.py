@@ -251,6 +251,7 @@ def cpu_baseline(D, n, reps, dt="f32", skip=None):
 
 PARITY_SAMPLES = 1024
 RS_REL_TOL = 1e-6
+RS_CHUNK_SWEEP = (2, 4, 16)  # rs pieces per round tried beside the library default (8) on a multi-GPU node
 
 
 def load_checker():
@@ -888,6 +889,9 @@ def main():
     ap.add_argument("--h2d", action="store_true",
                     help="with --ctx-multi: host-inclusive rounds (fa_submit_pinned of every client from host "
                          "memory, overlapped per GPU, + fa_finalize into host memory)")
+    ap.add_argument("--rs-chunks", type=int, default=0,
+                    help="with --ctx-multi rs: pieces per round of the in-process reduce-scatter (fa_tuning.rs_chunks; "
+                         "the reduction of piece c+1 overlaps the exchange of piece c); 0 = the library default")
     args = ap.parse_args()
     if args.steps < 1 or args.warmup < 0:
         ap.error("--steps must be >= 1 and --warmup >= 0")
@@ -1149,6 +1153,8 @@ def ctx_multi(args):
     idt = fa.F32 if in_dt == "f32" else fa.BF16
     s_in = 4 if in_dt == "f32" else 2
     rs = args.ctx_multi == "rs"
+    if args.rs_chunks:
+        fa.set_tuning(rs_chunks=args.rs_chunks)  # the process default the context starts from
     agg = fa.Aggregator(devices=[dev_of(g) for g in range(G)], rs=rs, shared_device=shared)
     agg.define(1, n, idt, fa.F32, D, fa.FEDAVG)
     for g in range(G):
@@ -1237,15 +1243,19 @@ def ctx_multi_secondaries(n_dev, deadline, timeout=120):
     # BASELINE C4 is quoted on 4 GPUs (RCCL reduce-scatter), C5 on 8 (128 x 1 GiB buckets arriving from host
     # memory, H2D overlapped over every GPU's link); the north star on all of them
     if n_dev >= 2:
-        legs = [("range", "northstar", False, n_dev, 0), ("rs", "northstar", False, n_dev, 0),
-                ("rs", "c4", False, min(4, n_dev), 0), ("rs", "c4", False, n_dev, 0),
-                ("range", "c5", True, min(8, n_dev), 0)]
+        legs = [("range", "northstar", False, n_dev, 0, 0), ("rs", "northstar", False, n_dev, 0, 0),
+                ("rs", "c4", False, min(4, n_dev), 0, 0), ("rs", "c4", False, n_dev, 0, 0),
+                ("range", "c5", True, min(8, n_dev), 0, 0)]
+        # the rs overlap depth on real xGMI (untuned so far: one-GPU boxes have no exchange to overlap): C4's
+        # 4-GPU reduce-scatter at other piece counts than the default, last, so the budget drops them first
+        legs += [("rs", "c4", False, min(4, n_dev), 0, c) for c in RS_CHUNK_SWEEP]
     else:  # C5's per-GPU share (c5r) keeps the host-inclusive rehearsal at 16 GiB of input per round
-        legs = [("rs", "c4", False, 8, 8), ("range", "c5r", True, 8, 8)]
+        legs = [("rs", "c4", False, 8, 8, 0), ("range", "c5r", True, 8, 8, 0)]
     res = {}
-    for layout, workload, h2d, gpus, shared in legs:
-        key = "ctx_%s_%s%s_%d%s" % (layout, workload, "_h2d" if h2d else "", gpus,
-                                   "shard_rehearsal_on_one_gpu" if shared else "gpu")
+    for layout, workload, h2d, gpus, shared, chunks in legs:
+        key = "ctx_%s_%s%s_%d%s%s" % (layout, workload, "_h2d" if h2d else "", gpus,
+                                     "shard_rehearsal_on_one_gpu" if shared else "gpu",
+                                     "_rschunks%d" % chunks if chunks else "")
         if key in res:
             continue
         left = deadline - time.monotonic() - 30  # deadline = T_START + BUDGET_S
@@ -1254,6 +1264,7 @@ def ctx_multi_secondaries(n_dev, deadline, timeout=120):
             continue
         cmd = [sys.executable, os.path.abspath(__file__), "--ctx-multi", layout, "--workload", workload]
         cmd += ["--ctx-shared", str(shared)] if shared else ["--ctx-gpus", str(gpus)]
+        cmd += ["--rs-chunks", str(chunks)] if chunks else []
         cmd += ["--h2d", "--steps", "3", "--warmup", "1"] if h2d else ["--steps", "3" if shared else "10", "--warmup",
                                                                         "1" if shared else "2"]
         try:

@@ -90,3 +90,15 @@ def test_eight_gpu_children_rehearsed_on_one_gpu(fa, torch_gpu, args):
     assert len(res["parity"]["per_gpu_samples"]) == 8 and min(res["parity"]["per_gpu_samples"]) >= 1024
     if "rs" in args:
         assert res["parity"]["max_err_over_bound"] < 1.0
+
+
+@pytest.mark.parametrize("chunks", [2, 16])
+def test_rs_chunk_sweep_child_rehearsed_on_one_gpu(fa, torch_gpu, chunks):
+    """The rs overlap-depth sweep the N = 1 run starts on a multi-GPU node (ctx_rs_c4_4gpu_rschunks<K>),
+    rehearsed as 4 shards of GPU 0 on a smaller bucket: the context takes the piece count it was given, and
+    every GPU's block-cyclic segments still pass the 1e-6 bound."""
+    res = run_bench(["--ctx-multi", "rs", "--workload", "ns_w8", "--ctx-shared", "4", "--rs-chunks", str(chunks),
+                     "--steps", "2", "--warmup", "1"])
+    assert res["tuning"]["rs_chunks"] == chunks and res["gpus"] == 4
+    ok(res["parity"], 4 * 1024)
+    assert res["parity"]["max_err_over_bound"] < 1.0

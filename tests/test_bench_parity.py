@@ -232,11 +232,16 @@ def test_ctx_children_the_n1_run_starts(monkeypatch):
     monkeypatch.setattr(subprocess, "run", fake_run)
     import time
     res = bench.ctx_multi_secondaries(8, time.monotonic() + 1000)
+    sweep = {"ctx_rs_c4_4gpu_rschunks%d" % c for c in bench.RS_CHUNK_SWEEP}
     assert {"ctx_range_northstar_8gpu", "ctx_rs_northstar_8gpu", "ctx_rs_c4_4gpu", "ctx_rs_c4_8gpu",
-            "ctx_range_c5_h2d_8gpu"} == set(res)
+            "ctx_range_c5_h2d_8gpu"} | sweep == set(res)
     assert all(r["parity"]["ok"] for r in res.values())
     c4 = [c for c in calls if "c4" in c and c[c.index("--ctx-gpus") + 1] == "4"]
-    assert c4 and c4[0][c4[0].index("--ctx-multi") + 1] == "rs"
+    assert c4 and c4[0][c4[0].index("--ctx-multi") + 1] == "rs" and "--rs-chunks" not in c4[0]
+    # the rs overlap-depth sweep of C4 at 4 GPUs comes last (the budget drops it first), one child per depth
+    assert [c[c.index("--rs-chunks") + 1] for c in calls if "--rs-chunks" in c] == \
+        [str(c) for c in bench.RS_CHUNK_SWEEP]
+    assert all("--rs-chunks" not in c for c in calls[:-len(bench.RS_CHUNK_SWEEP)])
     calls.clear()
     res = bench.ctx_multi_secondaries(1, time.monotonic() + 1000)
     assert set(res) == {"ctx_rs_c4_8shard_rehearsal_on_one_gpu", "ctx_range_c5r_h2d_8shard_rehearsal_on_one_gpu"}
