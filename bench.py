@@ -673,18 +673,20 @@ def read_stream_peak(fa, torch, setup, stream, reps=7):
     """Measured read-STREAM peak on this run's own client slots: a read-only launch over
     the D buckets -- from one phase up the phased kernel itself with its output stream switched off
     (fa_diag_read_stream) -- median of `reps` HIP-event timings on the launch stream.  GB/s of bytes
-    read; frac_of_read_stream = achieved / this, i.e. what the output stream costs on top of the reads."""
-    if setup.in_dt != fa.F32:
-        return None
+    read; frac_of_read_stream = achieved / this, i.e. what the output stream costs on top of the reads.
+    The probe reads bytes: a bf16 slot is read as the fp32 words its bytes make (the same bytes, the same
+    addresses), so a bf16 workload gets the read rate of its own input too."""
     # one read-only launch per range piece (a bucket set held in pieces, e.g. C5 on one GPU, is reduced one
-    # launch per piece too): bytes of all pieces / the sum of their median times
-    per_client = [setup.agg.pieces(0, 0, k) for k in range(setup.D)]
+    # launch per piece too): bytes of all pieces / the sum of their median times.  The reps rotate over the
+    # input sets as the timed loop does, so a set that fits the MALL is not read back from it.
+    sets = [[setup.agg.pieces(s, 0, k) for k in range(setup.D)] for s in range(setup.nsets)]
     nbytes, t_ms = 0, 0.0
-    for j in range(len(per_client[0])):
-        ptrs = [pc[j][0] for pc in per_client]
-        n = per_client[0][j][1] - per_client[0][j][1] % 4
+    for j in range(len(sets[0][0])):
+        n = sets[0][0][j][1] * setup.s_in // 4  # fp32 words of the piece's bytes
+        n -= n % 4
         ms = []
         for i in range(reps + 2):
+            ptrs = [pc[j][0] for pc in sets[i % setup.nsets]]
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(stream)
             fa.diag_read_stream(ptrs, n, stream=stream)
@@ -1286,12 +1288,16 @@ def single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier):
         s = Setup(fa, torch, sD, sn, si, so, 0, device)
         torch.cuda.synchronize()
         w2, ka, _ = timed_loop(torch, s, max(10, args.steps), 3, stream, dist, barrier)
+        achieved = s.algo_bytes() / (ka * 1e-3) / 1e9
+        # the same config's own read-only rate (its slots, its size): how far its kernel is from reading alone
+        rp = None if under_profiler() else read_stream_peak(fa, torch, s, stream)
         sec[name] = {"description": sdesc, "gib_s": round(s.input_bytes() * max(10, args.steps) / w2 / 2**30, 1),
                      "kernel_ms_avg": round(ka, 4),
-                     "achieved_GBs": round(s.algo_bytes() / (ka * 1e-3) / 1e9, 1),
+                     "achieved_GBs": round(achieved, 1),
                      "algorithmic_bytes_per_launch": s.algo_bytes(),
                      "traffic": traffic_from_profile(name, 1)[0],
-                     "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "read_stream_peak": rp, "frac_of_read_stream": round(achieved / rp, 4) if rp else None,
                      "input_sets_rotated": s.nsets, "parity": parity_guarded(lambda: s.parity(0))}
         s.close()
 

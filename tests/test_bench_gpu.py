@@ -46,6 +46,17 @@ def test_pieced_workload_prints_its_line(fa, torch_gpu, layout):
         assert line["parity"]["check"].startswith("bit-exact")
 
 
+@pytest.mark.parametrize("workload", ["c3", "c2"])
+def test_read_stream_peak_of_bf16_and_rotated_workloads(fa, torch_gpu, workload):
+    """The read-only rate beside a config's kernel: a bf16 workload (C3) is read as the fp32 words its bytes
+    make, and a workload whose input set fits the MALL (C2, 3 sets rotated) is read set by set."""
+    line = run_bench(["--workload", workload, "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-secondary",
+                      "--no-live-pmc"])
+    ok(line["parity"])
+    rf = line["roofline"]
+    assert rf["read_stream_peak"] > 1000 and 0.5 < rf["frac_of_read_stream"] < 1.2, rf
+
+
 @pytest.mark.parametrize("layout", ["range", "rs"])
 def test_ctx_multi_child_carries_parity(fa, torch_gpu, layout):
     res = run_bench(["--ctx-multi", layout, "--workload", "ns_w8", "--steps", "3", "--warmup", "1"])
