@@ -1296,12 +1296,18 @@ __global__ __launch_bounds__(256) void read_probe_kernel(const ClientTable t, in
 }
 
 hipError_t launch_read_probe(const ClientTable& t, int nc, int64_t nvec, float* sink, hipStream_t s) {
-    // from one phase up: the phased kernel itself with no output (its reads, LDS and meetings, no writes)
+    // the phased kernel itself with no output (its reads, LDS and meetings, no writes) wherever an f32 chain of
+    // this shape takes it: from one phase up, and below one phase with >= sized_min_clients() clients in one
+    // phase sized to the buffers (the product's launch for such buckets; the simple probe below reads those
+    // up to 14% slower than the product reduces them, r04s16)
     PhasedDevice* d = phased_device();
-    Tuning tu{256, 0, 16, 1, 2, 4};  // walk 5's f32 form, full phases only (no sized phase: nc = 0)
-    if (d && plan_chain(FA_F32, FA_F32, nvec, 0, true, tu, d->cus).kind == kPlanPhased) {
-        const hipError_t e = launch_phased_r<float, float, 192, 256>(d, t, nc, nullptr, nullptr, 0, nvec, nvec * 4, s);
-        if (e != hipErrorNotSupported) return e;
+    Tuning tu{256, 0, 16, 1, 2, 4};  // walk 5's f32 form
+    if (d) {
+        const ChainPlan pl = plan_chain(FA_F32, FA_F32, nvec, nc, true, tu, d->cus);
+        if (pl.kind == kPlanPhased) {
+            const hipError_t e = launch_phased_plan<float, float>(d, pl, t, nc, nullptr, nullptr, 0, nvec, nvec * 4, s);
+            if (e != hipErrorNotSupported) return e;
+        }
     }
     const int g = (d ? d->cus : 256) * 8;
     hipLaunchKernelGGL(read_probe_kernel, dim3((unsigned)g), dim3(256), 0, s, t, nc, nvec, sink);

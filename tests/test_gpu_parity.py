@@ -931,11 +931,14 @@ def test_phased_graph_replays(fa, O, torch_gpu):
     assert t1 < 1.5 * t0 + 0.05, (t0, t1)
 
 
-@pytest.mark.parametrize("n,D", [(1_000_000, 8), (int(PHASE_ELEMS * 88 / 72 * 1.5), 6)])
+@pytest.mark.parametrize("n,D", [(1_000_000, 8), (4_000_000, 16), (2_000_000, 20), (16_000_000, 16),
+                                 (int(PHASE_ELEMS * 88 / 72 * 1.5), 6)])
 def test_read_stream_probe_reads_only(fa, O, torch_gpu, n, D):
-    """fa_diag_read_stream (bench's roofline.read_stream_peak): the simple probe below one phase, the phased
-    kernel with its output stream switched off above; it writes nothing -- every client buffer keeps its
-    bits and the kernel's output pointer stays null (put() returns before any store)."""
+    """fa_diag_read_stream (bench's roofline.read_stream_peak): the simple probe below one phase with few
+    clients, the phased kernel with its output stream switched off where an f32 chain takes it (a sized
+    phase below one phase from 16 clients: register stage + LDS, and LDS only; full phases above); it writes
+    nothing -- every client buffer keeps its bits and the kernel's output pointer stays null (put() returns
+    before any store)."""
     torch = torch_gpu
     clients = [filled(fa, torch, n, False, 55, k) for k in range(D)]
     before = [c.clone() for c in clients]
