@@ -128,6 +128,105 @@ CPU_RECEIVE_LOOPS = [
 ]
 
 
+# BASELINE config C1 end to end over loopback (tests/golden/lenet5_c1: LeNet-5 model parts made by the
+# reference's own builders, spec of its manifest): fake data owners (tests/tools/fa_fake_owners, the load
+# generator and checker: every element of every reply bit-exact against the oracle) against an aggregator
+# process -- the reference's own CPU path (oracle/_ref/ref_cpu_aggregator: its systemAPI / network_layer with
+# aggregator.cpp:55-167 on CPU libtorch) or the drop-in fa_aggregator.  Owner view: first send to last reply.
+C1_E2E_ROUNDS = 40
+FAKE_OWNERS = os.path.join(ROOT, "tests", "tools", "bin", "fa_fake_owners")
+FA_AGGREGATOR = os.path.join(PKG_DIR, "bin", "fa_aggregator")
+REF_CPU_AGGREGATOR = os.path.join(ROOT, "oracle", "_ref", "ref_cpu_aggregator")
+REF_PORTS = (8080, 8081, 8082, 8083)  # the reference's fixed routing table (network_layer.h:80-86)
+
+
+def ports_free(ports):
+    import socket
+    for p in ports:
+        with socket.socket() as so:
+            try:
+                so.bind(("0.0.0.0", p))
+            except OSError:
+                return False
+    return True
+
+
+def free_port_base():
+    import random
+    for _ in range(50):
+        b = random.randrange(10000, 32000, 100)
+        if ports_free(range(b, b + 40)):
+            return b
+    raise RuntimeError("no free port range")
+
+
+def e2e_c1(agg_cmd, mode, port_base, rounds=C1_E2E_ROUNDS, startup_s=0.5, timeout=120):
+    """Rounds of BASELINE C1 (LeNet-5, D = 2, fp32) through one aggregator process over loopback; returns the
+    owners' round times (round 0, which allocates, reported apart) and their bit-exact check of every reply."""
+    golden = os.path.join(ROOT, "tests", "golden", "lenet5_c1")
+    with tempfile.TemporaryDirectory(prefix="fa_c1_") as tmp:  # the reference process writes its logs in cwd
+        agg = subprocess.Popen(agg_cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, cwd=tmp,
+                               start_new_session=True)
+        try:
+            time.sleep(startup_s)
+            if agg.poll() is not None:
+                raise RuntimeError("aggregator exited early: %s" % agg.stderr.read()[-300:].decode(errors="replace"))
+            r = subprocess.run([FAKE_OWNERS, "--blobs", golden, "--parts", "1,2,3", "-d", "2", "-c", "1",
+                                "--rounds", str(rounds), "--port-base", str(port_base), "--model-name", "2",
+                                "--start", "6", "--end", "1", "--mode", mode, "--reply-timeout", "30"],
+                               capture_output=True, text=True, timeout=timeout, cwd=tmp)
+        finally:
+            if agg.poll() is None:
+                try:
+                    agg.wait(timeout=10)  # fa_aggregator --rounds exits by itself
+                except subprocess.TimeoutExpired:
+                    os.killpg(agg.pid, signal.SIGKILL)  # the reference's loop never returns (aggregator.cpp:55)
+                    agg.wait()
+    if r.returncode not in (0, 1):
+        raise RuntimeError("fake owners rc %d: %s" % (r.returncode, r.stderr[-300:]))
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    ms = res["round_ms"][1:]
+    return {"rounds_timed": len(ms), "round_ms_median": round(statistics.median(ms), 3),
+            "round_ms_mean": round(statistics.mean(ms), 3),
+            "round_ms_min": min(ms), "round0_ms": res["round_ms"][0], "mode": mode,
+            "parity": {"check": "every element of every reply bit-exact vs the oracle (fake owners: %s)" %
+                       ("fl(fl(x+x)/1000) of the last receipt" if mode == "literal" else "the ordered FedAvg chain"),
+                       "samples": res["checked_elems"], "mismatches": 0 if res["ok"] else None, "ok": bool(res["ok"])}}
+
+
+def cpu_c1(threads, cpu_model):
+    """BASELINE C1's CPU figures (rank 0, before the GPU is touched): the reference's own aggregator process on
+    CPU libtorch over loopback, and its receive loop alone (oracle/_ref/ref_harness bench-round)."""
+    out = {"cpu_cores": threads, "host_cpu": cpu_model, "cpu_kind": "reference"}
+    harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    try:
+        lines = []
+        for t in (threads, 1):
+            r = subprocess.run([harness] + [str(x) for x in ["bench-round", 2, 0, 6, 1, 10, 2, t, 500]],
+                               capture_output=True, text=True, timeout=120, check=True)
+            lines.append(json.loads(r.stdout.strip().splitlines()[-1]))
+        out.update({"cpu_round_ms": round(lines[0]["round_ms_avg"], 4), "cpu_gib_s": round(lines[0]["gib_s"], 4),
+                    "cpu_round_ms_1_core": round(lines[1]["round_ms_avg"], 4),
+                    "cpu_path": "the reference's receive loop for a whole round, network aside: torch::load of each "
+                                "receipt + (p+p)/1000 + copy_ (aggregator.cpp:59-93, :108-150), 3 buckets x 2 receipts",
+                    "cpu_sample": "LeNet-5 split 6,1: 61,550 fp32 parameters per owner, 500 rounds after 1 warm-up"})
+    except Exception as e:  # noqa: BLE001
+        out["cpu_error"] = repr(e)[:200]
+    if os.access(REF_CPU_AGGREGATOR, os.X_OK) and os.access(FAKE_OWNERS, os.X_OK):
+        if ports_free(REF_PORTS):
+            try:
+                # the reference's receiver binds its port a second after it is released (network_layer.cpp)
+                out["cpu_e2e_loopback"] = dict(e2e_c1([REF_CPU_AGGREGATOR, "2", "1"], "literal", 8079, startup_s=2.5),
+                                               path="the reference's aggregator process on CPU libtorch: its own "
+                                                    "systemAPI / network_layer / torch::save replies, "
+                                                    "aggregator.cpp:55-167 restated (oracle/ref_cpu_aggregator.cpp)")
+            except Exception as e:  # noqa: BLE001
+                out["cpu_e2e_error"] = repr(e)[:300]
+        else:
+            out["cpu_e2e_error"] = "the reference's fixed ports 8080-8083 are in use"
+    return out
+
+
 CPU_MAX_SAMPLE_BYTES = 36 << 30  # host memory one CPU leg may fill (C4's whole config, 35.7 GB, fits)
 
 
@@ -194,6 +293,8 @@ def cpu_baseline(D, n, reps, dt="f32", skip=None):
                                 "cpu_sample": what + ", 3 timed reps", "cpu_ms_per_round": round(rc["avg_s"] * 1e3, 2)}
                 except Exception as e:  # noqa: BLE001
                     per[key] = {"cpu_error": repr(e)[:200]}
+            if budget_left() - 250 > 20:  # BASELINE C1: the reference's CPU aggregator over loopback, its loop
+                per["round_c1"] = cpu_c1(threads, cpu_model)
             for key, spec, mp, receipts, what in CPU_RECEIVE_LOOPS:
                 try:
                     lit = run(["bench-literal"] + list(spec) + [receipts, threads, mp], timeout=leg_timeout(120))
@@ -556,10 +657,14 @@ class Setup:
 # model_part 1 (aggregator.cpp:59-93), phase 2 the last-part layers 2..L+1 (:108-150).
 ROUNDS = {
     # name: (clients, dtype, phase-1 bucket, phase-2 buckets, description)
+    "round_c1": (2, "f32", 50_536, [10_164, 850], "LeNet-5 split 6,1, 2 owners, fp32"),
     "round_c2": (8, "f32", 83_584, [9_442_304, 5_130], "ResNet-18 split 3,8, 8 owners, fp32"),
     "round_c3": (32, "bf16", 2_594_688, [29_511_680, 5_130], "ResNet-101 split 10,19, 32 owners, bf16"),
     "round_c4": (64, "f32", 38_720, [2_359_808, 119_586_826], "VGG-19 split 3,19, 64 owners, fp32"),
 }
+
+
+ROUND_MAX_SETS = 16
 
 
 class RoundSetup:
@@ -574,7 +679,9 @@ class RoundSetup:
         self.s = 4 if dt == "f32" else 2
         self.sizes = [p1] + list(p2)
         set_bytes = D * sum(self.sizes) * self.s
-        self.nsets = max(1, -(-min_rotate_bytes // set_bytes))
+        # C1's whole round is 0.5 MB: it sits in L2 / the MALL whatever the rotation (its round is launch-bound),
+        # so a few sets suffice; the other rounds rotate past the MALL as the workloads do
+        self.nsets = min(ROUND_MAX_SETS, max(1, -(-min_rotate_bytes // set_bytes)))
         self.agg = fa.Aggregator(devices=[device])
         for st in range(self.nsets):
             for j, n in enumerate(self.sizes):
@@ -669,16 +776,12 @@ def device_to_host(ptr, count, dtype):
     return out
 
 
-def read_stream_peak(fa, torch, setup, stream, reps=7):
-    """Measured read-STREAM peak on this run's own client slots: a read-only launch over
-    the D buckets -- from one phase up the phased kernel itself with its output stream switched off
-    (fa_diag_read_stream) -- median of `reps` HIP-event timings on the launch stream.  GB/s of bytes
-    read; frac_of_read_stream = achieved / this, i.e. what the output stream costs on top of the reads.
-    The probe reads bytes: a bf16 slot is read as the fp32 words its bytes make (the same bytes, the same
-    addresses), so a bf16 workload gets the read rate of its own input too."""
-    # one read-only launch per range piece (a bucket set held in pieces, e.g. C5 on one GPU, is reduced one
-    # launch per piece too): bytes of all pieces / the sum of their median times.  The reps rotate over the
-    # input sets as the timed loop does, so a set that fits the MALL is not read back from it.
+def _read_rate(torch, setup, stream, launch, reps):
+    """GB/s of one read-only launch form over the setup's client slots: one launch per range piece (a bucket
+    set held in pieces, e.g. C5 on one GPU, is reduced one launch per piece too), bytes of all pieces / the
+    sum of their median HIP-event times on the launch stream.  The reps rotate over the input sets as the
+    timed loop does, so a set that fits the MALL is not read back from it.  A bf16 slot is read as the fp32
+    words its bytes make (the same bytes, the same addresses)."""
     sets = [[setup.agg.pieces(s, 0, k) for k in range(setup.D)] for s in range(setup.nsets)]
     nbytes, t_ms = 0, 0.0
     for j in range(len(sets[0][0])):
@@ -689,7 +792,7 @@ def read_stream_peak(fa, torch, setup, stream, reps=7):
             ptrs = [pc[j][0] for pc in sets[i % setup.nsets]]
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(stream)
-            fa.diag_read_stream(ptrs, n, stream=stream)
+            launch(ptrs, n)
             b.record(stream)
             b.synchronize()
             if i >= 2:
@@ -697,6 +800,30 @@ def read_stream_peak(fa, torch, setup, stream, reps=7):
         nbytes += setup.D * n * 4
         t_ms += statistics.median(ms)
     return round(nbytes / (t_ms * 1e-3) / 1e9, 1)
+
+
+def read_stream_peak(fa, torch, setup, stream, reps=7):
+    """Measured read-STREAM peak on this run's own client slots: a read-only launch over the D
+    buckets -- from one phase up the phased kernel itself with its output stream switched off
+    (fa_diag_read_stream).  frac_of_read_stream = achieved / this, i.e. what the output stream costs on top
+    of the product's own reads."""
+    return _read_rate(torch, setup, stream, lambda ptrs, n: fa.diag_read_stream(ptrs, n, stream=stream), reps)
+
+
+READ_PLAIN_FORMS = [(g, u) for g in (2048, 4096, 8192, 16384) for u in (8, 16)]
+
+
+def read_plain_peak(fa, torch, setup, stream, reps=5):
+    """The independent read ceiling on the same slots: the best of plain grid-stride nt read launches
+    (fa_diag_read_plain, tools/hbm_probe.hip's read kernel; grids x loads in flight of READ_PLAIN_FORMS),
+    which share nothing with the product kernels' access pattern.  Returns {GB/s, the best form, every form}."""
+    rates = {}
+    for g, u in READ_PLAIN_FORMS:
+        rates["grid%d_u%d" % (g, u)] = _read_rate(
+            torch, setup, stream, lambda ptrs, n: fa.diag_read_plain(ptrs, n, grid=g, unroll=u, stream=stream), reps)
+    best = max(rates, key=rates.get)
+    return {"GBs": rates[best], "form": best, "forms": rates,
+            "kernel": "plain grid-stride read, 256 lanes per workgroup, nt 16-byte loads, slot after slot"}
 
 
 def timed_loop(torch, setup, steps, warmup, stream, dist, barrier, per_launch=10):
@@ -1013,6 +1140,8 @@ def main():
     achieved = setup.algo_bytes() / (kavg * 1e-3) / 1e9
     read_peak = read_stream_peak(fa, torch, setup, stream) if args.layout == "range" and not under_profiler() \
         else None
+    read_ind = read_plain_peak(fa, torch, setup, stream) if args.layout == "range" and not under_profiler() \
+        else None
     # ranks sharing one GPU (rehearsal) run the one-shot walk, so no committed profile of the phased kernel
     # describes their launches: no traffic then
     committed = (None, None) if shared_gpus else traffic_from_profile(args.workload, world,
@@ -1052,7 +1181,10 @@ def main():
                                                          else "its clients' local reduction"),
                      "phased_meeting_timeouts": int(max_over_ranks(timeouts)),
                      "read_stream_peak": read_peak, "frac_of_read_stream":
-                         round(achieved / read_peak, 4) if read_peak else None},
+                         round(achieved / read_peak, 4) if read_peak else None,
+                     "read_stream_peak_independent": read_ind["GBs"] if read_ind else None,
+                     "frac_of_read_stream_independent": round(achieved / read_ind["GBs"], 4) if read_ind else None,
+                     "read_stream_peak_independent_detail": read_ind},
         "cpu_baseline": cpu,
         "parity": par,
     }
@@ -1291,6 +1423,7 @@ def single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier):
         achieved = s.algo_bytes() / (ka * 1e-3) / 1e9
         # the same config's own read-only rate (its slots, its size): how far its kernel is from reading alone
         rp = None if under_profiler() else read_stream_peak(fa, torch, s, stream)
+        ri = None if under_profiler() else read_plain_peak(fa, torch, s, stream, reps=3)
         sec[name] = {"description": sdesc, "gib_s": round(s.input_bytes() * max(10, args.steps) / w2 / 2**30, 1),
                      "kernel_ms_avg": round(ka, 4),
                      "achieved_GBs": round(achieved, 1),
@@ -1298,6 +1431,9 @@ def single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier):
                      "traffic": traffic_from_profile(name, 1)[0],
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "read_stream_peak": rp, "frac_of_read_stream": round(achieved / rp, 4) if rp else None,
+                     "read_stream_peak_independent": ri["GBs"] if ri else None,
+                     "read_stream_peak_independent_form": ri["form"] if ri else None,
+                     "frac_of_read_stream_independent": round(achieved / ri["GBs"], 4) if ri else None,
                      "input_sets_rotated": s.nsets, "parity": parity_guarded(lambda: s.parity(0))}
         s.close()
 
@@ -1316,6 +1452,20 @@ def single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier):
                 "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "input_sets_rotated": s.nsets,
                 "parity": parity_guarded(lambda: s.parity())}
             s.close()
+
+    # BASELINE C1 end to end: the drop-in process fa_aggregator on this GPU against the fake owners over
+    # loopback, FedAvg (owners at once) and the reference-literal mode (owners in turn, as the CPU reference
+    # leg runs); both checked reply by reply against the oracle
+    if os.access(FA_AGGREGATOR, os.X_OK) and os.access(FAKE_OWNERS, os.X_OK):
+        c1 = sec.setdefault("round_c1", {})
+        for mode in ("fedavg", "literal"):
+            try:
+                base = free_port_base()
+                c1["e2e_loopback_" + mode] = e2e_c1(
+                    [FA_AGGREGATOR, "-i", "-1", "-d", "2", "-c", "1", "--mode", mode, "--rounds", str(C1_E2E_ROUNDS),
+                     "--port-base", str(base)], mode, base)
+            except Exception as e:  # noqa: BLE001
+                c1["e2e_loopback_" + mode] = {"error": repr(e)[:300]}
 
     def one(key, s, desc):
         torch.cuda.synchronize()

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 5
+#define FA_ABI_VERSION 6
 
 typedef struct fa_ctx fa_ctx; /* opaque: device slots, streams, pinned staging */
 
@@ -69,8 +69,9 @@ typedef enum {
 #define FA_ACCUMULATE_ON_ARRIVAL 0x4
 /* Test only: accept a device id more than once (several shards of one context on one GPU), so the
  * multi-GPU host logic runs on a one-GPU box.  RCCL refuses two ranks on one device, so with
- * FA_SHARD_CLIENT_RS the reduce-scatter is replaced by its definition (each shard block := the sum of
- * the GPUs' partials in rank order, a device launch); everything else of the layout is unchanged. */
+ * FA_SHARD_CLIENT_RS the reduce-scatter is replaced by its definition (shard g's block := the sum of the
+ * GPUs' partials in ring order, starting at rank g + 1 and ending at rank g as a ring reduce-scatter
+ * accumulates it; one device launch); everything else of the layout is unchanged. */
 #define FA_TEST_SHARED_DEVICE 0x100
 
 int fa_version(void);
@@ -206,6 +207,14 @@ int fa_sync_part(fa_ctx* ctx, int part_id, const float* h_weights, void* hip_str
  * grid was not co-resident -- the GPU was shared with other kernels -- and those launches ran slower;
  * results are unaffected.  Synchronizes with the device. */
 int fa_phased_timeouts(int device, uint64_t* count);
+
+/* The phased kernel gives each HIP stream it runs on a counter slot of its own on that device (the first
+ * 48 streams; later ones share hashed slots, which costs speed, never results).  A context returns its own
+ * streams' slots in fa_destroy; a caller that passed its own stream (fa_reduce_device, fa_sync_device,
+ * fa_reduce_part / fa_reduce_parts / fa_sync_part with hip_stream) returns that stream's slot here before it
+ * destroys or stops using the stream, so a long-lived process cycling through many streams keeps owned
+ * slots.  Launches still in flight on the stream stay correct.  A stream without a slot: FA_OK, no-op. */
+int fa_release_stream(int device, void* hip_stream);
 
 /* Literal mode divisor used by fa_reduce_device when ctx == NULL. */
 #define FA_DEFAULT_DIVISOR 1000.0f

@@ -11,6 +11,8 @@ m >= 2 = parts[1].layers[m-2]), a *client slot* is one data owner's receipt.
 """
 import ctypes
 import os
+import threading
+import weakref
 
 import numpy as np
 
@@ -86,9 +88,11 @@ def lib():
         "fa_ctx_get_tuning": (I, [P, ctypes.POINTER(_Tuning)]),
         "fa_rs_segments": (I, [S, I, I, I, ctypes.POINTER(S), I]),
         "fa_phased_timeouts": (I, [I, ctypes.POINTER(U64)]),
+        "fa_release_stream": (I, [I, P]),
         "fa_reduce_device": (I, [P, I, P, P, I, S, I, P, I, I, P, P]),
         "fa_fill_uniform": (I, [P, S, I, U64, U32, U64, P]),
         "fa_diag_read_stream": (I, [P, I, S, P]),  # diagnostics (outside fa.h)
+        "fa_diag_read_plain": (I, [P, I, S, I, I, P]),
         "fa_diag_plan_chain": (I, [I, I, S, I, I, I, ctypes.POINTER(I), ctypes.POINTER(ctypes.c_longlong)]),
         "fa_diag_rs_plan": (I, [S, I, I, I, I, I, I, ctypes.POINTER(I), ctypes.POINTER(I),
                                 ctypes.POINTER(ctypes.c_longlong)]),
@@ -135,12 +139,53 @@ def _addr(x):
     raise TypeError("need a tensor, array or int address, got %r" % type(x))
 
 
+# Caller streams handed to the library as torch stream objects: (device, hipStream_t) -> live Python objects
+# wrapping it.  When the last one is collected the stream is retired and its phased counter slot goes back
+# (fa_release_stream); torch's pooled streams are wrapped again later, and simply take a slot anew.
+_tracked = {}
+_tracked_mu = threading.Lock()
+
+
+def _untrack(key):
+    with _tracked_mu:
+        _tracked[key] -= 1
+        if _tracked[key]:
+            return
+        del _tracked[key]
+    try:
+        if _lib is not None:
+            _lib.fa_release_stream(key[0], key[1])
+    except Exception:  # interpreter shutdown
+        pass
+
+
 def _stream(stream):
     if stream is None:
         return None
     if isinstance(stream, int):
         return stream
-    return stream.cuda_stream  # torch.cuda.Stream on ROCm wraps a hipStream_t
+    h = stream.cuda_stream  # torch.cuda.Stream on ROCm wraps a hipStream_t
+    if h and not getattr(stream, "_fa_tracked", False):
+        dev = stream.device.index if getattr(stream, "device", None) is not None else 0
+        key = (dev or 0, h)
+        try:
+            weakref.finalize(stream, _untrack, key)
+            stream._fa_tracked = True
+        except (TypeError, AttributeError):  # an object that cannot be tracked: release_stream() by hand
+            return h
+        with _tracked_mu:
+            _tracked[key] = _tracked.get(key, 0) + 1
+    return h
+
+
+def release_stream(stream, device=None):
+    """fa_release_stream: give back the phased kernel's owned counter slot of a caller stream (a torch stream
+    object or a raw hipStream_t address) before destroying it.  Torch stream objects passed to this module
+    are released by themselves when collected; raw handles need this call."""
+    if device is None:
+        device = stream.device.index if hasattr(stream, "device") and stream.device.index is not None else 0
+    h = stream if isinstance(stream, int) else stream.cuda_stream
+    check(lib().fa_release_stream(device, h))
 
 
 def reduce_device(clients, weights, n, in_dtype, out, out_dtype=F32, mode=FEDAVG, init=None, stream=None, gpu=0,
@@ -175,6 +220,14 @@ def diag_read_stream(buffers, n, stream=None):
     (n elements each, n % 4 == 0, 16-byte aligned) on `stream`; time it with events on that stream."""
     arr = (ctypes.c_void_p * len(buffers))(*[_addr(b) for b in buffers])
     check(lib().fa_diag_read_stream(arr, len(buffers), n, _stream(stream)))
+
+
+def diag_read_plain(buffers, n, grid=8192, unroll=16, stream=None):
+    """fa_diag_read_plain (diagnostic, outside fa.h): the independent read ceiling -- one plain grid-stride
+    launch (`grid` workgroups of 256 lanes, `unroll` nt 16-byte loads in flight) reading the fp32 device
+    buffers (n elements each) one after another, on `stream`."""
+    arr = (ctypes.c_void_p * len(buffers))(*[_addr(b) for b in buffers])
+    check(lib().fa_diag_read_plain(arr, len(buffers), n, grid, unroll, _stream(stream)))
 
 
 PLAN_ONE_SHOT, PLAN_SCALAR, PLAN_PHASED = 0, 1, 2

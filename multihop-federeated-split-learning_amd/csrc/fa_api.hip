@@ -1748,6 +1748,15 @@ int fa_sync_part(fa_ctx* ctx, int part_id, const float* h_weights, void* hip_str
     return FA_OK;
 }
 
+int fa_release_stream(int device, void* hip_stream) {
+    g_err.clear();
+    int n = 0;
+    FA_HIP(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) return fail(FA_ERR_ARG, "device %d", device);
+    fa::phased_release_stream(device, static_cast<hipStream_t>(hip_stream));
+    return FA_OK;
+}
+
 int fa_phased_timeouts(int device, uint64_t* count) {
     g_err.clear();
     if (!count) return fail(FA_ERR_ARG, "count is null");
@@ -1756,27 +1765,56 @@ int fa_phased_timeouts(int device, uint64_t* count) {
     return FA_OK;
 }
 
+namespace {
+// a 256-byte device word per device for the read diagnostics' never-taken store
+int read_sink(float** out) {
+    static float* sinks[64] = {};
+    static std::mutex mu;
+    int dev = 0;
+    FA_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return fail(FA_ERR_ARG, "device %d", dev);
+    std::lock_guard<std::mutex> lk(mu);
+    if (!sinks[dev]) FA_HIP(hipMalloc((void**)&sinks[dev], 256));
+    *out = sinks[dev];
+    return FA_OK;
+}
+
+int read_table(const void* const* d_bufs, int nc, size_t n, fa::ClientTable* t) {
+    if (!d_bufs || nc < 1 || nc > fa::kMaxClients || n % 4) return fail(FA_ERR_ARG, "bad read-stream arguments");
+    for (int k = 0; k < nc; ++k) {
+        if (!d_bufs[k] || (uintptr_t)d_bufs[k] % 16) return fail(FA_ERR_ARG, "buffer %d null or misaligned", k);
+        t->src[k] = d_bufs[k];
+    }
+    return FA_OK;
+}
+}  // namespace
+
 // Diagnostic, not part of the ABI in fa.h: one read-stream probe launch over nc device buffers of n fp32
 // elements each (16-byte aligned, n a multiple of 4, nc <= 128) on `hip_stream`, enqueued; bench.py times
 // it with events on that stream (roofline.read_stream_peak).
 extern "C" int fa_diag_read_stream(const void* const* d_bufs, int nc, size_t n, void* hip_stream) {
     g_err.clear();
-    if (!d_bufs || nc < 1 || nc > fa::kMaxClients || n % 4) return fail(FA_ERR_ARG, "bad read-stream arguments");
     fa::ClientTable t{};
-    for (int k = 0; k < nc; ++k) {
-        if (!d_bufs[k] || (uintptr_t)d_bufs[k] % 16) return fail(FA_ERR_ARG, "buffer %d null or misaligned", k);
-        t.src[k] = d_bufs[k];
-    }
-    static float* sinks[64] = {};  // per device
-    static std::mutex mu;
-    int dev = 0;
-    FA_HIP(hipGetDevice(&dev));
-    if (dev < 0 || dev >= 64) return fail(FA_ERR_ARG, "device %d", dev);
-    {
-        std::lock_guard<std::mutex> lk(mu);
-        if (!sinks[dev]) FA_HIP(hipMalloc((void**)&sinks[dev], 256));
-    }
-    FA_HIP(fa::launch_read_probe(t, nc, (int64_t)(n / 4), sinks[dev], static_cast<hipStream_t>(hip_stream)));
+    float* sink = nullptr;
+    int rc;
+    if ((rc = read_table(d_bufs, nc, n, &t)) || (rc = read_sink(&sink))) return rc;
+    FA_HIP(fa::launch_read_probe(t, nc, (int64_t)(n / 4), sink, static_cast<hipStream_t>(hip_stream)));
+    return FA_OK;
+}
+
+// Diagnostic, not part of the ABI in fa.h: the independent read ceiling -- a plain grid-stride read of the
+// same buffers (grid workgroups of 256 lanes, `unroll` 8 or 16 non-temporal 16-byte loads in flight per
+// lane, buffer after buffer), none of the product kernels' structure; bench.py times it on the launch stream
+// (roofline.read_stream_peak_independent).
+extern "C" int fa_diag_read_plain(const void* const* d_bufs, int nc, size_t n, int grid, int unroll,
+                                  void* hip_stream) {
+    g_err.clear();
+    if (grid < 1 || grid > (1 << 20) || (unroll != 8 && unroll != 16)) return fail(FA_ERR_ARG, "bad grid or unroll");
+    fa::ClientTable t{};
+    float* sink = nullptr;
+    int rc;
+    if ((rc = read_table(d_bufs, nc, n, &t)) || (rc = read_sink(&sink))) return rc;
+    FA_HIP(fa::launch_read_plain(t, nc, (int64_t)(n / 4), grid, unroll, sink, static_cast<hipStream_t>(hip_stream)));
     return FA_OK;
 }
 

@@ -91,5 +91,7 @@ hipError_t launch_fill(void* dst, int64_t n, fa_dtype dt, uint64_t seed, uint32_
                        hipStream_t s);
 // Read-stream probe over nc f32 buffers of nvec 16-byte vectors (16-byte aligned); nothing is written.
 hipError_t launch_read_probe(const ClientTable& t, int nc, int64_t nvec, float* sink, hipStream_t s);
+hipError_t launch_read_plain(const ClientTable& t, int nc, int64_t nvec, int grid, int unroll, float* sink,
+                             hipStream_t s);
 
 }  // namespace fa

@@ -1314,6 +1314,39 @@ hipError_t launch_read_probe(const ClientTable& t, int nc, int64_t nvec, float* 
     return hipGetLastError();
 }
 
+// Independent read ceiling (roofline.read_stream_peak_independent): nothing of the product's access pattern --
+// a plain grid-stride walk with U non-temporal 16-byte loads in flight per lane, buffer after buffer within one
+// launch (tools/hbm_probe.hip's read kernel over the same slots).  The sum is stored only if it equals a value
+// uniform[-1,1) inputs never produce, so nothing is written and nothing is elided.
+template <int U>
+__global__ __launch_bounds__(256) void read_plain_kernel(const ClientTable t, int nc, int64_t nvec, float* sink) {
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < nc; ++k) {
+        const f32x4* p = static_cast<const f32x4*>(t.src[k]);
+        int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+        for (; v + (U - 1) * stride < nvec; v += U * stride) {
+            f32x4 x[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) x[u] = __builtin_nontemporal_load(p + v + u * stride);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc += x[u];
+        }
+        for (; v < nvec; v += stride) acc += __builtin_nontemporal_load(p + v);
+    }
+    const float sum = acc.x + acc.y + acc.z + acc.w;
+    if (sum == 1.0e30f) sink[0] = sum;
+}
+
+hipError_t launch_read_plain(const ClientTable& t, int nc, int64_t nvec, int grid, int unroll, float* sink,
+                             hipStream_t s) {
+    if (unroll == 8)
+        hipLaunchKernelGGL(read_plain_kernel<8>, dim3((unsigned)grid), dim3(256), 0, s, t, nc, nvec, sink);
+    else
+        hipLaunchKernelGGL(read_plain_kernel<16>, dim3((unsigned)grid), dim3(256), 0, s, t, nc, nvec, sink);
+    return hipGetLastError();
+}
+
 hipError_t launch_fill(void* dst, int64_t n, fa_dtype dt, uint64_t seed, uint32_t client, uint64_t idx0,
                        hipStream_t s) {
     Tuning tu{256, 8192, 8, 0, 0};

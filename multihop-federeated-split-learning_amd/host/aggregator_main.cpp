@@ -188,22 +188,44 @@ public:
     }
     ~Aggregator() { fa_destroy(ctx_); }
 
-    // Stale receipts across rounds (host/receipts.h): a receipt its owner sent before its receipts of the
-    // previous phase, or a copy of one already reduced, is dropped -- never counted, never in a slot.
+    // Stale receipts across rounds (host/receipts.h): a byte copy of a receipt its owner already had reduced
+    // (a late copy of an earlier round's) is dropped -- never counted, never in a slot.
     void end_phase() { ledger_.end_phase(); }
+
+    static ReceiptKey key_of(const Receipt& r) {
+        return ReceiptKey{r.t_start, r.blob_len, archive_fingerprint(r.blob(), r.blob_len)};
+    }
+
+    // A receipt of the other phase is never taken (see main): counted as a stale copy when it is a byte copy
+    // of one already reduced, else as ignored (a retransmission of this round's).
+    void other_phase(const Receipt& r, int phase) {
+        if (ledger_.is_reduced_copy(r.client_id, r.model_part, key_of(r))) {
+            std::cerr << "[aggregator] stale part " << r.model_part << " from owner " << r.client_id
+                      << " during phase " << phase << " (a byte copy of a receipt already reduced): dropped\n";
+            ++stale_dropped_;
+        } else {
+            std::cerr << "[aggregator] part " << r.model_part << " from owner " << r.client_id << " during phase "
+                      << phase << " (a retransmission of this round's): ignored\n";
+            ++ignored_;
+        }
+    }
 
     // Consumes one receipt of bucket `mp` into its client slot.  Returns whether it is the first receipt of
     // this (owner, bucket) in the round: a retransmission replaces the slot's contents (the newest one wins,
     // as a second torch::load would) but is not another receipt -- the phase waits for D distinct owners.
     // A stale receipt (above) is dropped: returns false without touching the slot.
     bool absorb(const Receipt& r) {
-        const uint64_t fp = archive_fingerprint(r.blob(), r.blob_len);
-        const std::string why = ledger_.stale(r.client_id, r.model_part, r.t_start, fp);
-        if (!why.empty()) {
-            std::cerr << "[aggregator] stale part " << r.model_part << " from owner " << r.client_id << " (" << why
+        const ReceiptKey key = key_of(r);
+        const ReceiptLedger::Verdict v = ledger_.check(r.client_id, r.model_part, key);
+        if (v.stale) {
+            std::cerr << "[aggregator] stale part " << r.model_part << " from owner " << r.client_id << " (" << v.why
                       << "): dropped\n";
             ++stale_dropped_;
             return false;
+        }
+        if (!v.note.empty()) {
+            std::cerr << "[aggregator] part " << r.model_part << " from owner " << r.client_id << " " << v.note << "\n";
+            ++clock_back_;
         }
         const auto t0 = std::chrono::steady_clock::now();
         TorchArchive ar;
@@ -249,11 +271,14 @@ public:
             FA_CHECK(fa_submit(ctx_, r.model_part, slot, flat.data(), weight_of(r.client_id)));
         }
         b.bytes_in += r.blob_len;
-        ledger_.accept(r.client_id, r.model_part, r.t_start, fp);
+        ledger_.accept(r.client_id, r.model_part, key);
         const bool first = b.arrived.insert(r.client_id).second;
         b.last = r;  // template of the reply: the last receipt (its buffers travel back, as in the reference)
         st_.absorb_s += secs_since(t0);
-        if (!first) std::cerr << "[aggregator] part " << r.model_part << ": owner " << r.client_id << " sent it again\n";
+        if (!first) {
+            std::cerr << "[aggregator] part " << r.model_part << ": owner " << r.client_id << " sent it again\n";
+            ++replaced_;
+        }
         return first;
     }
 
@@ -313,6 +338,9 @@ public:
 
     size_t bytes_in(int mp) { return buckets_[mp].bytes_in; }
     unsigned long long stale_dropped() const { return stale_dropped_; }
+    unsigned long long ignored() const { return ignored_; }
+    unsigned long long replaced() const { return replaced_; }
+    unsigned long long clock_back() const { return clock_back_; }
 
     // The data owners whose receipt of bucket mp has not arrived this round ("mp 2: 4 7 9").
     std::string missing(const std::vector<int>& mps) {
@@ -392,7 +420,8 @@ private:
     std::vector<int> expected_;  // the data owners' ids in slot order
     Stats st_;
     ReceiptLedger ledger_;
-    unsigned long long stale_dropped_ = 0;
+    // cumulative receipt accounting, printed with every round
+    unsigned long long stale_dropped_ = 0, ignored_ = 0, replaced_ = 0, clock_back_ = 0;
 };
 
 // The next receipt, with the failure detection the reference lacks (its receive loop blocks forever on a
@@ -466,15 +495,16 @@ int main(int argc, char** argv) {
         // (data_owner.cpp:228-245), which goes out after phase 1 ends, and its next part 1 only after every
         // phase-2 reply, which goes out after phase 2 ends.  So it is ignored (named in the log), never carried
         // into a later phase, where it would stand for a receipt its owner has not sent yet.  A late copy of
-        // the SAME phase's bucket from an earlier round is caught by its t_start (ReceiptLedger) and
-        // dropped (host/receipts.h); the round line counts them (stale_dropped).
+        // the SAME phase's bucket from an earlier round is a byte copy of a receipt already reduced, caught by
+        // its (t_start, length, content) key and dropped (ReceiptLedger, host/receipts.h).  The round line
+        // counts, cumulatively: stale_dropped (byte copies, either phase), ignored (other-phase receipts that
+        // are not copies), replaced (retransmissions within a phase), clock_back (owner clocks that went back).
         auto t0 = std::chrono::steady_clock::now();
         int received = 0;
         while (received < o.data_owners) {
             Receipt r = wait_receipt(net, o, agg, {1}, round, 1);
             if (r.model_part != 1) {
-                std::cerr << "[aggregator] part " << r.model_part << " from owner " << r.client_id
-                          << " during phase 1 (a retransmission of the last round's): ignored\n";
+                agg.other_phase(r, 1);
                 continue;
             }
             if (agg.absorb(r)) ++received;
@@ -496,8 +526,8 @@ int main(int argc, char** argv) {
         for (int mp = 2; mp <= L + 1; ++mp) mps.push_back(mp);
         while (got < want) {
             Receipt r = wait_receipt(net, o, agg, mps, round, 2);
-            if (r.model_part == 1) {  // a retransmission of this round's part 1 (above), already reduced
-                std::cerr << "[aggregator] part 1 from owner " << r.client_id << " during phase 2: ignored\n";
+            if (r.model_part == 1) {  // a retransmission of this round's part 1 (above), or a late copy
+                agg.other_phase(r, 2);
                 continue;
             }
             if (r.model_part < 2 || r.model_part > L + 1) {
@@ -524,9 +554,11 @@ int main(int argc, char** argv) {
                "\"absorb_s\":%.6f,\"finalize_s\":%.6f,\"frame_s\":%.6f},"
                "\"phase2\":{\"receive_s\":%.6f,\"reduce_s\":%.6f,\"bytes_in\":%zu,\"layers\":%d,"
                "\"absorb_s\":%.6f,\"finalize_s\":%.6f,\"frame_s\":%.6f,\"send_s\":%.6f},"
-               "\"send_failures\":%llu,\"stale_dropped\":%llu}\n",
+               "\"send_failures\":%llu,\"stale_dropped\":%llu,\"ignored\":%llu,\"replaced\":%llu,"
+               "\"clock_back\":%llu}\n",
                round, recv1, red1, in1, s1.absorb_s, s1.finalize_s, s1.frame_s, recv2, red2, in2, L, s2.absorb_s,
-               s2.finalize_s, s2.frame_s, send2, (unsigned long long)net.send_failures(), agg.stale_dropped());
+               s2.finalize_s, s2.frame_s, send2, (unsigned long long)net.send_failures(), agg.stale_dropped(), agg.ignored(),
+               agg.replaced(), agg.clock_back());
         fflush(stdout);
     }
     net.stop();

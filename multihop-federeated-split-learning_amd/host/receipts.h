@@ -2,17 +2,20 @@
 //
 // The reference aggregator counts raw receipts and consumes whatever arrives (aggregator.cpp:59-92,
 // :112-149).  The wire carries no round number, so a delayed copy of an earlier round's receipt would be
-// reduced as if it were this round's.  What the wire does carry is t_start, stamped on the owner's clock by
-// its sender thread when the frame goes out (network_layer.cpp:761), and an owner's sends follow the
-// protocol (data_owner.cpp:224-253): its part 1 of round r+1 only after the phase-2 replies of round r,
-// which go out after its phase-2 receipts of round r arrived; its phase-2 receipts only after the phase-1
-// reply, i.e. after its part 1.  So, per owner:
-//   * the floor of a phase = the newest t_start among the owner's receipts the previous phase reduced; a
-//     receipt sent before it (t_start < floor) belongs to an earlier phase: stale;
-//   * t_start == floor (one millisecond) is decided by content: a byte copy of a receipt the last two phases
-//     reduced (archive_fingerprint) is stale, anything else is new;
-//   * within a phase, a second receipt of (owner, bucket) sent before the one already taken does not
-//     replace it (the newest wins, whichever arrives last).
+// reduced as if it were this round's.  What a late copy is, though, is a BYTE copy of a frame its owner
+// already sent -- header included, so it carries the very t_start its original carried (stamped on the
+// owner's clock by its sender thread when the frame went out, network_layer.cpp:761).  So the ledger
+// keys every receipt it reduced by (owner, bucket, t_start, archive length, content fingerprint) and:
+//   * drops a receipt whose key matches one its owner already had reduced (the last kKeep phases of that
+//     bucket): a late copy or a retransmission that arrived after its phase ended;
+//   * accepts everything else, including a receipt stamped before its owner's previous phase (an owner
+//     clock that stepped back: an NTP step, a VM resume) -- logged, never dropped, since dropping a genuine
+//     receipt would leave the phase waiting forever for an owner that will not resend;
+//   * within a phase, a second receipt of (owner, bucket) replaces the one taken unless it was sent before
+//     it (the newest wins, whichever arrives last).
+// A genuine receipt is only ever mistaken for a copy if it carries the exact millisecond stamp, length and
+// sampled content of an earlier receipt of the same owner and bucket: a clock stepped back onto that very
+// millisecond with the sampled words unchanged.
 // Header-only and free of HIP, so the CPU suite tests it (tests/tools/receipts_selftest.cpp).
 #pragma once
 
@@ -20,16 +23,16 @@
 #include <cstddef>
 #include <cstdint>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <string>
 #include <utility>
-#include <vector>
 
 namespace fahost {
 
 // FNV-1a over the length and 1024 evenly spaced 8-byte words of an archive (and its ragged tail): two
 // rounds' receipts of a bucket differ in (nearly) every parameter, so the sampled words tell them apart; a
-// copy matches.  O(1) in the archive size.
+// copy matches.  O(1) in the archive size; the ledger never relies on it alone (the exact t_start too).
 inline uint64_t archive_fingerprint(const uint8_t* b, size_t len) {
     uint64_t h = 1469598103934665603ull ^ (uint64_t)len;
     const size_t words = len / 8;
@@ -43,56 +46,78 @@ inline uint64_t archive_fingerprint(const uint8_t* b, size_t len) {
     return h;
 }
 
+// What a receipt is, as far as the ledger knows it.
+struct ReceiptKey {
+    long t_start = 0;
+    size_t len = 0;
+    uint64_t fp = 0;
+    bool operator==(const ReceiptKey& o) const { return t_start == o.t_start && len == o.len && fp == o.fp; }
+};
+
 class ReceiptLedger {
 public:
-    // Empty when the receipt is current; else why it is stale.
-    std::string stale(int owner, int model_part, long t_start, uint64_t fp) const {
-        auto fl = floor_.find(owner);
-        if (fl != floor_.end()) {
-            if (t_start < fl->second)
-                return "sent at " + std::to_string(t_start) + ", before its owner's receipts of the previous phase (" +
-                       std::to_string(fl->second) + ")";
-            auto c = consumed_.find(owner);
-            if (t_start == fl->second && c != consumed_.end() &&
-                std::find(c->second.begin(), c->second.end(), fp) != c->second.end())
-                return "a copy of a receipt an earlier phase already reduced";
+    static constexpr size_t kKeep = 64;  // reduced receipts remembered per (owner, bucket): 64 rounds back
+
+    struct Verdict {
+        bool stale = false;
+        std::string why;   // stale: why it is dropped
+        std::string note;  // current but worth a log line (the owner's clock went back)
+    };
+
+    Verdict check(int owner, int model_part, const ReceiptKey& k) const {
+        Verdict v;
+        auto c = consumed_.find({owner, model_part});
+        if (c != consumed_.end() && std::find(c->second.begin(), c->second.end(), k) != c->second.end()) {
+            v.stale = true;
+            v.why = "a byte copy of the receipt sent at " + std::to_string(k.t_start) + ", already reduced";
+            return v;
         }
         auto a = accepted_.find({owner, model_part});
-        if (a != accepted_.end() && t_start < a->second.first)
-            return "sent at " + std::to_string(t_start) + ", before the receipt already taken (" +
-                   std::to_string(a->second.first) + ")";
-        return std::string();
+        if (a != accepted_.end() && k.t_start < a->second.t_start) {
+            v.stale = true;
+            v.why = "sent at " + std::to_string(k.t_start) + ", before the receipt already taken (" +
+                    std::to_string(a->second.t_start) + ")";
+            return v;
+        }
+        auto fl = floor_.find(owner);
+        if (fl != floor_.end() && k.t_start < fl->second)
+            v.note = "sent at " + std::to_string(k.t_start) + ", before its owner's receipts of the previous phase (" +
+                     std::to_string(fl->second) + "): the owner's clock went back; new content, accepted";
+        return v;
+    }
+
+    // Whether the receipt is a byte copy of one already reduced (a receipt of the other phase is never
+    // taken; this tells a late copy from a retransmission of the current round's).
+    bool is_reduced_copy(int owner, int model_part, const ReceiptKey& k) const {
+        auto c = consumed_.find({owner, model_part});
+        return c != consumed_.end() && std::find(c->second.begin(), c->second.end(), k) != c->second.end();
     }
 
     // The receipt was consumed into its slot (it replaces an earlier one of the same (owner, bucket)).
-    void accept(int owner, int model_part, long t_start, uint64_t fp) { accepted_[{owner, model_part}] = {t_start, fp}; }
+    void accept(int owner, int model_part, const ReceiptKey& k) { accepted_[{owner, model_part}] = k; }
 
-    // The phase's buckets are reduced: its receipts set every owner's floor for the next phase, and their
-    // fingerprints join the last two phases' (what a late copy at the floor's millisecond is matched against).
+    // The phase's buckets are reduced: their receipts join the reduced ones, and the newest stamp of each
+    // owner becomes its floor (what a later phase's stamps are compared with, for the clock note).
     void end_phase() {
+        for (auto& kv : accepted_) {
+            auto& q = consumed_[kv.first];
+            q.push_back(kv.second);
+            if (q.size() > kKeep) q.pop_front();
+        }
         std::map<int, long> fl;
-        std::map<int, std::vector<uint64_t>> fps;
         for (auto& kv : accepted_) {
             const int owner = kv.first.first;
             auto it = fl.find(owner);
-            fl[owner] = it == fl.end() ? kv.second.first : std::max(it->second, kv.second.first);
-            fps[owner].push_back(kv.second.second);
+            fl[owner] = it == fl.end() ? kv.second.t_start : std::max(it->second, kv.second.t_start);
         }
         for (auto& kv : fl) floor_[kv.first] = kv.second;
-        for (auto& kv : fps) {
-            auto& prev = last_phase_fps_[kv.first];
-            std::vector<uint64_t> both = prev;
-            both.insert(both.end(), kv.second.begin(), kv.second.end());
-            consumed_[kv.first] = both;
-            prev = kv.second;
-        }
         accepted_.clear();
     }
 
 private:
-    std::map<int, long> floor_;                                   // owner -> t_start floor of this phase
-    std::map<int, std::vector<uint64_t>> consumed_, last_phase_fps_;  // owner -> the last two / last phase's
-    std::map<std::pair<int, int>, std::pair<long, uint64_t>> accepted_;  // (owner, bucket) -> (t_start, fp)
+    std::map<int, long> floor_;                                      // owner -> newest stamp of its last phase
+    std::map<std::pair<int, int>, std::deque<ReceiptKey>> consumed_;  // (owner, bucket) -> reduced receipts
+    std::map<std::pair<int, int>, ReceiptKey> accepted_;              // (owner, bucket) -> taken this phase
 };
 
 }  // namespace fahost

@@ -20,6 +20,8 @@
 //   golden  <name> <type> <start> <end> <nc> <D> <seed> <wseed> <outdir> [blob_mp; -1 = every bucket <= 200k]
 //   bench-fedavg <n> <D> <threads> <reps> [bf16]
 //   bench-literal <name> <type> <start> <end> <nc> <D> <threads> <model_part> [arith]
+//   bench-round <name> <type> <start> <end> <nc> <D> <threads> <rounds>
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -322,11 +324,48 @@ int cmd_bench_literal(int argc, char** argv) {
     return 0;
 }
 
+// A whole aggregation round of the reference's receive loop, network aside: phase 1 = D receipts of
+// model_part 1, phase 2 = D receipts of every last-part layer (aggregator.cpp:59-93, :108-150), each
+// receipt torch::load'ed and folded (literal_receipt).  Blobs are made before the clock; `rounds` rounds are
+// timed after one warm-up round.  Reports ms per round and GiB/s of parameters received.
+int cmd_bench_round(int argc, char** argv) {
+    int name = atoi(argv[2]), type = atoi(argv[3]), start = atoi(argv[4]), end = atoi(argv[5]), nc = atoi(argv[6]);
+    int D = atoi(argv[7]), threads = atoi(argv[8]), rounds = atoi(argv[9]);
+    at::set_num_threads(threads);
+    AggState agg = build_state(name, type, start, end, nc);
+    auto bs = buckets_of(agg);
+    std::vector<std::vector<std::string>> blobs(bs.size());
+    int64_t params = 0;
+    for (size_t b = 0; b < bs.size(); ++b) {
+        params += param_numel(bs[b].global);
+        for (int k = 0; k < D; ++k) {
+            auto cm = client_module(name, type, start, end, nc, bs[b].model_part);
+            fill_client(cm, bucket_seed(0x5EED, bs[b].model_part), k);
+            blobs[b].push_back(save_blob(cm));
+        }
+    }
+    std::vector<double> ms;
+    for (int r = 0; r < rounds + 1; ++r) {
+        const double t0 = now_s();
+        for (size_t b = 0; b < bs.size(); ++b)
+            for (int k = 0; k < D; ++k) literal_receipt(bs[b], blobs[b][(size_t)k], 1000);
+        if (r) ms.push_back((now_s() - t0) * 1e3);
+    }
+    std::sort(ms.begin(), ms.end());
+    double avg = 0;
+    for (double x : ms) avg += x / ms.size();
+    printf("{\"mode\":\"round\",\"buckets\":%zu,\"params\":%lld,\"D\":%d,\"threads\":%d,\"rounds\":%d,"
+           "\"round_ms_avg\":%.4f,\"round_ms_median\":%.4f,\"gib_s\":%.4f}\n",
+           bs.size(), (long long)params, D, threads, rounds, avg, ms[ms.size() / 2],
+           (double)D * params * 4 / (avg * 1e-3) / (1ull << 30));
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
     if (argc < 2) {
-        fprintf(stderr, "usage: ref_harness layout|golden|bench-fedavg|bench-literal ...\n");
+        fprintf(stderr, "usage: ref_harness layout|golden|bench-fedavg|bench-literal|bench-round ...\n");
         return 2;
     }
     std::string mode = argv[1];
@@ -345,6 +384,8 @@ int main(int argc, char** argv) {
         rc = cmd_bench_fedavg(argc, argv);
     } else if (mode == "bench-literal" && argc >= 10) {
         rc = cmd_bench_literal(argc, argv);
+    } else if (mode == "bench-round" && argc >= 10) {
+        rc = cmd_bench_round(argc, argv);
     } else {
         fprintf(stderr, "bad arguments\n");
     }

@@ -53,7 +53,7 @@ def test_library_is_gfx950_code(fa, tmp_path):
 
 def test_version_and_errors_without_gpu(fa):
     L = fa.lib()
-    assert L.fa_version() == 5
+    assert L.fa_version() == 6
     # argument errors are reported before any device work
     rc = L.fa_reduce_device(None, 0, None, None, 0, 16, 0, None, 0, 0, None, None)
     assert rc == fa.ERR_ARG and "null" in fa.last_error()

@@ -220,15 +220,9 @@ def test_retransmitted_receipts_count_once(torch_gpu, extra):
             agg.kill()
 
 
-@pytest.mark.parametrize("extra", [[], ["--eager"], ["--mode", "literal"]])
-def test_late_duplicates_of_earlier_rounds_are_dropped(torch_gpu, extra):
-    """Owner 2 re-sends its previous round's receipts during the next round, once before and once after the
-    current ones (fake_owners --retransmit-late).  The wire has no round number; fa_aggregator tells them
-    apart by t_start (stamped when the owner sends, network_layer.cpp:761) and by content, so a late copy
-    neither counts as the owner's receipt nor replaces the newer one: every reply of every round stays
-    bit-exact against the oracle over THIS round's values, and the log names the dropped copies
-    (aggregator.cpp:59-92 would reduce the stale parameters without a word)."""
-    D, rounds, base = 4, 3, pick_base()
+def _run_late_copies(extra, owner_flags, rounds=3, D=4):
+    """fa_aggregator against fake owners with the given failure injection; returns the round lines."""
+    base = pick_base()
     agg = subprocess.Popen([AGG, "-i", "-1", "-d", str(D), "-c", "1", "--rounds", str(rounds), "--port-base",
                             str(base), "--stall-report", "5", "--receipt-timeout", "30"] + extra,
                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
@@ -236,7 +230,7 @@ def test_late_duplicates_of_earlier_rounds_are_dropped(torch_gpu, extra):
         time.sleep(0.5)
         r = subprocess.run([OWNERS, "--blobs", os.path.join(GOLDEN, "lenet5_c1"), "--parts", "1,2,3", "-d", str(D),
                             "-c", "1", "--rounds", str(rounds), "--port-base", str(base), "--model-name", "2",
-                            "--start", "6", "--end", "1", "--retransmit-late", "2", "--reply-timeout", "60"]
+                            "--start", "6", "--end", "1", "--reply-timeout", "60"] + owner_flags
                            + (["--mode", "literal"] if "literal" in extra else []),
                            capture_output=True, text=True, timeout=180)
         assert r.returncode == 0, r.stderr[-2000:]
@@ -246,11 +240,51 @@ def test_late_duplicates_of_earlier_rounds_are_dropped(torch_gpu, extra):
         assert agg.returncode == 0, err[-2000:]
         lines = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
         assert len(lines) == rounds
-        assert lines[-1]["stale_dropped"] >= 1 and "stale part" in err, err[-2000:]
-        assert lines[0]["stale_dropped"] == 0  # round 0 has no earlier round to be late from
+        return lines, err
     finally:
         if agg.poll() is None:
             agg.kill()
+
+
+def _assert_late_copies_counted(lines, parts=3):
+    """Owner K sends its previous round's receipt of every bucket twice per round (once before and once after
+    the current one).  Both copies of every bucket are dropped, none absorbed: the counts are exact.  K sends
+    in order and the aggregator takes receipts in accept order, so by the end of round r every copy of
+    rounds < r and all of round r's but (at most) the after-copy of its last bucket have been seen; that one
+    lands in the next round's phase 1 (an other-phase byte copy, also counted) or after the last round."""
+    assert lines[0]["stale_dropped"] == 0  # round 0 has no earlier round to be late from
+    for r, l in enumerate(lines[1:], start=1):
+        assert 2 * parts * r - 1 <= l["stale_dropped"] <= 2 * parts * r, (r, l)
+        assert l["replaced"] == 0 and l["ignored"] == 0, l  # no copy replaced a slot or was taken for a resend
+
+
+@pytest.mark.parametrize("extra", [[], ["--eager"], ["--mode", "literal"]])
+def test_late_duplicates_of_earlier_rounds_are_dropped(torch_gpu, extra):
+    """Owner 2 re-sends its previous round's receipts during the next round, once before and once after the
+    current ones (fake_owners --retransmit-late).  The wire has no round number; a late copy is a byte copy
+    of a frame already reduced, t_start included (stamped when the owner sent it, network_layer.cpp:761), so
+    fa_aggregator drops it by its (t_start, length, content) key: it neither counts as the owner's receipt nor
+    replaces the newer one, every reply of every round stays bit-exact against the oracle over THIS round's
+    values, and the counts are exact (aggregator.cpp:59-92 would reduce the stale parameters without a word)."""
+    lines, err = _run_late_copies(extra, ["--retransmit-late", "2"])
+    assert "stale part" in err, err[-2000:]
+    _assert_late_copies_counted(lines)
+    assert all(l["clock_back"] == 0 for l in lines)
+
+
+@pytest.mark.parametrize("extra", [[], ["--eager"], ["--mode", "literal"]])
+def test_owner_clock_going_back_does_not_stall(torch_gpu, extra):
+    """Owner 1's clock steps back 10 minutes every round (fake_owners --clock-skew 1,600000: an NTP step, a VM
+    resume), so each round its genuine receipts are stamped before its receipts of the previous round.  The
+    ledger drops only byte copies of reduced receipts, so they are accepted (the log names the clock), the
+    rounds complete and every reply is bit-exact.  The same owner also re-sends its previous round's receipts
+    late (--retransmit-late 1): those copies now carry stamps NEWER than the current receipts, and are still
+    dropped, every one."""
+    lines, err = _run_late_copies(extra, ["--clock-skew", "1,600000", "--retransmit-late", "1"])
+    assert "clock went back" in err, err[-2000:]
+    for r, l in enumerate(lines):
+        assert l["clock_back"] == r, (r, l)  # its part 1 of every later round (phase 2 follows its own part 1)
+    _assert_late_copies_counted(lines)
 
 
 @pytest.mark.parametrize("extra", [[], ["--eager"], ["--mode", "literal"], ["--layout", "rs", "--rs-chunks", "3"]])

@@ -849,6 +849,70 @@ def test_destroyed_context_releases_its_counter_slot(fa, torch_gpu):
     assert r["fresh_stream_owns"]
 
 
+_CALLER_STREAM_CHILD = r"""
+import ctypes, gc, json, sys
+import numpy as np
+import torch
+sys.path.insert(0, %(tests)r)
+sys.path.insert(0, %(oracle)r)
+from conftest import load_pkg
+import oracle as O
+fa = load_pkg()
+fa.lib()
+n, D = 4 << 20, 16  # below one phase with 16 clients: one sized phase of the phased kernel
+assert fa.plan_chain(fa.F32, fa.F32, n, D)[0] == fa.PLAN_PHASED
+w = O.weights(D)
+clients = []
+for k in range(D):
+    t = torch.empty(n, dtype=torch.float32, device="cuda")
+    fa.fill_uniform(t, n, fa.F32, 0x5EED, k)
+    clients.append(t)
+out = torch.empty(n, dtype=torch.float32, device="cuda")
+hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime torch already loaded
+idx = np.unique(np.concatenate([[0, n - 1], np.random.default_rng(3).integers(0, n, 512)]))
+want = O.sampled_chain(0x5EED, w, idx)[0].view(np.uint32)
+base = fa.phased_owned_slots(0)
+owned, exact, during, after = [], [], [], []
+for i in range(60):  # more caller streams than owned slots, one after another
+    p = ctypes.c_void_p()
+    assert hip.hipStreamCreateWithFlags(ctypes.byref(p), 1) == 0
+    out.zero_()
+    torch.cuda.synchronize()
+    fa.reduce_device(clients, w, n, fa.F32, out, fa.F32, stream=p.value)  # its first phased launch takes a slot
+    assert hip.hipStreamSynchronize(p) == 0
+    owned.append(fa.phased_slot(p.value)[1])
+    during.append(fa.phased_owned_slots(0) - base)
+    exact.append(bool(np.array_equal(out.cpu().numpy()[idx].view(np.uint32), want)))
+    fa.release_stream(p.value, 0)
+    after.append(fa.phased_owned_slots(0) - base)
+    assert hip.hipStreamDestroy(p) == 0
+# torch stream objects are released when collected (the binding tracks what it was handed)
+for i in range(60):
+    st = torch.cuda.Stream()
+    fa.reduce_device(clients, w, n, fa.F32, out, fa.F32, stream=st)
+    st.synchronize()
+    during.append(fa.phased_owned_slots(0) - base)
+    del st
+    gc.collect()
+    after.append(fa.phased_owned_slots(0) - base)
+print(json.dumps({"owned": owned, "exact": exact, "during": during, "after": after,
+                  "bad_device": fa.lib().fa_release_stream(999, None)}))
+"""
+
+
+def test_caller_streams_release_their_counter_slots(fa, torch_gpu):
+    """fa_release_stream: 60 raw caller streams one after another, each launching one phased reduction (its
+    first launch takes an owned counter slot) and releasing it before hipStreamDestroy -- every one of them gets
+    an owned slot (48 would be the limit without the release) and a bit-exact result against the oracle; then
+    60 torch.cuda.Stream objects, whose slots the binding gives back when they are collected."""
+    r = _child(_CALLER_STREAM_CHILD)
+    assert all(r["owned"]) and len(r["owned"]) == 60, r["owned"]
+    assert all(r["exact"]), r["exact"]
+    assert all(d == 1 for d in r["during"]), r["during"]
+    assert all(a == 0 for a in r["after"]), r["after"]
+    assert r["bad_device"] == fa.ERR_ARG
+
+
 _TIMELINE_CHILD = r"""
 import ctypes, json, sys
 import numpy as np

@@ -9,9 +9,11 @@
 //   fa_fake_owners --blobs DIR --parts 1,2,3 -d D -c C [--rounds R] [--mode fedavg|literal]
 //                  [--port-base P] [--model-name N --model-type T --start S --end E] [--seed X]
 //                  [--drop-owner K [--drop-phase P]] [--retransmit K] [--retransmit-late K]
-//                  [--reply-timeout S] [--rel-tol X]
+//                  [--clock-skew K,S] [--reply-timeout S] [--rel-tol X]
 //                  [--sequential]   (owners send at once, one connection each, unless --sequential
 //                                    or --mode literal, whose result depends on the arrival order)
+// Every frame is stamped (t_start, network_layer.cpp:761) when it first goes out, on its owner's clock;
+// --clock-skew K,S sets owner K's clock back S ms more every round (an NTP step, a VM resume).
 // Prints one JSON line: {"ok": bool, "rounds": R, "checked_elems": ..., "round_ms": [...]}.
 #include <unistd.h>
 
@@ -52,6 +54,25 @@ long now_ms() {
         .count();
 }
 
+// Overwrites the t_start field of a length-prefixed OPERATION frame in place (the frame was built with a
+// 13-digit placeholder, so a millisecond epoch stamp has the same width).
+bool restamp(Bytes& f, long t) {
+    static const char kField[] = "\nt_start : ";
+    const size_t scan = std::min<size_t>(f.size(), 512);
+    const char* b = f.data();
+    const char* at = std::search(b, b + scan, kField, kField + sizeof kField - 1);
+    if (at == b + scan) return false;
+    char* d = f.data() + (at - b) + (sizeof kField - 1);
+    size_t w = 0;
+    while (d + w < b + scan && d[w] != ',') ++w;
+    const std::string v = std::to_string(t);
+    if (v.size() != w) return false;
+    std::memcpy(d, v.data(), w);
+    return true;
+}
+
+constexpr long kStampPlaceholder = 1000000000000L;
+
 struct Part {
     int mp;
     std::string blob;
@@ -71,6 +92,8 @@ int main(int argc, char** argv) {
     int drop_owner = -1, drop_phase = 1;  // failure injection: owner K never sends its phase-P receipts
     int retransmit = -1;                  // owner K sends every receipt twice (a retransmission)
     int retransmit_late = -1;             // owner K re-sends its previous round's receipts during this round
+    int skew_owner = -1;                  // --clock-skew K,S: owner K's clock goes back S ms every round
+    long skew_ms = 0;
     double rel_tol = 0;                   // > 0: fp32 replies within rel_tol * sum_k |w_k x_k| (the rs layout)
     long reply_timeout_ms = 600000;
     for (int i = 1; i < argc; ++i) {
@@ -95,6 +118,14 @@ int main(int argc, char** argv) {
         else if (a == "--retransmit") retransmit = std::atoi(v), ++i;
         else if (a == "--retransmit-late") retransmit_late = std::atoi(v), ++i;
         else if (a == "--rel-tol") rel_tol = std::atof(v), ++i;
+        else if (a == "--clock-skew") {
+            const char* c = std::strchr(v, ',');
+            if (!c) {
+                std::cerr << "--clock-skew K,S\n";
+                return 2;
+            }
+            skew_owner = std::atoi(v), skew_ms = std::atol(c + 1), ++i;
+        }
         else if (a == "--reply-timeout") reply_timeout_ms = (long)(std::atof(v) * 1000), ++i;
         else {
             std::cerr << "unknown argument " << a << "\n";
@@ -102,7 +133,7 @@ int main(int argc, char** argv) {
         }
     }
     if (mode == "literal") concurrent = false;
-    if (retransmit_late >= D || retransmit >= D || drop_owner >= D) {
+    if (retransmit_late >= D || retransmit >= D || drop_owner >= D || skew_owner >= D) {
         std::cerr << "owner index out of range (-d " << D << ")\n";
         return 2;
     }
@@ -169,9 +200,11 @@ int main(int argc, char** argv) {
     std::vector<float> w(D, 1.0f / (float)D);  // the aggregator's default weights
     bool ok = true;
     size_t checked = 0;
-    std::vector<long> round_ms;
+    std::vector<double> round_ms;
     double max_err_over_bound = 0;  // --rel-tol: the worst element against its bound
-    std::map<int, std::vector<std::shared_ptr<const Bytes>>> prev_frames;  // the previous round's, per mp
+    std::map<int, std::vector<std::shared_ptr<Bytes>>> prev_frames;  // the previous round's, per mp
+    // owner k's clock in round r (--clock-skew)
+    auto owner_now = [&](int k, int round) { return now_ms() - (k == skew_owner ? skew_ms * round : 0L); };
     auto collect = [&](int want, std::vector<Receipt>* got) {
         const long t_end = now_ms() + reply_timeout_ms;
         while ((int)got->size() < want && now_ms() < t_end) {
@@ -200,7 +233,7 @@ int main(int argc, char** argv) {
         // The data owners' side of a round (their training) is not timed: values and frames are made
         // first, then the clock runs from the first phase-1 send to the last phase-2 reply.
         std::map<int, std::vector<std::vector<uint8_t>>> values;  // mp -> per client (the parameters' own dtype)
-        std::map<int, std::vector<std::shared_ptr<const Bytes>>> frames;
+        std::map<int, std::vector<std::shared_ptr<Bytes>>> frames;
         for (auto& p : parts) {
             for (int k = 0; k < D; ++k) {
                 std::vector<uint8_t> x(p.n * (size_t)p.es);
@@ -211,7 +244,7 @@ int main(int argc, char** argv) {
                 m.prev_node = -1;
                 m.type_op = AGGREGATION;
                 m.model_part = p.mp;
-                m.t_start = now_ms();
+                m.t_start = kStampPlaceholder;  // stamped when it goes out
                 char* vals = nullptr;
                 auto f = operation_frame(m, p.ar.size(), &vals);
                 std::string err;
@@ -228,7 +261,9 @@ int main(int argc, char** argv) {
         std::vector<Receipt> replies;
         for (int phase = 1; phase <= 2 && ok; ++phase) {
             int sent = 0;
-            std::vector<std::vector<std::shared_ptr<const Bytes>>> by_owner(D);
+            // (frame, fresh): a fresh frame is stamped on its owner's clock as it goes out; a copy keeps the
+            // stamp its original went out with
+            std::vector<std::vector<std::pair<std::shared_ptr<Bytes>, bool>>> by_owner(D);
             for (int k = 0; k < D; ++k)
                 for (auto& p : parts) {
                     if ((phase == 1) != (p.mp == 1)) continue;
@@ -237,32 +272,39 @@ int main(int argc, char** argv) {
                     // and once after this round's (a delayed duplicate; the aggregator must drop both copies,
                     // whichever order they land in)
                     const bool late = k == retransmit_late && prev_frames.count(p.mp);
-                    if (late) by_owner[k].push_back(prev_frames[p.mp][k]);
-                    by_owner[k].push_back(frames[p.mp][k]);
-                    if (k == retransmit) by_owner[k].push_back(frames[p.mp][k]);  // the same receipt again
-                    if (late) by_owner[k].push_back(prev_frames[p.mp][k]);
+                    if (late) by_owner[k].push_back({prev_frames[p.mp][k], false});
+                    by_owner[k].push_back({frames[p.mp][k], true});
+                    if (k == retransmit) by_owner[k].push_back({frames[p.mp][k], false});  // the same receipt again
+                    if (late) by_owner[k].push_back({prev_frames[p.mp][k], false});
                     ++sent;  // one reply per bucket and destination, retransmission or not
                 }
+            std::atomic<bool> send_ok{true};
+            auto stamp = [&](int k, std::pair<std::shared_ptr<Bytes>, bool>& f) {
+                if (f.second && !restamp(*f.first, owner_now(k, round))) send_ok = false;
+            };
             if (concurrent) {  // every owner is its own process in the reference: they send at once
                 std::vector<std::thread> th;
-                std::atomic<bool> send_ok{true};
                 for (int k = 0; k < D; ++k)
                     th.emplace_back([&, k] {
                         for (auto& f : by_owner[k]) {
                             const int fd = connect_to(routes.host_for(-1), routes.port_for(-1), 100, 200);
-                            if (fd < 0 || !send_all(fd, f->data(), f->size())) send_ok = false;
+                            stamp(k, f);
+                            if (fd < 0 || !send_all(fd, f.first->data(), f.first->size())) send_ok = false;
                             if (fd >= 0) close(fd);
                         }
                     });
                 for (auto& t : th) t.join();
-                if (!send_ok) {
-                    std::cerr << "send to the aggregator failed\n";
-                    ok = false;
-                    break;
-                }
             } else {  // one after another, in owner order (literal mode: the last receipt is owner D-1's)
                 for (int k = 0; k < D; ++k)
-                    for (auto& f : by_owner[k]) tx.send(-1, f);
+                    for (auto& f : by_owner[k]) {
+                        stamp(k, f);
+                        tx.send(-1, f.first);
+                    }
+            }
+            if (!send_ok) {
+                std::cerr << "send to the aggregator failed (or a frame could not be stamped)\n";
+                ok = false;
+                break;
             }
             std::vector<Receipt> got;
             if (!collect(sent, &got)) {
@@ -279,8 +321,7 @@ int main(int argc, char** argv) {
                 prev_frames[kv.first].assign(kv.second.size(), nullptr);
                 prev_frames[kv.first][retransmit_late] = kv.second[retransmit_late];
             }
-        round_ms.push_back((long)std::llround(
-            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count()));
+        round_ms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
         for (auto& r : replies) {
             const Part* p = nullptr;
             for (auto& q : parts)
@@ -344,7 +385,7 @@ int main(int argc, char** argv) {
     }
     printf("{\"ok\": %s, \"rounds\": %d, \"data_owners\": %d, \"checked_elems\": %zu, \"round_ms\": [", ok ? "true" : "false",
            rounds, D, checked);
-    for (size_t i = 0; i < round_ms.size(); ++i) printf("%s%ld", i ? ", " : "", round_ms[i]);
+    for (size_t i = 0; i < round_ms.size(); ++i) printf("%s%.3f", i ? ", " : "", round_ms[i]);
     printf("], \"max_err_over_bound\": %.6g}\n", max_err_over_bound);
     for (auto& kv : listeners) kv.second->stop();
     return ok ? 0 : 1;

@@ -2,16 +2,18 @@
 //
 // Plays the protocol of data_owner.cpp:224-253 / aggregator.cpp:55-167 with explicit t_start stamps
 // (network_layer.cpp:761: the sender stamps its clock when the frame goes out) and checks which receipts
-// the ledger calls stale: late copies of earlier rounds before and after the current receipt, copies at
-// the floor's own millisecond (decided by content), older copies within a phase, and the receipts that
-// must stay current (a frozen part resent with the same bytes in a later round, a retransmission of the
-// current receipt).  Prints one JSON line; exit code 1 if any check failed.
+// the ledger calls stale: late byte copies of earlier rounds before and after the current receipt, older
+// receipts within a phase; and the receipts that must stay current: an owner whose clock stepped back
+// between rounds (new content stamped before its previous phase -- the liveness case), a frozen part
+// resent with the same bytes under a new stamp, a retransmission of the current receipt.  Prints one JSON
+// line; exit code 1 if any check failed.
 #include <cstdio>
 #include <string>
 #include <vector>
 
 #include "receipts.h"
 
+using fahost::ReceiptKey;
 using fahost::ReceiptLedger;
 
 namespace {
@@ -26,73 +28,99 @@ void expect(bool cond, const char* what) {
     }
 }
 
-// Content of owner k's receipt of bucket mp in round r (what the fingerprint is taken over).
-uint64_t fp_of(int round, int owner, int mp) {
+// Owner k's receipt of bucket mp in round r, stamped ts (the key is what the ledger sees of it).
+ReceiptKey key_of(int round, int owner, int mp, long ts) {
     std::vector<uint8_t> blob(4096 + 13 * mp);
     for (size_t i = 0; i < blob.size(); ++i) blob[i] = (uint8_t)(i * 31 + round * 7 + owner * 3 + mp);
-    return fahost::archive_fingerprint(blob.data(), blob.size());
+    return ReceiptKey{ts, blob.size(), fahost::archive_fingerprint(blob.data(), blob.size())};
 }
 
 }  // namespace
 
 int main() {
-    const int D = 4, L = 2;  // owners 0..3, phase 2 = model parts 2..3
-    ReceiptLedger led;
-    long t = 1000;
-    std::vector<std::vector<long>> sent(3, std::vector<long>(D * (L + 2)));  // [round][owner*(L+2)+mp] = t_start
-    auto take = [&](int round, int owner, int mp, long ts) {
-        const uint64_t fp = fp_of(round, owner, mp);
-        const std::string why = led.stale(owner, mp, ts, fp);
-        if (why.empty()) led.accept(owner, mp, ts, fp);
-        return why;
-    };
-    for (int round = 0; round < 3; ++round) {
-        // phase 1: part 1 from every owner
-        for (int k = 0; k < D; ++k) sent[round][k * (L + 2) + 1] = ++t;
-        if (round > 0) {  // owner 2's part 1 of the previous round, late, BEFORE its current one
-            const std::string why = take(round - 1, 2, 1, sent[round - 1][2 * (L + 2) + 1]);
-            expect(!why.empty(), "late copy of last round's part 1 before the current one is stale");
+    // the protocol, three rounds, with owner 2's late copies and owner 1's clock stepping back 10 s a round
+    {
+        const int D = 4, L = 2;  // owners 0..3, phase 2 = model parts 2..3
+        ReceiptLedger led;
+        long t = 100000;
+        std::vector<std::vector<ReceiptKey>> sent(3, std::vector<ReceiptKey>(D * (L + 2)));
+        auto stamp = [&](int round, int k) { return ++t - (k == 1 ? 10000L * round : 0L); };
+        auto take = [&](int owner, int mp, const ReceiptKey& k) {
+            const ReceiptLedger::Verdict v = led.check(owner, mp, k);
+            if (!v.stale) led.accept(owner, mp, k);
+            return v;
+        };
+        for (int round = 0; round < 3; ++round) {
+            for (int k = 0; k < D; ++k) sent[round][k * (L + 2) + 1] = key_of(round, k, 1, stamp(round, k));
+            if (round > 0)  // owner 2's part 1 of the previous round, late, BEFORE its current one
+                expect(take(2, 1, sent[round - 1][2 * (L + 2) + 1]).stale,
+                       "late copy of last round's part 1 before the current one is stale");
+            for (int k = 0; k < D; ++k) {
+                const auto v = take(k, 1, sent[round][k * (L + 2) + 1]);
+                expect(!v.stale, "current part 1");
+                expect(v.note.empty() == !(k == 1 && round > 0), "the skewed owner's clock is noted, only it");
+            }
+            if (round > 0) {  // ... and AFTER it: neither counts nor replaces the newer receipt
+                expect(take(2, 1, sent[round - 1][2 * (L + 2) + 1]).stale,
+                       "late copy of last round's part 1 after the current one is stale");
+                expect(led.is_reduced_copy(2, 1, sent[round - 1][2 * (L + 2) + 1]), "other-phase copy is a copy");
+            }
+            // a retransmission of this round's own receipt (same stamp, same bytes) is current (it replaces)
+            expect(!take(3, 1, sent[round][3 * (L + 2) + 1]).stale, "retransmission of the current receipt");
+            expect(!led.is_reduced_copy(3, 1, sent[round][3 * (L + 2) + 1]), "not reduced before the phase ends");
+            led.end_phase();
+            expect(led.is_reduced_copy(3, 1, sent[round][3 * (L + 2) + 1]), "reduced once the phase ends");
+            t += 5;
+            for (int k = 0; k < D; ++k)
+                for (int mp = 2; mp <= L + 1; ++mp) sent[round][k * (L + 2) + mp] = key_of(round, k, mp, stamp(round, k));
+            if (round > 0) {
+                expect(take(1, 3, sent[round - 1][1 * (L + 2) + 3]).stale,
+                       "late copy of the skewed owner's last-round layer is stale (stamped after its current)");
+                expect(take(2, 2, sent[round - 1][2 * (L + 2) + 2]).stale, "late copy of last round's layer");
+            }
+            for (int k = 0; k < D; ++k)
+                for (int mp = 2; mp <= L + 1; ++mp)
+                    expect(!take(k, mp, sent[round][k * (L + 2) + mp]).stale, "current phase-2 layer");
+            led.end_phase();
+            t += 5;
         }
-        for (int k = 0; k < D; ++k) expect(take(round, k, 1, sent[round][k * (L + 2) + 1]).empty(), "current part 1");
-        if (round > 0) {  // ... and AFTER it: neither counts nor replaces the newer receipt
-            expect(!take(round - 1, 2, 1, sent[round - 1][2 * (L + 2) + 1]).empty(),
-                   "late copy of last round's part 1 after the current one is stale");
-        }
-        // a retransmission of this round's own receipt (same stamp, same bytes) is current (it replaces)
-        expect(take(round, 3, 1, sent[round][3 * (L + 2) + 1]).empty(), "retransmission of the current receipt");
-        led.end_phase();
-        // phase 2: the last-part layers, after the phase-1 reply
-        t += 5;
-        for (int k = 0; k < D; ++k)
-            for (int mp = 2; mp <= L + 1; ++mp) sent[round][k * (L + 2) + mp] = ++t;
-        if (round > 0)
-            expect(!take(round - 1, 1, 3, sent[round - 1][1 * (L + 2) + 3]).empty(),
-                   "late copy of last round's phase-2 layer is stale");
-        for (int k = 0; k < D; ++k)
-            for (int mp = 2; mp <= L + 1; ++mp)
-                expect(take(round, k, mp, sent[round][k * (L + 2) + mp]).empty(), "current phase-2 layer");
-        led.end_phase();
-        t += 5;
+        // a copy from two rounds back still matches
+        expect(led.check(2, 2, sent[0][2 * (L + 2) + 2]).stale, "a copy two rounds old is stale");
     }
-
-    // one millisecond: owner 0's part 1 of the next round stamped in the same ms as its last phase-2 send
+    // single cases
     {
         ReceiptLedger l2;
-        l2.accept(0, 1, 50, fp_of(0, 0, 1));
+        l2.accept(0, 1, key_of(0, 0, 1, 50));
         l2.end_phase();
-        l2.accept(0, 2, 60, fp_of(0, 0, 2));
+        l2.accept(0, 2, key_of(0, 0, 2, 60));
         l2.end_phase();
-        expect(!l2.stale(0, 1, 60, fp_of(0, 0, 2)).empty(), "a byte copy at the floor's millisecond is stale");
-        expect(l2.stale(0, 1, 60, fp_of(1, 0, 1)).empty(), "new content at the floor's millisecond is current");
-        expect(!l2.stale(0, 1, 59, fp_of(1, 0, 1)).empty(), "anything sent before the floor is stale");
-        // a frozen part: the same bytes as an earlier round, sent later, is current
-        expect(l2.stale(0, 1, 70, fp_of(0, 0, 1)).empty(), "same bytes sent after the floor are current");
-        // within a phase: an older copy never replaces the newer one; a newer one does
-        l2.accept(0, 1, 70, fp_of(1, 0, 1));
-        expect(!l2.stale(0, 1, 65, fp_of(9, 0, 1)).empty(), "an older receipt does not replace a newer one");
-        expect(l2.stale(0, 1, 71, fp_of(9, 0, 1)).empty(), "a newer receipt replaces");
-        // an owner never seen before has no floor
-        expect(l2.stale(7, 1, 1, 0).empty(), "an unknown owner's first receipt is current");
+        // the same millisecond as the floor: new content is current, a byte copy of a reduced one is stale
+        expect(!l2.check(0, 1, key_of(1, 0, 1, 60)).stale, "new content at the floor's millisecond is current");
+        expect(l2.check(0, 1, key_of(0, 0, 1, 50)).stale, "a byte copy is stale");
+        // the clock went back: new content before the floor is current (noted), never dropped
+        const auto back = l2.check(0, 1, key_of(1, 0, 1, 10));
+        expect(!back.stale && !back.note.empty(), "new content sent before the floor is current, with a note");
+        // a frozen part: the same bytes as an earlier round under a new stamp is current
+        expect(!l2.check(0, 1, ReceiptKey{70, key_of(0, 0, 1, 50).len, key_of(0, 0, 1, 50).fp}).stale,
+               "same bytes, new stamp: current");
+        // ... and a different bucket with the same stamp and content is not a copy of this one
+        expect(!l2.check(0, 3, key_of(0, 0, 2, 60)).stale, "copies are per bucket");
+        // within a phase: an older receipt never replaces the newer one; a newer one does
+        l2.accept(0, 1, key_of(1, 0, 1, 70));
+        expect(l2.check(0, 1, key_of(9, 0, 1, 65)).stale, "an older receipt does not replace a newer one");
+        expect(!l2.check(0, 1, key_of(9, 0, 1, 71)).stale, "a newer receipt replaces");
+        // an owner never seen before
+        expect(!l2.check(7, 1, ReceiptKey{1, 0, 0}).stale, "an unknown owner's first receipt is current");
+    }
+    // the memory is bounded: kKeep phases of a bucket
+    {
+        ReceiptLedger l3;
+        for (long r = 0; r < (long)ReceiptLedger::kKeep + 2; ++r) {
+            l3.accept(0, 1, ReceiptKey{1000 + r, 8, (uint64_t)r});
+            l3.end_phase();
+        }
+        expect(!l3.is_reduced_copy(0, 1, ReceiptKey{1000, 8, 0}), "the oldest key was forgotten");
+        expect(l3.is_reduced_copy(0, 1, ReceiptKey{1002, 8, 2}), "the last kKeep keys are kept");
     }
     // fingerprints: content and length sensitive, O(1) sampling still sees a change in every word sampled
     {
