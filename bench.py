@@ -165,12 +165,12 @@ def e2e_c1(agg_cmd, mode, port_base, rounds=C1_E2E_ROUNDS, startup_s=0.5, timeou
     owners' round times (round 0, which allocates, reported apart) and their bit-exact check of every reply."""
     golden = os.path.join(ROOT, "tests", "golden", "lenet5_c1")
     with tempfile.TemporaryDirectory(prefix="fa_c1_") as tmp:  # the reference process writes its logs in cwd
-        agg = subprocess.Popen(agg_cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, cwd=tmp,
-                               start_new_session=True)
+        agg_out = open(os.path.join(tmp, "agg.out"), "w+")
+        agg = subprocess.Popen(agg_cmd, stdout=agg_out, stderr=subprocess.DEVNULL, cwd=tmp, start_new_session=True)
         try:
             time.sleep(startup_s)
             if agg.poll() is not None:
-                raise RuntimeError("aggregator exited early: %s" % agg.stderr.read()[-300:].decode(errors="replace"))
+                raise RuntimeError("aggregator exited early (rc %s)" % agg.returncode)
             r = subprocess.run([FAKE_OWNERS, "--blobs", golden, "--parts", "1,2,3", "-d", "2", "-c", "1",
                                 "--rounds", str(rounds), "--port-base", str(port_base), "--model-name", "2",
                                 "--start", "6", "--end", "1", "--mode", mode, "--reply-timeout", "30"],
@@ -182,11 +182,28 @@ def e2e_c1(agg_cmd, mode, port_base, rounds=C1_E2E_ROUNDS, startup_s=0.5, timeou
                 except subprocess.TimeoutExpired:
                     os.killpg(agg.pid, signal.SIGKILL)  # the reference's loop never returns (aggregator.cpp:55)
                     agg.wait()
+        agg_out.seek(0)
+        phases = []  # fa_aggregator's own round lines (the reference process prints a log, no JSON)
+        for l in agg_out.read().splitlines():
+            try:
+                phases.append(json.loads(l)) if l.startswith("{") else None
+            except ValueError:
+                pass
+        agg_out.close()
     if r.returncode not in (0, 1):
         raise RuntimeError("fake owners rc %d: %s" % (r.returncode, r.stderr[-300:]))
     res = json.loads(r.stdout.strip().splitlines()[-1])
     ms = res["round_ms"][1:]
-    return {"rounds_timed": len(ms), "round_ms_median": round(statistics.median(ms), 3),
+    server = None
+    if len(phases) > 1:
+        med = lambda f: round(statistics.median(f(p) for p in phases[1:]) * 1e3, 4)  # noqa: E731
+        server = {"phase1_reduce_ms": med(lambda p: p["phase1"]["reduce_s"]),
+                  "phase2_reduce_ms": med(lambda p: p["phase2"]["reduce_s"]),
+                  "phase2_send_ms": med(lambda p: p["phase2"]["send_s"]),
+                  "absorb_ms": med(lambda p: p["phase1"]["absorb_s"] + p["phase2"]["absorb_s"]),
+                  "note": "medians over rounds 1.. of the aggregator's own round lines: reduce = the batched GPU "
+                          "reduction + D2H into the reply frame + framing, absorb = archive parse + H2D submit"}
+    return {"aggregator_view": server,"rounds_timed": len(ms), "round_ms_median": round(statistics.median(ms), 3),
             "round_ms_mean": round(statistics.mean(ms), 3),
             "round_ms_min": min(ms), "round0_ms": res["round_ms"][0], "mode": mode,
             "parity": {"check": "every element of every reply bit-exact vs the oracle (fake owners: %s)" %

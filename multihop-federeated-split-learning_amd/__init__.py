@@ -12,7 +12,6 @@ m >= 2 = parts[1].layers[m-2]), a *client slot* is one data owner's receipt.
 import ctypes
 import os
 import threading
-import weakref
 
 import numpy as np
 
@@ -141,22 +140,32 @@ def _addr(x):
 
 # Caller streams handed to the library as torch stream objects: (device, hipStream_t) -> live Python objects
 # wrapping it.  When the last one is collected the stream is retired and its phased counter slot goes back
-# (fa_release_stream); torch's pooled streams are wrapped again later, and simply take a slot anew.
+# (fa_release_stream); torch's pooled streams are wrapped again later, and simply take a slot anew.  Torch
+# stream objects take no weak references, so the tracker rides in the object's __dict__ and goes with it.
 _tracked = {}
 _tracked_mu = threading.Lock()
 
 
-def _untrack(key):
-    with _tracked_mu:
-        _tracked[key] -= 1
-        if _tracked[key]:
-            return
-        del _tracked[key]
-    try:
-        if _lib is not None:
-            _lib.fa_release_stream(key[0], key[1])
-    except Exception:  # interpreter shutdown
-        pass
+class _StreamSlot:
+    __slots__ = ("key",)
+
+    def __init__(self, key):
+        self.key = key
+        with _tracked_mu:
+            _tracked[key] = _tracked.get(key, 0) + 1
+
+    def __del__(self):
+        key = self.key
+        with _tracked_mu:
+            _tracked[key] -= 1
+            if _tracked[key]:
+                return
+            del _tracked[key]
+        try:
+            if _lib is not None:
+                _lib.fa_release_stream(key[0], key[1])
+        except Exception:  # interpreter shutdown
+            pass
 
 
 def _stream(stream):
@@ -165,16 +174,12 @@ def _stream(stream):
     if isinstance(stream, int):
         return stream
     h = stream.cuda_stream  # torch.cuda.Stream on ROCm wraps a hipStream_t
-    if h and not getattr(stream, "_fa_tracked", False):
+    if h and getattr(stream, "_fa_slot", None) is None:
         dev = stream.device.index if getattr(stream, "device", None) is not None else 0
-        key = (dev or 0, h)
         try:
-            weakref.finalize(stream, _untrack, key)
-            stream._fa_tracked = True
-        except (TypeError, AttributeError):  # an object that cannot be tracked: release_stream() by hand
-            return h
-        with _tracked_mu:
-            _tracked[key] = _tracked.get(key, 0) + 1
+            stream._fa_slot = _StreamSlot((dev or 0, h))
+        except AttributeError:  # an object without a __dict__: release_stream() by hand
+            pass
     return h
 
 

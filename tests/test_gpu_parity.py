@@ -908,8 +908,8 @@ def test_caller_streams_release_their_counter_slots(fa, torch_gpu):
     r = _child(_CALLER_STREAM_CHILD)
     assert all(r["owned"]) and len(r["owned"]) == 60, r["owned"]
     assert all(r["exact"]), r["exact"]
-    assert all(d == 1 for d in r["during"]), r["during"]
-    assert all(a == 0 for a in r["after"]), r["after"]
+    assert all(d == 1 for d in r["during"]), str(r["during"])
+    assert all(a == 0 for a in r["after"]), str(r["after"])
     assert r["bad_device"] == fa.ERR_ARG
 
 

@@ -205,13 +205,21 @@ int main(int argc, char** argv) {
     std::map<int, std::vector<std::shared_ptr<Bytes>>> prev_frames;  // the previous round's, per mp
     // owner k's clock in round r (--clock-skew)
     auto owner_now = [&](int k, int round) { return now_ms() - (k == skew_owner ? skew_ms * round : 0L); };
+    // Replies land on several listeners (one per owner port): poll them all without blocking and nap 20 us
+    // when none had anything -- a blocking wait on one listener would add its timeout to every phase (the
+    // round time of a small model is a few ms)
     auto collect = [&](int want, std::vector<Receipt>* got) {
         const long t_end = now_ms() + reply_timeout_ms;
         while ((int)got->size() < want && now_ms() < t_end) {
+            bool any = false;
             for (auto& kv : listeners) {
                 Receipt r;
-                while (kv.second->try_next_receipt(&r, 5)) got->push_back(r);
+                while (kv.second->try_next_receipt(&r, 0)) {
+                    got->push_back(r);
+                    any = true;
+                }
             }
+            if (!any) std::this_thread::sleep_for(std::chrono::microseconds(20));
         }
         return (int)got->size() == want;
     };
