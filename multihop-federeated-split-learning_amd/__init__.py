@@ -98,6 +98,7 @@ def lib():
         "fa_diag_pieces": (I, [S, I, I, ctypes.POINTER(I), ctypes.POINTER(S)]),
         "fa_diag_phased_slot": (I, [I, P, ctypes.POINTER(I)]),
         "fa_diag_phased_owned": (I, [I]),
+        "fa_diag_host_reads": (ctypes.c_longlong, [P]),
         "fa_set_tuning": (I, [ctypes.POINTER(_Tuning)]),
         "fa_get_tuning": (I, [ctypes.POINTER(_Tuning)]),
     }
@@ -502,6 +503,11 @@ class Aggregator:
 
     def sync(self):
         check(lib().fa_sync(self.handle))
+
+    def host_reads(self):
+        """fa_diag_host_reads (diagnostic): reductions of this context that read their receipts where they
+        arrived (small pinned receipts of a one-GPU range part)."""
+        return lib().fa_diag_host_reads(self.handle)
 
     def close(self):
         if self.handle:

@@ -117,6 +117,12 @@ constexpr size_t kStageBytes = 32u << 20;  // pinned staging chunk per buffer
 constexpr size_t kShardUnit = 64;          // range shards / rs pieces: multiples of 64 elements (16-B phase kept)
 constexpr int kMaxSegments = 256;          // buckets per batched launch
 constexpr int kSegRing = 4;                // device segment tables per GPU (GpuRes::seg)
+// Small receipts read in place (host_keep / host_reduce): a one-GPU range part whose D receipts total at most
+// kHostReadMax bytes, in pinned memory, is reduced by kernels that read the receipts' segments over PCIe,
+// in at most kHostReadPieces launches (the pieces on which every receipt and the destination are contiguous)
+constexpr size_t kHostReadMax = FA_HOST_READ_MAX_BYTES;
+constexpr int kHostReadPieces = 16;
+constexpr int kNotHostReadable = 1;  // host_reduce: the path does not apply (nothing was launched)
 
 // Host memcpy into / out of the pinned staging chunks, split over worker threads:
 // one thread copies ~8-10 GB/s, a PCIe Gen5 x16 link takes ~50 GB/s.  One pool per GPU, so the GPUs of a
@@ -287,6 +293,15 @@ struct Part {
     bool ready = false; // this round's output is reduced already (eager prefix reached D, fa_reduce_parts)
     std::vector<std::vector<Run>> runs;  // per GPU: where its output goes (set by the last reduction)
     std::vector<void*> run_src;          // per GPU: the buffer the runs read
+    // Small receipts kept where they arrived (host_keep): per slot the receipt's pinned segments -- the host
+    // address (for a later DMA, host_flush) and the address a kernel reads it at -- empty = in the slot.
+    struct HostSeg {
+        const char* host;
+        const char* dev;
+        size_t bytes;
+    };
+    std::vector<std::vector<HostSeg>> host_src;
+    int n_host = 0;  // slots whose receipt is kept host-side this round
 };
 
 }  // namespace
@@ -299,6 +314,7 @@ struct fa_ctx {
     std::vector<GpuRes> gpu;
     std::map<int, Part> parts;
     std::unique_ptr<CopyPool> workers;  // G > 1: one persistent host thread per GPU (for_each_gpu)
+    unsigned long long host_reads = 0;  // reductions that read their receipts in place (fa_diag_host_reads)
 };
 
 namespace {
@@ -649,12 +665,207 @@ int emulated_reduce_scatter(fa_ctx* ctx, Part& p, size_t a, size_t q, size_t off
     return FA_OK;
 }
 
+// A host buffer given as the concatenation of `n` segments (one segment for a flat buffer, one per
+// parameter record for an archive mapped in place): the source of a receipt or the destination of a
+// reduced bucket.
+struct Gather {
+    int n;
+    const void* const* seg;
+    const size_t* bytes;
+    // fn(piece, rel, take) for each piece of bytes [a, a + len) of the concatenation; rel = offset of
+    // the piece from a.
+    template <class F>
+    void pieces(size_t a, size_t len, F&& fn) const {
+        size_t seg_lo = 0, rel = 0;
+        for (int k = 0; k < n && len > 0; ++k) {
+            const size_t seg_hi = seg_lo + bytes[k];
+            if (a < seg_hi) {
+                const size_t off = a - seg_lo, take = std::min(len, seg_hi - a);
+                fn(const_cast<char*>(static_cast<const char*>(seg[k])) + off, rel, take);
+                a += take;
+                rel += take;
+                len -= take;
+            }
+            seg_lo = seg_hi;
+        }
+    }
+    void copy_out(size_t a, size_t len, char* dst) const {  // concatenation[a, a+len) -> dst
+        pieces(a, len, [&](char* p, size_t rel, size_t take) { std::memcpy(dst + rel, p, take); });
+    }
+    void copy_in(size_t a, size_t len, const char* src) const {  // src -> concatenation[a, a+len)
+        pieces(a, len, [&](char* p, size_t rel, size_t take) { std::memcpy(p, src + rel, take); });
+    }
+    size_t total() const {
+        size_t t = 0;
+        for (int k = 0; k < n; ++k) t += bytes[k];
+        return t;
+    }
+    int check(const char* what) const {
+        if (n < 0 || (n > 0 && (!seg || !bytes))) return fail(FA_ERR_ARG, "bad %s segment list", what);
+        for (int k = 0; k < n; ++k)
+            if (!seg[k] && bytes[k]) return fail(FA_ERR_ARG, "%s segment %d is null", what, k);
+        return FA_OK;
+    }
+};
+
+// ------------------------------------------------------------------ small receipts read in place
+//
+// A small model's round is bound by stream round trips, not bytes: BASELINE C1 (LeNet-5, two owners) spent
+// ~0.23 ms per round inside this library for 31 us of kernels (profiles/r05_c1_trace.json) -- an H2D copy per
+// receipt segment, the reduction, a D2H copy, each a queue hop.  So a pinned receipt of a one-GPU range part
+// whose D receipts total at most kHostReadMax bytes stays where it arrived (host_keep): its segments'
+// device-visible addresses are noted and the reduction's kernels read them over PCIe -- into the output, or
+// at fa_finalize_gather(FA_HOST_PINNED) straight into the reply's pinned records (host_reduce), one launch per
+// piece and one synchronization.  Same kernels, same chain, same bits.  Whatever else needs the slots first
+// copies the kept receipts in (host_flush), so every other path sees exactly what the plain submit gives.
+// FA_HOST_READ=0 turns it off (experiments).
+
+bool host_read_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("FA_HOST_READ");
+        return !e || std::atoi(e) != 0;
+    }();
+    return on;
+}
+
+// The address a kernel on the current device reads pinned host memory at, or null.
+const char* device_visible(const void* ptr) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, ptr) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (a.type != hipMemoryTypeHost || !a.devicePointer || !a.hostPointer) return nullptr;
+    return static_cast<const char*>(a.devicePointer) + (static_cast<const char*>(ptr) - static_cast<const char*>(a.hostPointer));
+}
+
+bool host_read_part(const fa_ctx* ctx, const Part& p) {
+    return host_read_enabled() && ctx->G == 1 && !p.rs && !(ctx->flags & FA_ACCUMULATE_ON_ARRIVAL) &&
+           p.npiece[0] == 1 && p.n > 0 && (size_t)p.D * p.n * dsize(p.in) <= kHostReadMax;
+}
+
+// Keeps a pinned receipt of slot `slot` where it is, if the part and every segment allow it (element-aligned,
+// device-visible); false = submit it the plain way.
+bool host_keep(fa_ctx* ctx, Part& p, int slot, const Gather& src) {
+    if (!host_read_part(ctx, p) || src.n > 4 * kHostReadPieces) return false;
+    const size_t si = dsize(p.in);
+    std::vector<Part::HostSeg> segs;
+    DeviceGuard dg(ctx->gpu[0].dev);
+    for (int k = 0; k < src.n; ++k) {
+        if (!src.bytes[k]) continue;
+        const char* h = static_cast<const char*>(src.seg[k]);
+        if ((uintptr_t)h % si || src.bytes[k] % si) return false;
+        const char* d = device_visible(h);
+        if (!d || (uintptr_t)d % si) return false;
+        segs.push_back({h, d, src.bytes[k]});
+    }
+    auto& slot_src = p.host_src[(size_t)slot];
+    if (slot_src.empty()) ++p.n_host;
+    slot_src = std::move(segs);
+    return true;
+}
+
+// Copies every kept receipt into its slot (what the plain pinned submit would have done) and forgets them.
+int host_flush(fa_ctx* ctx, Part& p) {
+    if (p.n_host == 0) return FA_OK;
+    GpuRes& r = ctx->gpu[0];
+    DeviceGuard dg(r.dev);
+    for (int k = 0; k < p.D; ++k) {
+        auto& segs = p.host_src[(size_t)k];
+        size_t o = 0;
+        for (auto& sg : segs) {
+            FA_HIP(hipMemcpyAsync(slot_ptr(p, 0, k) + o, sg.host, sg.bytes, hipMemcpyHostToDevice, r.copy));
+            o += sg.bytes;
+        }
+        segs.clear();
+    }
+    ++r.copy_gen;
+    p.n_host = 0;
+    return FA_OK;
+}
+
+// Every receipt the reduction reads is kept host-side (FedAvg: all D; literal: the last one).
+bool host_read_all(const Part& p) {
+    if (p.n_host == 0) return false;
+    if (p.mode == FA_LITERAL) {
+        const int k = p.last_slot >= 0 ? p.last_slot : p.D - 1;
+        return !p.host_src[(size_t)k].empty();
+    }
+    return p.n_host == p.D;
+}
+
+// The reduction over the kept receipts: into the part's output (dst null; the copy-out follows as usual) or
+// straight into the pinned destination segments, synchronized.  kNotHostReadable (nothing launched) when the
+// destination is not device-visible or element-aligned, or the pieces would be more than kHostReadPieces.
+int host_reduce(fa_ctx* ctx, Part& p, const float* w, hipStream_t s, const Gather* dst) {
+    const size_t si = dsize(p.in), so = dsize(p.out);
+    std::vector<int> ks;  // the slots the chain reads, in order
+    if (p.mode == FA_LITERAL) ks.push_back(p.last_slot >= 0 ? p.last_slot : p.D - 1);
+    else for (int k = 0; k < p.D; ++k) ks.push_back(k);
+    GpuRes& r = ctx->gpu[0];
+    DeviceGuard dg(r.dev);
+    std::vector<size_t> cuts{0, p.n};
+    for (int k : ks) {
+        size_t e = 0;
+        for (auto& sg : p.host_src[(size_t)k]) cuts.push_back(e += sg.bytes / si);
+    }
+    std::vector<Part::HostSeg> out;
+    if (dst) {
+        size_t e = 0;
+        for (int j = 0; j < dst->n; ++j) {
+            if (!dst->bytes[j]) continue;
+            const char* h = static_cast<const char*>(dst->seg[j]);
+            const char* d = device_visible(h);
+            if (!d || (uintptr_t)h % so || (uintptr_t)d % so || dst->bytes[j] % so) return kNotHostReadable;
+            out.push_back({h, d, dst->bytes[j]});
+            cuts.push_back(e += dst->bytes[j] / so);
+        }
+    }
+    std::sort(cuts.begin(), cuts.end());
+    cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
+    while (!cuts.empty() && cuts.back() > p.n) cuts.pop_back();
+    if (cuts.size() - 1 > (size_t)kHostReadPieces) return kNotHostReadable;
+    // element e of a segment list (si bytes per element) -> its device-visible address
+    auto at = [](const std::vector<Part::HostSeg>& segs, size_t e, size_t es) -> const char* {
+        size_t b = e * es;
+        for (auto& sg : segs) {
+            if (b < sg.bytes) return sg.dev + b;
+            b -= sg.bytes;
+        }
+        return nullptr;
+    };
+    hipStream_t st = s ? s : r.compute;
+    std::vector<const void*> ptrs(ks.size());
+    for (size_t c = 0; c + 1 < cuts.size(); ++c) {
+        const size_t a = cuts[c], len = cuts[c + 1] - a;
+        for (size_t i = 0; i < ks.size(); ++i) ptrs[i] = at(p.host_src[(size_t)ks[i]], a, si);
+        void* o = dst ? const_cast<char*>(at(out, a, so)) : static_cast<char*>(p.dout[0]) + a * so;
+        int rc = reduce_on(ctx, 0, ctx->tuning.tu, ptrs.data(), w, (int)ks.size(), len, p.in, o, p.out, p.mode,
+                           p.divisor, nullptr, st);
+        if (rc) return rc;
+    }
+    ++ctx->host_reads;
+    if (dst) {
+        FA_HIP(hipStreamSynchronize(st));
+        return FA_OK;
+    }
+    int rc = mark_done(ctx, p, 0, st);
+    if (rc) return rc;
+    set_range_runs(p, 1);
+    return FA_OK;
+}
+
 // Enqueue the full reduction of part p on every GPU (the ctx's streams, or `s` for a one-GPU ctx):
 // range -> each GPU's shard; rs -> the clients' fp32 partials, piece by piece, each piece's RCCL
 // reduce-scatter (ring over xGMI) overlapping the reduction of the next.
 int reduce_part(fa_ctx* ctx, Part& p, const float* w, hipStream_t s) {
     Trace tr(p.rs ? "fa_reduce rs D %d" : "fa_reduce D %d", p.D);
     const int G = ctx->G;
+    if (p.n_host > 0) {  // small receipts kept where they arrived: read them there, or copy them in first
+        if (host_read_all(p)) return host_reduce(ctx, p, w, s, nullptr);
+        int rc = host_flush(ctx, p);
+        if (rc) return rc;
+    }
     if (!p.rs) {
         for (int g = 0; g < G; ++g) {
             GpuRes& r = ctx->gpu[(size_t)g];
@@ -768,48 +979,6 @@ int reduce_part(fa_ctx* ctx, Part& p, const float* w, hipStream_t s) {
     return FA_OK;
 }
 
-// A host buffer given as the concatenation of `n` segments (one segment for a flat buffer, one per
-// parameter record for an archive mapped in place): the source of a receipt or the destination of a
-// reduced bucket.
-struct Gather {
-    int n;
-    const void* const* seg;
-    const size_t* bytes;
-    // fn(piece, rel, take) for each piece of bytes [a, a + len) of the concatenation; rel = offset of
-    // the piece from a.
-    template <class F>
-    void pieces(size_t a, size_t len, F&& fn) const {
-        size_t seg_lo = 0, rel = 0;
-        for (int k = 0; k < n && len > 0; ++k) {
-            const size_t seg_hi = seg_lo + bytes[k];
-            if (a < seg_hi) {
-                const size_t off = a - seg_lo, take = std::min(len, seg_hi - a);
-                fn(const_cast<char*>(static_cast<const char*>(seg[k])) + off, rel, take);
-                a += take;
-                rel += take;
-                len -= take;
-            }
-            seg_lo = seg_hi;
-        }
-    }
-    void copy_out(size_t a, size_t len, char* dst) const {  // concatenation[a, a+len) -> dst
-        pieces(a, len, [&](char* p, size_t rel, size_t take) { std::memcpy(dst + rel, p, take); });
-    }
-    void copy_in(size_t a, size_t len, const char* src) const {  // src -> concatenation[a, a+len)
-        pieces(a, len, [&](char* p, size_t rel, size_t take) { std::memcpy(p, src + rel, take); });
-    }
-    size_t total() const {
-        size_t t = 0;
-        for (int k = 0; k < n; ++k) t += bytes[k];
-        return t;
-    }
-    int check(const char* what) const {
-        if (n < 0 || (n > 0 && (!seg || !bytes))) return fail(FA_ERR_ARG, "bad %s segment list", what);
-        for (int k = 0; k < n; ++k)
-            if (!seg[k] && bytes[k]) return fail(FA_ERR_ARG, "%s segment %d is null", what, k);
-        return FA_OK;
-    }
-};
 
 // Accumulate on arrival: extend the chain over the in-order prefix of submitted slots.  Slots
 // [p.reduced, j) are all submitted: one launch continues the fp32 accumulator over them (or, when j == D,
@@ -845,7 +1014,9 @@ int submit_impl(fa_ctx* ctx, int part_id, int slot, const Gather& src, float wei
     const size_t si = dsize(p->in), total = src.total();
     if (total != p->n * si)
         return fail(FA_ERR_ARG, "part %d expects %zu bytes per receipt, got %zu", part_id, p->n * si, total);
-    rc = for_each_gpu(ctx->workers.get(), ctx->G, [&](int g) -> int {
+    const bool kept = pinned && host_keep(ctx, *p, slot, src);  // a small receipt stays where it arrived
+    if (!kept && (rc = host_flush(ctx, *p))) return rc;         // else the kept ones go to their slots first
+    if (!kept) rc = for_each_gpu(ctx->workers.get(), ctx->G, [&](int g) -> int {
         if (!holds(*p, g, slot)) return FA_OK;  // rs: only the slot's GPU receives it
         GpuRes& r = ctx->gpu[(size_t)g];
         DeviceGuard dg(r.dev);
@@ -979,6 +1150,8 @@ int copy_output(fa_ctx* ctx, Part& p, const Gather& dst, bool pinned) {
 }
 
 void reset_round(Part& p) {
+    for (auto& h : p.host_src) h.clear();
+    p.n_host = 0;
     std::fill(p.submitted.begin(), p.submitted.end(), 0);
     p.n_submitted = 0;
     p.last_slot = -1;
@@ -997,6 +1170,17 @@ int finalize_impl(fa_ctx* ctx, int part_id, const Gather& dst, bool pinned) {
         return fail(FA_ERR_STATE, "part %d: %d of %d clients submitted", part_id, p->n_submitted, p->D);
     if (p->n_submitted == 0) return fail(FA_ERR_STATE, "part %d: nothing submitted", part_id);
     if ((rc = dst.check("host destination"))) return rc;
+    if (dst.total() != p->n * dsize(p->out))
+        return fail(FA_ERR_ARG, "output of %zu bytes expected, destination holds %zu", p->n * dsize(p->out),
+                    dst.total());
+    if (!p->ready && p->reduced == 0 && pinned && host_read_all(*p)) {  // kept receipts -> the pinned reply
+        rc = host_reduce(ctx, *p, p->w.data(), nullptr, &dst);
+        if (rc != kNotHostReadable) {
+            if (rc) return rc;
+            reset_round(*p);
+            return FA_OK;
+        }
+    }
     if (!p->ready) {
         if (p->reduced > 0) {  // accumulate on arrival: finish the chain after the reduced prefix
             for (int g = 0; g < ctx->G; ++g) {
@@ -1036,7 +1220,7 @@ int reduce_parts_impl(fa_ctx* ctx, int n_parts, const int* ids, const float* con
     std::vector<int> single;
     for (int i = 0; i < n_parts; ++i) {
         Part& p = *ps[(size_t)i];
-        bool batch = !p.rs && p.mode == FA_FEDAVG && p.D <= fa::kMaxClients;
+        bool batch = !p.rs && p.mode == FA_FEDAVG && p.D <= fa::kMaxClients && p.n_host == 0;
         for (int g = 0; batch && g < ctx->G; ++g) {
             DeviceGuard dg(ctx->gpu[(size_t)g].dev);
             batch = p.npiece[(size_t)g] == 1 &&
@@ -1404,6 +1588,7 @@ int fa_bucket_define(fa_ctx* ctx, int part_id, size_t n_elems, fa_dtype in, fa_d
     p.rs = rs;
     p.w.assign((size_t)n_clients, 0.0f);
     p.submitted.assign((size_t)n_clients, 0);
+    p.host_src.assign((size_t)n_clients, {});
     const size_t G = (size_t)ctx->G;
     const bool eager = (ctx->flags & FA_ACCUMULATE_ON_ARRIVAL) && !rs && mode == FA_FEDAVG;
     if (rs) {
@@ -1601,6 +1786,7 @@ int fa_bucket_slot(fa_ctx* ctx, int part_id, int gpu, int client_slot, void** d_
     if (p->npiece[(size_t)gpu] > 1)
         return fail(FA_ERR_STATE, "part %d is held as %d pieces on GPU %d: use fa_bucket_piece", part_id,
                     p->npiece[(size_t)gpu], gpu);
+    if ((rc = host_flush(ctx, *p))) return rc;  // the caller may read the slot: the kept receipts land first
     if (d_ptr) *d_ptr = slot_ptr(*p, gpu, client_slot);
     if (n_elems) *n_elems = p->cnt[(size_t)gpu];
     if (elem_offset) *elem_offset = p->off[(size_t)gpu];
@@ -1630,6 +1816,7 @@ int fa_bucket_piece(fa_ctx* ctx, int part_id, int gpu, int piece, int client_slo
     if (!holds(*p, gpu, client_slot))
         return fail(FA_ERR_ARG, "client slot %d is not held by GPU %d (rs layout: slots [%d,%d))", client_slot, gpu,
                     p->c0[(size_t)gpu], p->c1[(size_t)gpu]);
+    if ((rc = host_flush(ctx, *p))) return rc;
     if (d_ptr) *d_ptr = piece_ptr(*p, gpu, client_slot, piece);
     if (n_elems) *n_elems = piece_cnt(*p, gpu, piece);
     if (elem_offset) *elem_offset = p->off[(size_t)gpu] + piece_lo(*p, gpu, piece);
@@ -1734,6 +1921,7 @@ int fa_sync_part(fa_ctx* ctx, int part_id, const float* h_weights, void* hip_str
     if (p->rs) return fail(FA_ERR_ARG, "part %d: state sync needs every client on every GPU (range layout)", part_id);
     if (hip_stream && ctx->G != 1) return fail(FA_ERR_ARG, "an explicit stream needs a single-GPU ctx");
     const float* w = h_weights ? h_weights : p->w.data();
+    if ((rc = host_flush(ctx, *p))) return rc;  // the sync works on the slots
     std::vector<void*> ptrs((size_t)p->D);
     for (int g = 0; g < ctx->G; ++g) {
         GpuRes& r = ctx->gpu[(size_t)g];
@@ -1817,6 +2005,10 @@ extern "C" int fa_diag_read_plain(const void* const* d_bufs, int nc, size_t n, i
     FA_HIP(fa::launch_read_plain(t, nc, (int64_t)(n / 4), grid, unroll, sink, static_cast<hipStream_t>(hip_stream)));
     return FA_OK;
 }
+
+// Diagnostic, not part of the ABI in fa.h: how many reductions of this context read their receipts in place
+// (small pinned receipts, host_reduce); -1 for a null context.
+extern "C" long long fa_diag_host_reads(fa_ctx* ctx) { return ctx ? (long long)ctx->host_reads : -1; }
 
 // Diagnostic, not part of the ABI in fa.h: the per-workgroup timeline of the last phased launch on `device`
 // when the process runs with FA_TIMELINE=1 (tools/timeline.py).

@@ -361,6 +361,14 @@ public:
     // copy each result into its reply.  With --eager the chains already ran as the receipts arrived.
     void reduce_all(const std::vector<int>& mps) {
         if (o_.eager || mps.size() < 2) return;
+        // small parts whose receipts the library reads in place (FA_HOST_READ_MAX_BYTES): each finalize then
+        // reduces straight into its reply, one round trip per part instead of a launch here and a copy there
+        if (o_.gpus == 1 && !o_.rs && o_.pinned &&
+            std::all_of(mps.begin(), mps.end(), [&](int mp) {
+                const Bucket& b = buckets_[mp];
+                return (size_t)o_.data_owners * b.numel * (size_t)b.elem <= FA_HOST_READ_MAX_BYTES;
+            }))
+            return;
         const auto t0 = std::chrono::steady_clock::now();
         FA_CHECK(fa_reduce_parts(ctx_, (int)mps.size(), mps.data(), nullptr, nullptr));
         st_.finalize_s += secs_since(t0);
@@ -455,14 +463,17 @@ int main(int argc, char** argv) {
         usage();
         return 2;
     }
-    std::shared_ptr<BufferPool> pool;  // pinned frame buffers: receipts DMA'd from, replies DMA'd into
+    // pinned frame buffers: receipts DMA'd from, replies DMA'd into -- small ones too (from 4 KiB): a small
+    // model's receipt then goes to its slot by one DMA instead of a copy into the staging chunks first, and
+    // its reply comes back the same way (BASELINE C1)
+    std::shared_ptr<BufferPool> pool;
     if (o.pinned) {
         pool = BufferPool::create(
             [](size_t n) -> char* {
                 void* p = nullptr;
                 return fa_host_alloc(n, &p) == FA_OK ? (char*)p : nullptr;
             },
-            [](char* p) { fa_host_free(p); }, true);
+            [](char* p) { fa_host_free(p); }, true, 4096);
         set_frame_allocator([pool](size_t n) { return pool->get(n); });
     }
     NetLayer net(o.id, RoutingTable(o.port_base), o.senders);

@@ -103,11 +103,24 @@ static bool recv_all(int fd, void* p, size_t n) {
     return true;
 }
 
+// The frame's buffer, from its first bytes (already read into `head`): sized `len`, with the archive of an
+// OPERATION frame 64-byte aligned in memory (aligned_frame_buffer), the head copied in.
+std::shared_ptr<Bytes> frame_buffer_for(const char* head, size_t have, size_t len) {
+    auto b = aligned_frame_buffer(len, values_offset(head, have));
+    std::memcpy(b->data(), head, have);
+    return b;
+}
+
+constexpr size_t kHeadBytes = 1024;  // an OPERATION header is ~150 bytes
+
 std::shared_ptr<Bytes> recv_frame(int fd) {
     int32_t len = 0;
     if (!recv_all(fd, &len, 4) || len <= 0) return nullptr;
-    auto b = new_frame_buffer((size_t)len);
-    if (!recv_all(fd, b->data(), (size_t)len)) return nullptr;
+    char head[kHeadBytes];
+    const size_t have = std::min<size_t>(kHeadBytes, (size_t)len);
+    if (!recv_all(fd, head, have)) return nullptr;
+    auto b = frame_buffer_for(head, have, (size_t)len);
+    if (!recv_all(fd, b->data() + have, (size_t)len - have)) return nullptr;
     return b;
 }
 
@@ -311,9 +324,15 @@ std::shared_ptr<Bytes> NetLayer::recv_frame_gated(int fd, uint64_t seq) {
     if (!recv_all(fd, &len, 4) || len <= 0) return nullptr;
     bool gated = gate_limit_ > 0 && (size_t)len >= kGateBytes;
     if (gated && !gate_enter(seq)) return nullptr;
-    auto b = new_frame_buffer((size_t)len);
-    char* c = reinterpret_cast<char*>(b->data());
-    size_t n = (size_t)len;
+    char head[kHeadBytes];
+    const size_t have = std::min<size_t>(kHeadBytes, (size_t)len);
+    if (!recv_all(fd, head, have)) {
+        if (gated) gate_leave();
+        return nullptr;
+    }
+    auto b = frame_buffer_for(head, have, (size_t)len);
+    char* c = reinterpret_cast<char*>(b->data()) + have;
+    size_t n = (size_t)len - have;
     auto last = std::chrono::steady_clock::now();
     while (n > 0) {
         pollfd p{fd, POLLIN, 0};

@@ -121,7 +121,13 @@ BufferPool::~BufferPool() {
 
 std::shared_ptr<Bytes> BufferPool::get(size_t n) {
     if (n < min_) return std::make_shared<Bytes>(n);
-    const size_t cls = (n + (2u << 20) - 1) / (2u << 20) * (2u << 20);
+    // 2 MiB classes from 2 MiB up; below, powers of two from 64 KiB (a small model's receipts, e.g. LeNet-5's
+    // 200 KB parts, then take 256 KiB buffers, not 2 MiB ones)
+    size_t cls = (n + (2u << 20) - 1) / (2u << 20) * (2u << 20);
+    if (n < (2u << 20)) {
+        cls = 64u << 10;
+        while (cls < n) cls <<= 1;
+    }
     char* p = nullptr;
     {
         std::lock_guard<std::mutex> g(m_);
@@ -156,10 +162,25 @@ size_t BufferPool::cached_bytes() {
     return t;
 }
 
+std::shared_ptr<Bytes> aligned_frame_buffer(size_t n, size_t lead) {
+    auto raw = new_frame_buffer(n + 64);
+    const size_t pad = (64 - ((uintptr_t)raw->data() + lead) % 64) % 64;
+    char* p = raw->data() + pad;
+    const bool pinned = raw->pinned;
+    return std::make_shared<Bytes>(p, n, pinned, [raw](char*) {});  // raw returns to its pool with the view
+}
+
+size_t values_offset(const char* text, size_t have) {
+    static const char kField[] = "\nvalues : ";
+    const char* e = text + have;
+    const char* at = std::search(text, e, kField, kField + sizeof kField - 1);
+    return at == e ? 0 : (size_t)(at - text) + sizeof kField - 1;
+}
+
 std::shared_ptr<Bytes> operation_frame(const Message& m, size_t values_len, char** values) {
     const std::string head = operation_header(m);
     const size_t text = head.size() + values_len + 3;
-    auto b = new_frame_buffer(4 + text);
+    auto b = aligned_frame_buffer(4 + text, 4 + head.size());  // the archive 64-byte aligned
     const int32_t len = (int32_t)text;
     std::memcpy(b->data(), &len, 4);  // native-endian int, as my_send does (network_layer.cpp:16)
     std::memcpy(b->data() + 4, head.data(), head.size());

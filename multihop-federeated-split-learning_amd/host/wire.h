@@ -67,10 +67,20 @@ using FrameAllocator = std::function<std::shared_ptr<Bytes>(size_t)>;
 void set_frame_allocator(FrameAllocator a);
 std::shared_ptr<Bytes> new_frame_buffer(size_t n);
 
-// A recycling pool of large frame buffers over an allocator pair (e.g. fa_host_alloc/fa_host_free
-// for pinned memory).  Buffers of at least `min_bytes` are rounded up to 2 MiB classes and return to
-// the pool when their last reference goes; a round's frames have the same sizes as the last
-// round's, so the steady state allocates nothing.  Smaller requests use the heap.
+// A frame buffer of n bytes whose byte `lead` lies on a 64-byte boundary: the torch::save archive of an
+// OPERATION frame starts there, so its tensor records (64-byte aligned within the archive) are 64-byte
+// aligned in memory and a kernel can read or write them in place (small receipts).  A view
+// into a new_frame_buffer of n + 64 bytes, which goes back to its pool with the view.
+std::shared_ptr<Bytes> aligned_frame_buffer(size_t n, size_t lead);
+// Where the archive (`values`) of an OPERATION frame's text starts, from its first `have` bytes; 0 when
+// they hold no "values : " field (a refactor frame, or a header longer than `have`).
+size_t values_offset(const char* text, size_t have);
+
+// A recycling pool of frame buffers over an allocator pair (e.g. fa_host_alloc/fa_host_free for pinned
+// memory).  Buffers of at least `min_bytes` are rounded up to a size class (2 MiB multiples from 2 MiB,
+// powers of two from 64 KiB below) and return to the pool when their last reference goes; a round's
+// frames have the same sizes as the last round's, so the steady state allocates nothing.  Smaller
+// requests use the heap.
 class BufferPool : public std::enable_shared_from_this<BufferPool> {
 public:
     using AllocFn = std::function<char*(size_t)>;
