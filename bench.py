@@ -144,6 +144,7 @@ def ports_free(ports):
     import socket
     for p in ports:
         with socket.socket() as so:
+            so.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)  # as the servers bind: TIME_WAIT is no conflict
             try:
                 so.bind(("0.0.0.0", p))
             except OSError:

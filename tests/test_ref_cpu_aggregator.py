@@ -32,6 +32,7 @@ PORTS = (8080, 8081, 8082, 8083)  # the reference's fixed routing table (network
 def ports_free():
     for p in PORTS:
         with socket.socket() as s:
+            s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)  # as the reference binds (network_layer.cpp:99)
             try:
                 s.bind(("0.0.0.0", p))
             except OSError:
