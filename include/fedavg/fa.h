@@ -105,13 +105,13 @@ int fa_submit(fa_ctx* ctx, int part_id, int client_slot, const void* host_src, f
  * caller keeps unchanged until fa_finalize returns: no staging copy.
  * Small receipts are read where they are: on a one-GPU range context without
  * FA_ACCUMULATE_ON_ARRIVAL, a part whose D receipts total at most
- * FA_HOST_READ_MAX_BYTES keeps element-aligned pinned receipts in place, and its
- * reduction's kernels read them over PCIe -- at fa_finalize_gather(FA_HOST_PINNED)
- * straight into the pinned destination, one stream round trip for the phase
- * (a small model's round is bound by round trips, not bytes).  Same bits.  Calls
- * that need the device slots (fa_bucket_slot/_piece, fa_sync_part, a pageable
- * submit to the part) copy the kept receipts in first.  FA_HOST_READ=0 in the
- * environment turns this off. */
+ * FA_HOST_READ_MAX_BYTES keeps element-aligned pinned receipts in place, and the
+ * fa_finalize* that ends the round has its kernels read them over PCIe -- with
+ * FA_HOST_PINNED straight into the pinned destination: one stream round trip for
+ * the phase (a small model's round is bound by round trips, not bytes).  Same
+ * bits.  Calls before it that need the device slots (fa_reduce_part(s),
+ * fa_sync_part, fa_bucket_slot/_piece, a pageable submit to the part) copy the
+ * kept receipts in first.  FA_HOST_READ=0 in the environment turns this off. */
 #define FA_HOST_READ_MAX_BYTES (1u << 20)
 int fa_submit_pinned(fa_ctx* ctx, int part_id, int client_slot, const void* host_src, float weight);
 

@@ -714,10 +714,12 @@ struct Gather {
 // ~0.23 ms per round inside this library for 31 us of kernels (profiles/r05_c1_trace.json) -- an H2D copy per
 // receipt segment, the reduction, a D2H copy, each a queue hop.  So a pinned receipt of a one-GPU range part
 // whose D receipts total at most kHostReadMax bytes stays where it arrived (host_keep): its segments'
-// device-visible addresses are noted and the reduction's kernels read them over PCIe -- into the output, or
-// at fa_finalize_gather(FA_HOST_PINNED) straight into the reply's pinned records (host_reduce), one launch per
-// piece and one synchronization.  Same kernels, same chain, same bits.  Whatever else needs the slots first
-// copies the kept receipts in (host_flush), so every other path sees exactly what the plain submit gives.
+// device-visible addresses are noted and the finalize that ends the round has the reduction's kernels read
+// them over PCIe -- straight into the reply's pinned records at fa_finalize_gather(FA_HOST_PINNED), else
+// into the output before the copy-out (host_reduce) -- one launch per piece and one synchronization.  Same
+// kernels, same chain, same bits.  The caller keeps pinned receipts until that finalize returns (fa.h), and
+// anything before it that needs the slots -- a reduction, a state sync, a slot address, a pageable submit --
+// first copies the kept receipts in (host_flush), so every other path sees exactly what the plain submit gives.
 // FA_HOST_READ=0 turns it off (experiments).
 
 bool host_read_enabled() {
@@ -861,11 +863,9 @@ int host_reduce(fa_ctx* ctx, Part& p, const float* w, hipStream_t s, const Gathe
 int reduce_part(fa_ctx* ctx, Part& p, const float* w, hipStream_t s) {
     Trace tr(p.rs ? "fa_reduce rs D %d" : "fa_reduce D %d", p.D);
     const int G = ctx->G;
-    if (p.n_host > 0) {  // small receipts kept where they arrived: read them there, or copy them in first
-        if (host_read_all(p)) return host_reduce(ctx, p, w, s, nullptr);
-        int rc = host_flush(ctx, p);
-        if (rc) return rc;
-    }
+    // small receipts kept where they arrived are read there only by the finalize that ends their round (the
+    // caller keeps them until then); a reduction before it takes them into the slots first
+    if (int rc = host_flush(ctx, p)) return rc;
     if (!p.rs) {
         for (int g = 0; g < G; ++g) {
             GpuRes& r = ctx->gpu[(size_t)g];
@@ -1173,9 +1173,14 @@ int finalize_impl(fa_ctx* ctx, int part_id, const Gather& dst, bool pinned) {
     if (dst.total() != p->n * dsize(p->out))
         return fail(FA_ERR_ARG, "output of %zu bytes expected, destination holds %zu", p->n * dsize(p->out),
                     dst.total());
-    if (!p->ready && p->reduced == 0 && pinned && host_read_all(*p)) {  // kept receipts -> the pinned reply
-        rc = host_reduce(ctx, *p, p->w.data(), nullptr, &dst);
-        if (rc != kNotHostReadable) {
+    if (!p->ready && p->reduced == 0 && host_read_all(*p)) {  // the kept receipts, read where they are:
+        rc = pinned ? host_reduce(ctx, *p, p->w.data(), nullptr, &dst) : kNotHostReadable;  // into the reply,
+        if (rc == kNotHostReadable) {                                                      // or the output
+            if ((rc = host_reduce(ctx, *p, p->w.data(), nullptr, nullptr)) == FA_OK) rc = copy_output(ctx, *p, dst, pinned);
+        }
+        if (rc == kNotHostReadable) {
+            rc = FA_OK;  // more pieces than kHostReadPieces: the plain path below
+        } else {
             if (rc) return rc;
             reset_round(*p);
             return FA_OK;

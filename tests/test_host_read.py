@@ -110,8 +110,9 @@ def test_literal_last_receipt_in_place(fa, O, torch_gpu):
 
 
 def test_kept_receipts_into_output_then_copy(fa, O, torch_gpu):
-    """A pageable destination, fa_reduce_parts before the finalize, fa_copy_output: the kept receipts are
-    reduced in place into the part's output, which the usual copy-out then returns."""
+    """A pageable destination: the kept receipts are reduced in place into the part's output, which the usual
+    copy-out returns.  fa_reduce_parts before the finalize (and fa_copy_output after it) take the plain path:
+    the kept receipts go to their slots first, since the caller keeps them only until the finalize."""
     D = 2
     sizes = {1: 50_536, 2: 10_164, 3: 850}
     xs = {mp: [O.gen(0x77 + mp, k, n) for k in range(D)] for mp, n in sizes.items()}
@@ -126,12 +127,13 @@ def test_kept_receipts_into_output_then_copy(fa, O, torch_gpu):
                 keep.append(buf)
                 agg.submit_gather(mp, k, views, w[k], pinned=True)
         out1 = agg.finalize(1)  # pageable destination
-        agg.reduce_parts([2, 3])  # the batched phase 2: kept parts reduce in place into their outputs
-        assert agg.host_reads() == 3
+        assert agg.host_reads() == 1
+        agg.reduce_parts([2, 3])  # the batched phase 2: the kept receipts are copied in, one batched launch
+        assert agg.host_reads() == 1
         out2 = agg.copy_output(2)
         dbuf, dviews = dst_views(fa, sizes[3], 4, [(0, sizes[3])], sizes[3] * 4)
         agg.finalize_gather(3, dviews, pinned=True)
-        assert agg.host_reads() == 3  # phase 2 was already reduced: the finalize only copies
+        assert agg.host_reads() == 1  # phase 2 was already reduced: the finalize only copies
         out3 = gathered(dviews, np.float32)
         for mp, got in ((1, out1), (2, out2), (3, out3)):
             assert np.array_equal(got.view(np.uint32), O.fedavg(xs[mp], w).view(np.uint32)), mp
