@@ -156,16 +156,16 @@ class _StreamSlot:
             _tracked[key] = _tracked.get(key, 0) + 1
 
     def __del__(self):
-        key = self.key
-        with _tracked_mu:
-            _tracked[key] -= 1
-            if _tracked[key]:
-                return
-            del _tracked[key]
         try:
+            key = self.key
+            with _tracked_mu:
+                _tracked[key] -= 1
+                if _tracked[key]:
+                    return
+                del _tracked[key]
             if _lib is not None:
                 _lib.fa_release_stream(key[0], key[1])
-        except Exception:  # interpreter shutdown
+        except Exception:  # interpreter shutdown: module globals may be gone
             pass
 
 
