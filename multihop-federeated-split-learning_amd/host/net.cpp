@@ -189,7 +189,15 @@ void NetLayer::stop() {
     // wake the receiver's poll/accept, and close the socket only after it has left: closing under it
     // raced its reads of listen_fd_ (TSan, tests/test_host_sanitizers.py) and could hand it a reused fd
     if (listen_fd_ >= 0) shutdown(listen_fd_, SHUT_RDWR);
-    if (rx_.joinable()) rx_.join();
+    if (rx_.joinable()) rx_.join();  // it has waited for every connection's reader to finish
+    {
+        std::lock_guard<std::mutex> lk(m_rd_);
+        rd_stop_ = true;
+    }
+    cv_rd_.notify_all();
+    for (auto& t : readers_)
+        if (t.joinable()) t.join();
+    readers_.clear();
     if (listen_fd_ >= 0) {
         close(listen_fd_);
         listen_fd_ = -1;
@@ -258,22 +266,34 @@ void NetLayer::publish(uint64_t seq, Item item) {
     cv_rx_.notify_all();
 }
 
+// A reader thread: takes accepted connections from rd_q_ and reads each to its end (reader_loop).
+void NetLayer::reader_worker() {
+    std::unique_lock<std::mutex> lk(m_rd_);
+    for (;;) {
+        ++rd_idle_;
+        cv_rd_.wait(lk, [&] { return rd_stop_ || !rd_q_.empty(); });
+        --rd_idle_;
+        if (rd_q_.empty()) return;  // stopping, nothing left to read
+        Conn* c = rd_q_.front();
+        rd_q_.pop_front();
+        lk.unlock();
+        reader_loop(c);  // sets c->done last
+        lk.lock();
+    }
+}
+
 void NetLayer::receiver_loop() {
     std::list<std::unique_ptr<Conn>> conns;
     auto reap = [&](bool all) {
-        for (auto it = conns.begin(); it != conns.end();) {
-            Conn& c = **it;
-            if (all && !c.done) {
-                std::lock_guard<std::mutex> g(c.m);
-                if (c.fd >= 0) shutdown(c.fd, SHUT_RDWR);  // unblocks a reader inside recv
+        if (all) {  // unblock every reader inside recv, then wait for each connection to be done
+            for (auto& c : conns) {
+                std::lock_guard<std::mutex> g(c->m);
+                if (c->fd >= 0) shutdown(c->fd, SHUT_RDWR);
             }
-            if (all || c.done) {
-                c.th.join();
-                it = conns.erase(it);
-            } else {
-                ++it;
-            }
+            for (auto& c : conns)
+                while (!c->done) std::this_thread::sleep_for(std::chrono::milliseconds(1));
         }
+        for (auto it = conns.begin(); it != conns.end();) it = (*it)->done ? conns.erase(it) : std::next(it);
     };
     const int lfd = listen_fd_;  // stop() closes it only after this thread has been joined
     while (running_) {
@@ -289,7 +309,12 @@ void NetLayer::receiver_loop() {
         Conn* c = conns.back().get();
         c->fd = fd;
         c->seq0 = take_seq();  // accept order fixes the FIFO position of the connection's first frame
-        c->th = std::thread(&NetLayer::reader_loop, this, c);
+        {
+            std::lock_guard<std::mutex> lk(m_rd_);
+            rd_q_.push_back(c);
+            if (rd_idle_ < (int)rd_q_.size()) readers_.emplace_back(&NetLayer::reader_worker, this);
+        }
+        cv_rd_.notify_one();
         reap(false);
     }
     reap(true);

@@ -6,7 +6,8 @@
 // sender threads (queue of outgoing frames, connect with retries, close unless
 // save_connection), and the main thread as the single consumer.
 // Differences, all deliberate:
-//  * every accepted connection is read by its own thread, so D data owners
+//  * every accepted connection is read by a reader thread of its own (from a pool of
+//    reusable readers), so D data owners
 //    sending at once are received in parallel (the reference reads one frame at
 //    a time in its select loop, :372-480).  The FIFO still holds frames in the
 //    reference's order -- the order their connections were accepted (or, on a
@@ -117,7 +118,6 @@ private:
         std::map<int, int> open;  // dest -> socket kept open (save_connection)
     };
     struct Conn {
-        std::thread th;
         std::atomic<bool> done{false};
         std::mutex m;
         int fd = -1;         // -1 once the reader closed it
@@ -132,6 +132,7 @@ private:
     void publish(uint64_t seq, Item item);
     void receiver_loop();
     void reader_loop(Conn* c);
+    void reader_worker();
     void sender_loop(int i);
     Item parse_frame(std::shared_ptr<Bytes> text, bool* keep);
     std::shared_ptr<Bytes> recv_frame_gated(int fd, uint64_t seq);
@@ -152,6 +153,17 @@ private:
     std::atomic<uint64_t> bytes_rx_{0};
     std::atomic<uint64_t> send_failures_{0};
     std::thread rx_;
+    // Reader threads, reused from connection to connection: the protocol opens a connection per frame (the
+    // reference's save_connection 0), and a thread started per connection put ~20-40 us of thread creation
+    // on every frame's path (a small model's round is a dozen frames).  An accepted connection waits in
+    // rd_q_ for an idle reader; when none is idle a new one starts, so concurrent owners are still read in
+    // parallel.  Idle readers stay for the next connections until stop().
+    std::mutex m_rd_;
+    std::condition_variable cv_rd_;
+    std::deque<Conn*> rd_q_;            // under m_rd_
+    int rd_idle_ = 0;                   // under m_rd_
+    bool rd_stop_ = false;              // under m_rd_
+    std::vector<std::thread> readers_;  // started by the receiver thread, joined by stop()
     std::mutex m_rx_;
     std::condition_variable cv_rx_;
     std::deque<Receipt> receipts_;
