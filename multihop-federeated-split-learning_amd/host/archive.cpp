@@ -12,6 +12,10 @@
 
 #include <zlib.h>
 
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
+
 namespace fahost {
 
 // ------------------------------------------------------------------ CRC-32 (IEEE, slicing-by-8)
@@ -35,7 +39,58 @@ const CrcTables& crc_tables() {
 }
 }  // namespace
 
-uint32_t crc32(const uint8_t* p, size_t n, uint32_t crc) {
+#if defined(__x86_64__)
+// Carry-less multiplication folding (PCLMULQDQ) over 16-byte blocks: four 128-bit accumulators fold 64 bytes
+// per step, then fold into one, reduce 128 -> 64 -> 32 bits and finish with a Barrett reduction -- the
+// method of Intel's "Fast CRC Computation for Generic Polynomials Using PCLMULQDQ" for the reflected IEEE
+// polynomial (constants x^(k) mod P for the fold distances, mu = floor(x^64 / P), P' = the polynomial).
+// `c` is the running (already inverted) state; n >= 64 and a multiple of 16.  ~10x the table's rate: a
+// reply's records are sealed with their CRC-32s (seal_params), which for a small model was the largest
+// host cost of a round.
+static inline __attribute__((target("pclmul,sse4.1"), always_inline)) __m128i clmul_fold(__m128i x, __m128i k,
+                                                                                         __m128i next) {
+    return _mm_xor_si128(_mm_xor_si128(_mm_clmulepi64_si128(x, k, 0x00), _mm_clmulepi64_si128(x, k, 0x11)), next);
+}
+
+static __attribute__((target("pclmul,sse4.1"))) uint32_t crc32_fold(const uint8_t* p, size_t n, uint32_t c) {
+    const __m128i k1k2 = _mm_set_epi64x(0x00000001c6e41596LL, 0x0000000154442bd4LL);
+    const __m128i k3k4 = _mm_set_epi64x(0x00000000ccaa009eLL, 0x00000001751997d0LL);
+    const __m128i k5 = _mm_set_epi64x(0, 0x0000000163cd6124LL);
+    const __m128i mu_p = _mm_set_epi64x(0x00000001f7011641LL, 0x00000001db710641LL);
+    const __m128i mask32 = _mm_set_epi32(0, 0, 0, -1);
+    auto ld = [](const uint8_t* q) { return _mm_loadu_si128(reinterpret_cast<const __m128i*>(q)); };
+    __m128i x1 = _mm_xor_si128(ld(p), _mm_cvtsi32_si128((int)c)), x2 = ld(p + 16), x3 = ld(p + 32),
+            x4 = ld(p + 48);
+    p += 64;
+    n -= 64;
+    for (; n >= 64; p += 64, n -= 64) {
+        x1 = clmul_fold(x1, k1k2, ld(p));
+        x2 = clmul_fold(x2, k1k2, ld(p + 16));
+        x3 = clmul_fold(x3, k1k2, ld(p + 32));
+        x4 = clmul_fold(x4, k1k2, ld(p + 48));
+    }
+    x1 = clmul_fold(x1, k3k4, x2);
+    x1 = clmul_fold(x1, k3k4, x3);
+    x1 = clmul_fold(x1, k3k4, x4);
+    for (; n >= 16; p += 16, n -= 16) x1 = clmul_fold(x1, k3k4, ld(p));
+    // 128 -> 64 bits (also appends 32 zero bits), then 64 -> 32
+    x1 = _mm_xor_si128(_mm_srli_si128(x1, 8), _mm_clmulepi64_si128(k3k4, x1, 0x01));
+    __m128i t = _mm_clmulepi64_si128(_mm_and_si128(x1, mask32), k5, 0x00);
+    x1 = _mm_xor_si128(_mm_srli_si128(x1, 4), t);
+    // Barrett reduction
+    t = _mm_and_si128(_mm_clmulepi64_si128(_mm_and_si128(x1, mask32), mu_p, 0x10), mask32);
+    t = _mm_clmulepi64_si128(t, mu_p, 0x00);
+    x1 = _mm_xor_si128(x1, t);
+    return (uint32_t)_mm_extract_epi32(x1, 1);
+}
+
+static bool have_clmul() {
+    static const bool h = __builtin_cpu_supports("pclmul") && __builtin_cpu_supports("sse4.1");
+    return h;
+}
+#endif
+
+uint32_t crc32_table(const uint8_t* p, size_t n, uint32_t crc) {
     const auto& T = crc_tables().t;
     uint32_t c = ~crc;
     while (n >= 8) {
@@ -50,6 +105,17 @@ uint32_t crc32(const uint8_t* p, size_t n, uint32_t crc) {
     }
     while (n--) c = T[0][(c ^ *p++) & 0xFF] ^ (c >> 8);
     return ~c;
+}
+
+uint32_t crc32(const uint8_t* p, size_t n, uint32_t crc) {
+#if defined(__x86_64__)
+    if (n >= 64 && have_clmul()) {
+        const size_t m = n & ~(size_t)15;
+        const uint32_t c = crc32_fold(p, m, ~crc);
+        return crc32_table(p + m, n - m, ~c);
+    }
+#endif
+    return crc32_table(p, n, crc);
 }
 
 // ------------------------------------------------------------------ little-endian helpers

@@ -90,6 +90,7 @@ private:
     std::vector<TensorView> params_, buffers_;
 };
 
-uint32_t crc32(const uint8_t* p, size_t n, uint32_t crc = 0);
+uint32_t crc32(const uint8_t* p, size_t n, uint32_t crc = 0);  // PCLMULQDQ folding where the CPU has it
+uint32_t crc32_table(const uint8_t* p, size_t n, uint32_t crc = 0);  // the portable slicing-by-8 form
 
 }  // namespace fahost

@@ -61,10 +61,21 @@ def test_network_layer_under_tsan():
         assert json.loads(r.stdout.strip().splitlines()[-1])["ok"]
 
 
+def test_reply_crc32_matches_zlib():
+    """The CRC-32 that seals every reply's zip records (host/archive.cpp: PCLMULQDQ folding where the CPU has
+    it) equals zlib's and the table form on every length 0..2999 at five misalignments and on multi-MB buffers
+    (tests/tools/crc_selftest.cpp); the reference's torch::load would reject a reply with a wrong one."""
+    subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "tools")], capture_output=True, timeout=600, check=True)
+    r = subprocess.run([os.path.join(BIN, "crc_selftest")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr[-2000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["bad"] == 0 and res["checks"] > 15_000
+
+
 def test_receipt_ledger_under_asan_ubsan():
-    """fa_aggregator's receipt ledger (host/receipts.h): late copies of earlier rounds, before and after the
-    current receipt, in both phases, dropped; copies at the floor's millisecond decided by content; a frozen
-    part resent later and a retransmission of the current receipt kept (tests/tools/receipts_selftest.cpp)."""
+    """fa_aggregator's receipt ledger (host/receipts.h): late byte copies of earlier rounds, before and after
+    the current receipt, in both phases, dropped; an owner clock stepped back, a frozen part resent under a new
+    stamp and a retransmission of the current receipt kept (tests/tools/receipts_selftest.cpp)."""
     for exe in ("receipts_selftest", "receipts_selftest_asan"):
         if exe == "receipts_selftest":
             subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "tools")], capture_output=True, timeout=600,
