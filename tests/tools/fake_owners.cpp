@@ -21,6 +21,9 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -72,6 +75,55 @@ bool restamp(Bytes& f, long t) {
 }
 
 constexpr long kStampPlaceholder = 1000000000000L;
+
+// The data owners' sending threads, one per owner for the whole run (each owner is a process of its own in
+// the reference): a phase hands every owner its job and waits for all of them, with no thread started per
+// phase (that cost ~20-40 us per owner on the round's path, a test artifact a deployment does not have).
+class OwnerThreads {
+public:
+    explicit OwnerThreads(int n) {
+        for (int k = 0; k < n; ++k) th_.emplace_back([this, k] { loop(k); });
+    }
+    ~OwnerThreads() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            quit_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    void run(std::function<void(int)> job) {  // job(k) on owner k's thread, for every owner; returns when all did
+        std::unique_lock<std::mutex> lk(m_);
+        job_ = std::move(job);
+        done_ = 0;
+        ++gen_;
+        cv_.notify_all();
+        done_cv_.wait(lk, [&] { return done_ == (int)th_.size(); });
+    }
+
+private:
+    void loop(int k) {
+        unsigned long seen = 0;
+        std::unique_lock<std::mutex> lk(m_);
+        for (;;) {
+            cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
+            if (quit_) return;
+            seen = gen_;
+            auto job = job_;
+            lk.unlock();
+            job(k);
+            lk.lock();
+            if (++done_ == (int)th_.size()) done_cv_.notify_all();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_cv_;
+    std::function<void(int)> job_;
+    unsigned long gen_ = 0;
+    int done_ = 0;
+    bool quit_ = false;
+};
 
 struct Part {
     int mp;
@@ -224,6 +276,7 @@ int main(int argc, char** argv) {
         return (int)got->size() == want;
     };
     const int threads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    OwnerThreads owners(concurrent ? D : 0);
     auto fill = [&](uint64_t sd, uint32_t k, size_t n, int es, uint8_t* x) {  // the oracle's generator, in chunks
         std::vector<std::thread> th;
         const size_t per = (n + threads - 1) / threads;
@@ -291,17 +344,14 @@ int main(int argc, char** argv) {
                 if (f.second && !restamp(*f.first, owner_now(k, round))) send_ok = false;
             };
             if (concurrent) {  // every owner is its own process in the reference: they send at once
-                std::vector<std::thread> th;
-                for (int k = 0; k < D; ++k)
-                    th.emplace_back([&, k] {
-                        for (auto& f : by_owner[k]) {
-                            const int fd = connect_to(routes.host_for(-1), routes.port_for(-1), 100, 200);
-                            stamp(k, f);
-                            if (fd < 0 || !send_all(fd, f.first->data(), f.first->size())) send_ok = false;
-                            if (fd >= 0) close(fd);
-                        }
-                    });
-                for (auto& t : th) t.join();
+                owners.run([&](int k) {
+                    for (auto& f : by_owner[k]) {
+                        const int fd = connect_to(routes.host_for(-1), routes.port_for(-1), 100, 200);
+                        stamp(k, f);
+                        if (fd < 0 || !send_all(fd, f.first->data(), f.first->size())) send_ok = false;
+                        if (fd >= 0) close(fd);
+                    }
+                });
             } else {  // one after another, in owner order (literal mode: the last receipt is owner D-1's)
                 for (int k = 0; k < D; ++k)
                     for (auto& f : by_owner[k]) {
