@@ -81,6 +81,9 @@ public:
                      std::string* err) const;
     void seal_params(uint8_t* dst) const;
     size_t size() const { return size_; }
+    // Parses that took their tensor views from the layout cache (an archive with the same structure, pickle
+    // and code records as one parsed before: every receipt of a bucket), process-wide.
+    static unsigned long long layout_cache_hits();
 
 private:
     const uint8_t* base_ = nullptr;

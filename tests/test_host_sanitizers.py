@@ -72,6 +72,22 @@ def test_reply_crc32_matches_zlib():
     assert res["bad"] == 0 and res["checks"] > 15_000
 
 
+def test_archive_layout_cache():
+    """Every receipt of a bucket is the same module saved again, so the archive parse caches its tensor views
+    by structure + pickle + code records (host/archive.cpp): on every committed receipt archive a second copy
+    with other parameter values, elsewhere in memory, hits the cache and its views equal the walk's, rebased;
+    a changed pickle byte misses it (tests/tools/archive_cache_selftest.cpp)."""
+    import glob
+    subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "tools")], capture_output=True, timeout=600, check=True)
+    blobs = sorted(glob.glob(os.path.join(GOLDEN, "*", "mp*_client0.pt")))
+    assert len(blobs) >= 5
+    r = subprocess.run([os.path.join(BIN, "archive_cache_selftest")] + blobs, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr[-2000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["failed"] == 0 and res["checks"] == 6 * len(blobs) and res["hits"] == 2 * len(blobs)
+
+
 def test_receipt_ledger_under_asan_ubsan():
     """fa_aggregator's receipt ledger (host/receipts.h): late byte copies of earlier rounds, before and after
     the current receipt, in both phases, dropped; an owner clock stepped back, a frozen part resent under a new
