@@ -111,7 +111,9 @@ int fa_submit(fa_ctx* ctx, int part_id, int client_slot, const void* host_src, f
  * the phase (a small model's round is bound by round trips, not bytes).  Same
  * bits.  Calls before it that need the device slots (fa_reduce_part(s),
  * fa_sync_part, fa_bucket_slot/_piece, a pageable submit to the part) copy the
- * kept receipts in first.  FA_HOST_READ=0 in the environment turns this off. */
+ * kept receipts in first.  A finalize that wrote a pinned destination this way
+ * leaves the part's device output (fa_bucket_output) as it was.  FA_HOST_READ=0
+ * in the environment turns this off. */
 #define FA_HOST_READ_MAX_BYTES (1u << 20)
 int fa_submit_pinned(fa_ctx* ctx, int part_id, int client_slot, const void* host_src, float weight);
 

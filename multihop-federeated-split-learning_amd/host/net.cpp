@@ -347,14 +347,12 @@ void NetLayer::gate_leave() {
 std::shared_ptr<Bytes> NetLayer::recv_frame_gated(int fd, uint64_t seq) {
     int32_t len = 0;
     if (!recv_all(fd, &len, 4) || len <= 0) return nullptr;
-    bool gated = gate_limit_ > 0 && (size_t)len >= kGateBytes;
-    if (gated && !gate_enter(seq)) return nullptr;
+    // the header first, outside the gate: a sender that stalls inside it holds up only its own reader
     char head[kHeadBytes];
     const size_t have = std::min<size_t>(kHeadBytes, (size_t)len);
-    if (!recv_all(fd, head, have)) {
-        if (gated) gate_leave();
-        return nullptr;
-    }
+    if (!recv_all(fd, head, have)) return nullptr;
+    bool gated = gate_limit_ > 0 && (size_t)len >= kGateBytes;
+    if (gated && !gate_enter(seq)) return nullptr;
     auto b = frame_buffer_for(head, have, (size_t)len);
     char* c = reinterpret_cast<char*>(b->data()) + have;
     size_t n = (size_t)len - have;
