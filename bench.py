@@ -185,11 +185,12 @@ def e2e_c1(agg_cmd, mode, port_base, rounds=C1_E2E_ROUNDS, startup_s=0.5, timeou
                     agg.wait()
         agg_out.seek(0)
         phases = []  # fa_aggregator's own round lines (the reference process prints a log, no JSON)
-        for l in agg_out.read().splitlines():
-            try:
-                phases.append(json.loads(l)) if l.startswith("{") else None
-            except ValueError:
-                pass
+        for line in agg_out.read().splitlines():
+            if line.startswith("{"):
+                try:
+                    phases.append(json.loads(line))
+                except ValueError:
+                    pass
         agg_out.close()
     if r.returncode not in (0, 1):
         raise RuntimeError("fake owners rc %d: %s" % (r.returncode, r.stderr[-300:]))
@@ -204,7 +205,7 @@ def e2e_c1(agg_cmd, mode, port_base, rounds=C1_E2E_ROUNDS, startup_s=0.5, timeou
                   "absorb_ms": med(lambda p: p["phase1"]["absorb_s"] + p["phase2"]["absorb_s"]),
                   "note": "medians over rounds 1.. of the aggregator's own round lines: reduce = the batched GPU "
                           "reduction + D2H into the reply frame + framing, absorb = archive parse + H2D submit"}
-    return {"aggregator_view": server,"rounds_timed": len(ms), "round_ms_median": round(statistics.median(ms), 3),
+    return {"aggregator_view": server, "rounds_timed": len(ms), "round_ms_median": round(statistics.median(ms), 3),
             "round_ms_mean": round(statistics.mean(ms), 3),
             "round_ms_min": min(ms), "round0_ms": res["round_ms"][0], "mode": mode,
             "parity": {"check": "every element of every reply bit-exact vs the oracle (fake owners: %s)" %
