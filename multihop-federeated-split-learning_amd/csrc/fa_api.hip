@@ -837,14 +837,49 @@ int host_reduce(fa_ctx* ctx, Part& p, const float* w, hipStream_t s, const Gathe
         return nullptr;
     };
     hipStream_t st = s ? s : r.compute;
-    std::vector<const void*> ptrs(ks.size());
-    for (size_t c = 0; c + 1 < cuts.size(); ++c) {
-        const size_t a = cuts[c], len = cuts[c + 1] - a;
-        for (size_t i = 0; i < ks.size(); ++i) ptrs[i] = at(p.host_src[(size_t)ks[i]], a, si);
-        void* o = dst ? const_cast<char*>(at(out, a, so)) : static_cast<char*>(p.dout[0]) + a * so;
-        int rc = reduce_on(ctx, 0, ctx->tuning.tu, ptrs.data(), w, (int)ks.size(), len, p.in, o, p.out, p.mode,
-                           p.divisor, nullptr, st);
-        if (rc) return rc;
+    const size_t npc = cuts.size() - 1, nk = ks.size();
+    std::vector<const void*> ptrs(npc * nk);
+    std::vector<void*> outs(npc);
+    bool aligned16 = true;  // every piece 16-byte aligned at both ends of the chain: one batched launch
+    for (size_t c = 0; c < npc; ++c) {
+        for (size_t i = 0; i < nk; ++i) {
+            ptrs[c * nk + i] = at(p.host_src[(size_t)ks[i]], cuts[c], si);
+            aligned16 = aligned16 && (uintptr_t)ptrs[c * nk + i] % 16 == 0;
+        }
+        outs[c] = dst ? const_cast<char*>(at(out, cuts[c], so)) : static_cast<char*>(p.dout[0]) + cuts[c] * so;
+        aligned16 = aligned16 && (uintptr_t)outs[c] % 16 == 0;
+    }
+    const fa::Tuning& tu = ctx->tuning.tu;
+    if (p.mode == FA_FEDAVG && aligned16 && nk <= (size_t)fa::kMaxClients && npc <= (size_t)fa::kSegArgMax &&
+        npc * nk <= (size_t)fa::kSegArgClients) {
+        // the archive records are 64-byte aligned in the frames (host/wire.cpp), so the pieces of a receipt
+        // and of its reply usually are: every piece in one segment launch (the same chain, the same bits)
+        fa::SegArgs a{};
+        const size_t V = 16 / si;
+        int64_t blocks = 0;
+        for (size_t c = 0; c < npc; ++c) {
+            const size_t len = cuts[c + 1] - cuts[c];
+            a.nc[c] = (int)nk;
+            a.src0[c] = (int)(c * nk);
+            a.blk0[c] = blocks;
+            a.nvec[c] = (int64_t)(len / V);
+            a.n[c] = (int64_t)len;
+            a.out[c] = outs[c];
+            blocks += std::max<int64_t>(1, (a.nvec[c] + tu.block - 1) / tu.block);
+            for (size_t i = 0; i < nk; ++i) {
+                a.src[c * nk + i] = ptrs[c * nk + i];
+                a.w[c * nk + i] = w[ks[i]];
+            }
+        }
+        a.nseg = (int)npc;
+        a.blk0[npc] = blocks;
+        FA_HIP(fa::launch_segargs(a, p.in, p.out, (int)nk, tu, st));
+    } else {
+        for (size_t c = 0; c < npc; ++c) {
+            int rc = reduce_on(ctx, 0, tu, &ptrs[c * nk], w, (int)nk, cuts[c + 1] - cuts[c], p.in, outs[c], p.out,
+                               p.mode, p.divisor, nullptr, st);
+            if (rc) return rc;
+        }
     }
     ++ctx->host_reads;
     if (dst) {

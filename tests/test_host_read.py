@@ -93,6 +93,40 @@ def test_small_pinned_round_reads_in_place(fa, O, torch_gpu, D, n, in_bf16, out_
                                   want.view(np.uint16 if out_bf16 else np.uint32))
 
 
+@pytest.mark.parametrize("in_bf16,out_bf16", [(False, False), (True, True), (False, True), (True, False)])
+def test_aligned_records_in_one_launch(fa, O, torch_gpu, in_bf16, out_bf16):
+    """Records 64-byte aligned in the receipts and the reply (as fa_aggregator's frames hold them): all
+    pieces of the phase in one segment launch -- bit-exact, f32 / bf16 in and out."""
+    D, n = 3, 50_536
+    es, eo = (2 if in_bf16 else 4), (2 if out_bf16 else 4)
+    xs = [O.gen(0xA11, k, n, dtype="bf16" if in_bf16 else "f32") for k in range(D)]
+    w = O.weights(D)
+    cuts = [2400, 2416, 50_416]  # LeNet-5 part 1's records: 2400 / 16 / 48 000 / 120 elements
+    def aligned_layout(es_):
+        segs, off, edges = [], 0, [0] + cuts + [n]
+        for a, b in zip(edges, edges[1:]):
+            off = (off + 63) // 64 * 64
+            segs.append((off, b - a))
+            off += (b - a) * es_
+        return segs, off
+    with fa.Aggregator(1) as agg:
+        agg.define(1, n, fa.BF16 if in_bf16 else fa.F32, fa.BF16 if out_bf16 else fa.F32, D, fa.FEDAVG)
+        keep = []
+        for k in range(D):
+            segs, total = aligned_layout(es)
+            buf, views = place(fa, xs[k], segs, total)
+            keep.append(buf)
+            agg.submit_gather(1, k, views, w[k], pinned=True)
+        dsegs, dtotal = aligned_layout(eo)
+        dbuf, dviews = dst_views(fa, n, eo, dsegs, dtotal)
+        agg.finalize_gather(1, dviews, pinned=True)
+        assert agg.host_reads() == 1
+        got = gathered(dviews, np.uint16 if out_bf16 else np.float32)
+        want = expected(O, xs, w, in_bf16, out_bf16)
+        assert np.array_equal(got.view(np.uint16 if out_bf16 else np.uint32),
+                              want.view(np.uint16 if out_bf16 else np.uint32))
+
+
 def test_literal_last_receipt_in_place(fa, O, torch_gpu):
     n, D = 10_164, 3
     xs = [O.gen(0x1234, k, n) for k in range(D)]
