@@ -59,7 +59,8 @@ def expected(O, xs, w, in_bf16, out_bf16, literal=None):
         return O.literal(xs[literal], out_dtype="bf16" if out_bf16 else "f32")
     if in_bf16:
         return O.fedavg(xs, w, out_dtype="bf16" if out_bf16 else "f32")
-    return O.fedavg(xs, w)
+    ref = O.fedavg(xs, w)
+    return O.f32_to_bf16(ref) if out_bf16 else ref  # the fp32 chain, rounded once (RNE)
 
 
 @pytest.mark.parametrize("D,n,in_bf16,out_bf16", [(1, 777, False, False), (2, 50_536, False, False),
