@@ -137,6 +137,7 @@ C1_E2E_ROUNDS = 40
 FAKE_OWNERS = os.path.join(ROOT, "tests", "tools", "bin", "fa_fake_owners")
 FA_AGGREGATOR = os.path.join(PKG_DIR, "bin", "fa_aggregator")
 REF_CPU_AGGREGATOR = os.path.join(ROOT, "oracle", "_ref", "ref_cpu_aggregator")
+REF_BINDING_AGGREGATOR = os.path.join(ROOT, "oracle", "_ref", "ref_aggregator")  # + INTEGRATION.md 2 on libfa
 REF_PORTS = (8080, 8081, 8082, 8083)  # the reference's fixed routing table (network_layer.h:80-86)
 
 
@@ -161,7 +162,7 @@ def free_port_base():
     raise RuntimeError("no free port range")
 
 
-def e2e_c1(agg_cmd, mode, port_base, rounds=C1_E2E_ROUNDS, startup_s=0.5, timeout=120):
+def e2e_c1(agg_cmd, mode, port_base, rounds=C1_E2E_ROUNDS, startup_s=0.5, timeout=120, owner_flags=()):
     """Rounds of BASELINE C1 (LeNet-5, D = 2, fp32) through one aggregator process over loopback; returns the
     owners' round times (round 0, which allocates, reported apart) and their bit-exact check of every reply."""
     golden = os.path.join(ROOT, "tests", "golden", "lenet5_c1")
@@ -174,7 +175,7 @@ def e2e_c1(agg_cmd, mode, port_base, rounds=C1_E2E_ROUNDS, startup_s=0.5, timeou
                 raise RuntimeError("aggregator exited early (rc %s)" % agg.returncode)
             r = subprocess.run([FAKE_OWNERS, "--blobs", golden, "--parts", "1,2,3", "-d", "2", "-c", "1",
                                 "--rounds", str(rounds), "--port-base", str(port_base), "--model-name", "2",
-                                "--start", "6", "--end", "1", "--mode", mode, "--reply-timeout", "30"],
+                                "--start", "6", "--end", "1", "--mode", mode, "--reply-timeout", "30"] + list(owner_flags),
                                capture_output=True, text=True, timeout=timeout, cwd=tmp)
         finally:
             if agg.poll() is None:
@@ -1485,6 +1486,18 @@ def single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier):
                      "--port-base", str(base)], mode, base)
             except Exception as e:  # noqa: BLE001
                 c1["e2e_loopback_" + mode] = {"error": repr(e)[:300]}
+        # the maintainer's other option: the reference's own process with its reduction
+        # replaced by the libfa binding -- its network layer, torch::load per receipt, torch::save per reply
+        if os.access(REF_BINDING_AGGREGATOR, os.X_OK) and ports_free(REF_PORTS):
+            try:
+                c1["e2e_loopback_reference_process_with_binding"] = dict(
+                    e2e_c1([REF_BINDING_AGGREGATOR, "2", "1"], "fedavg", 8079, startup_s=2.5,
+                           owner_flags=["--sequential"]),
+                    path="the reference's aggregator process (systemAPI / network_layer / torch::load / "
+                         "torch::save) with aggregator.cpp:55-167 replaced by the INTEGRATION.md 2 binding on "
+                         "libfa.so (oracle/_ref/ref_aggregator)")
+            except Exception as e:  # noqa: BLE001
+                c1["e2e_loopback_reference_process_with_binding"] = {"error": repr(e)[:300]}
 
     def one(key, s, desc):
         torch.cuda.synchronize()
