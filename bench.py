@@ -846,6 +846,13 @@ def read_plain_peak(fa, torch, setup, stream, reps=5):
             "kernel": "plain grid-stride read, 256 lanes per workgroup, nt 16-byte loads, slot after slot"}
 
 
+def settle(freed_bytes):
+    """Wait out the driver's clear of device memory just freed before the next leg is timed: the clear runs
+    beside the next leg's kernels at ~35 GB/s of freed memory (the c4 workload 0.87 -> 0.83-0.84 of spec for
+    1.3 s after 36 GiB were freed, for 3.7 s after 129 GiB; tools/order_effect.py, gpurun_out r05s24-s25)."""
+    time.sleep(min(8.0, freed_bytes / 30e9))
+
+
 def timed_loop(torch, setup, steps, warmup, stream, dist, barrier, per_launch=10):
     """`steps` steps back to back, bracketed by barrier + synchronize: returns (wall seconds, region_ms, kern_ms).
 
@@ -1213,6 +1220,7 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_secondary:
         setup.close()
+        settle(setup.input_bytes())
         line["secondary"] = single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier)
         for key, fig in cpu_per.items():  # the reference's CPU path beside each config's device figure
             line["secondary"].setdefault(key, {}).update(fig)
@@ -1456,6 +1464,7 @@ def single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier):
                      "frac_of_read_stream_independent": round(achieved / ri["GBs"], 4) if ri else None,
                      "input_sets_rotated": s.nsets, "parity": parity_guarded(lambda: s.parity(0))}
         s.close()
+        settle(s.nsets * s.input_bytes())
 
     # the buckets of one aggregator round as it forms them: per-round device time and roofline fraction,
     # phase 2 batched (fa_reduce_parts) and, for comparison, one launch per part
@@ -1472,6 +1481,7 @@ def single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier):
                 "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "input_sets_rotated": s.nsets,
                 "parity": parity_guarded(lambda: s.parity())}
             s.close()
+            settle(s.nsets * s.input_bytes())
 
     # BASELINE C1 end to end: the drop-in process fa_aggregator on this GPU against the fake owners over
     # loopback, FedAvg (owners at once) and the reference-literal mode (owners in turn, as the CPU reference
@@ -1507,6 +1517,7 @@ def single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier):
                     "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                     "input_sets_rotated": s.nsets, "parity": parity_guarded(lambda: s.parity(0))}
         s.close()
+        settle(s.nsets * s.input_bytes())
     # compute-node aggregation on the C2 shape: 8 client copies synced in place
     sD, sn, si, so, _ = WORKLOADS["c2"]
     one("sync_c2", SyncSetup(fa, torch, sD, sn, si, so, 0, device),

@@ -1537,6 +1537,16 @@ int fa_create_ex(fa_ctx** out, const int* device_ids, int n_gpus, int flags) {
     ctx->tuning = defaults();
     ctx->gpu.resize((size_t)n_gpus);
     const int threads = std::max(1, default_copy_threads() / n_gpus);
+    // The exchange stream exists only where there is an exchange (the rs layout).  A high-priority stream
+    // costs every launch on the device ~2% while its queue lives, even idle (the c4 workload 0.875 -> 0.858
+    // of spec once one more high-priority stream had been created, and it stays so after the stream is
+    // destroyed -- the runtime keeps the queue; tools/order_effect.py, gpurun_out r05s27-s29).  FA_COMM_ALWAYS=1
+    // creates it for every context, as up to round 5 (experiments).
+    static const bool comm_always = [] {
+        const char* e = std::getenv("FA_COMM_ALWAYS");
+        return e && std::atoi(e) > 0;
+    }();
+    const bool need_comm = comm_always || (flags & FA_SHARD_CLIENT_RS);
     for (int g = 0; g < n_gpus; ++g) {
         GpuRes& r = ctx->gpu[(size_t)g];
         r.dev = device_ids[g];
@@ -1547,7 +1557,7 @@ int fa_create_ex(fa_ctx** out, const int* device_ids, int n_gpus, int flags) {
                   hipStreamCreateWithFlags(&r.copy, hipStreamNonBlocking) == hipSuccess &&
                   // the rs exchange's stream at the highest priority: its RCCL blocks are dispatched ahead of
                   // the next piece's reduction waiting on the compute stream
-                  hipStreamCreateWithPriority(&r.comm, hipStreamNonBlocking, prio_hi) == hipSuccess &&
+                  (!need_comm || hipStreamCreateWithPriority(&r.comm, hipStreamNonBlocking, prio_hi) == hipSuccess) &&
                   hipEventCreateWithFlags(&r.copy_ev, hipEventDisableTiming) == hipSuccess &&
                   hipEventCreateWithFlags(&r.step_ev, hipEventDisableTiming) == hipSuccess;
         for (int i = 0; ok && i < 2; ++i)
@@ -1913,7 +1923,7 @@ int fa_sync(fa_ctx* ctx) {
         DeviceGuard dg(r.dev);
         FA_HIP(hipStreamSynchronize(r.copy));
         FA_HIP(hipStreamSynchronize(r.compute));
-        FA_HIP(hipStreamSynchronize(r.comm));
+        if (r.comm) FA_HIP(hipStreamSynchronize(r.comm));
     }
     return FA_OK;
 }
