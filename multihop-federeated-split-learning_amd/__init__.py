@@ -99,6 +99,7 @@ def lib():
         "fa_diag_phased_slot": (I, [I, P, ctypes.POINTER(I)]),
         "fa_diag_phased_owned": (I, [I]),
         "fa_diag_host_reads": (ctypes.c_longlong, [P]),
+        "fa_diag_exchange_streams": (I, [P]),
         "fa_set_tuning": (I, [ctypes.POINTER(_Tuning)]),
         "fa_get_tuning": (I, [ctypes.POINTER(_Tuning)]),
     }
@@ -508,6 +509,10 @@ class Aggregator:
         """fa_diag_host_reads (diagnostic): reductions of this context that read their receipts where they
         arrived (small pinned receipts of a one-GPU range part)."""
         return lib().fa_diag_host_reads(self.handle)
+
+    def exchange_streams(self):
+        """fa_diag_exchange_streams (diagnostic): GPUs of this context holding an exchange stream (rs only)."""
+        return lib().fa_diag_exchange_streams(self.handle)
 
     def close(self):
         if self.handle:

@@ -2060,6 +2060,15 @@ extern "C" int fa_diag_read_plain(const void* const* d_bufs, int nc, size_t n, i
 // (small pinned receipts, host_reduce); -1 for a null context.
 extern "C" long long fa_diag_host_reads(fa_ctx* ctx) { return ctx ? (long long)ctx->host_reads : -1; }
 
+// GPUs of the context that hold an exchange stream: the rs layout's high-priority stream, none otherwise
+// (fa_create: a second high-priority stream on a device slows every later launch there).
+extern "C" int fa_diag_exchange_streams(fa_ctx* ctx) {
+    if (!ctx) return -1;
+    int n = 0;
+    for (auto& r : ctx->gpu) n += r.comm ? 1 : 0;
+    return n;
+}
+
 // Diagnostic, not part of the ABI in fa.h: the per-workgroup timeline of the last phased launch on `device`
 // when the process runs with FA_TIMELINE=1 (tools/timeline.py).
 extern "C" int fa_diag_phased_timeline(int device, unsigned long long* out, int cap) {

@@ -36,6 +36,21 @@ def rs_ctx(fa, G):
 
 # ----------------------------------------------------------------- FA_SHARD_CLIENT_RS
 
+@pytest.mark.gpu
+def test_exchange_stream_only_in_rs_contexts(fa, torch_gpu):
+    """Only the rs layout has an exchange, so only an rs context holds the (high-priority) exchange stream:
+    a second high-priority stream on a device slowed every later launch there by ~2% (DESIGN.md 5,
+    profiles/r05_order_effect.jsonl), e.g. a process that creates a context per workload."""
+    with fa.Aggregator(1) as agg:
+        assert agg.exchange_streams() == 0
+    with fa.Aggregator(1, eager=True) as agg:
+        assert agg.exchange_streams() == 0
+    with fa.Aggregator(devices=[0, 0], shared_device=True) as agg:  # range layout on two shards
+        assert agg.exchange_streams() == 0
+    with rs_ctx(fa, 2) as agg:
+        assert agg.exchange_streams() == 2
+
+
 @pytest.mark.parametrize("n,D,chunks,bf16,out_bf16", [
     (1_000_003, 5, 1, False, False), (4_194_304, 8, 8, False, False), (333_333, 3, 4, True, False),
     (63, 2, 3, False, False), (2_000_000, 130, 2, False, False),
