@@ -11,7 +11,8 @@
  * Threading: one fa_ctx per aggregator; calls on one ctx are serialized by the
  * caller (the reference's single consumer main thread, aggregator.cpp:60/:113).
  * Device work runs on ctx-owned HIP streams (one compute + one copy stream per
- * GPU) or on the caller's stream for fa_reduce_device.
+ * GPU, plus a high-priority exchange stream per GPU for FA_SHARD_CLIENT_RS only)
+ * or on the caller's stream for fa_reduce_device.
  *
  * Numerics (tests/, DESIGN.md "Parity"):
  *   FA_FEDAVG  out_i = sum_k w_k x_{k,i} as an ordered fp32 FMA chain in client
