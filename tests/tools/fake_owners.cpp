@@ -9,11 +9,13 @@
 //   fa_fake_owners --blobs DIR --parts 1,2,3 -d D -c C [--rounds R] [--mode fedavg|literal]
 //                  [--port-base P] [--model-name N --model-type T --start S --end E] [--seed X]
 //                  [--drop-owner K [--drop-phase P]] [--retransmit K] [--retransmit-late K]
-//                  [--clock-skew K,S] [--reply-timeout S] [--rel-tol X]
+//                  [--clock-skew K,S] [--reply-timeout S] [--rel-tol X] [--routing-table]
 //                  [--sequential]   (owners send at once, one connection each, unless --sequential
 //                                    or --mode literal, whose result depends on the arrival order)
 // Every frame is stamped (t_start, network_layer.cpp:761) when it first goes out, on its owner's clock;
 // --clock-skew K,S sets owner K's clock back S ms more every round (an NTP step, a VM resume).
+// --routing-table: the refactor message carries the owners' addresses (read_table 1, as the init node's
+// does, network_layer.cpp:335-359); the reference's own process cannot reach an owner id above 3 without it.
 // Prints one JSON line: {"ok": bool, "rounds": R, "checked_elems": ..., "round_ms": [...]}.
 #include <unistd.h>
 
@@ -147,6 +149,7 @@ int main(int argc, char** argv) {
     int skew_owner = -1;                  // --clock-skew K,S: owner K's clock goes back S ms every round
     long skew_ms = 0;
     double rel_tol = 0;                   // > 0: fp32 replies within rel_tol * sum_k |w_k x_k| (the rs layout)
+    bool routing_table = false;           // --routing-table: the refactor message carries the owners' addresses
     long reply_timeout_ms = 600000;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
@@ -165,6 +168,7 @@ int main(int argc, char** argv) {
         else if (a == "--seed") seed = std::strtoull(v, nullptr, 0), ++i;
         else if (a == "--divisor") divisor = (float)std::atof(v), ++i;
         else if (a == "--sequential") concurrent = false;
+        else if (a == "--routing-table") routing_table = true;
         else if (a == "--drop-owner") drop_owner = std::atoi(v), ++i;
         else if (a == "--drop-phase") drop_phase = std::atoi(v), ++i;
         else if (a == "--retransmit") retransmit = std::atoi(v), ++i;
@@ -247,6 +251,11 @@ int main(int argc, char** argv) {
     rf.dataset = 0;
     rf.data_owners = ids;
     rf.read_table = 0;
+    if (routing_table) {  // the addresses of owners 4..17 (systemAPI.cpp:212-240): the reference needs them
+        for (int id : ids)
+            if (id > 3) rf.rooting_table.push_back({id, "127.0.0.1"});
+        rf.read_table = 1;
+    }
     tx.send(-1, frame_bytes(rf));
 
     std::vector<float> w(D, 1.0f / (float)D);  // the aggregator's default weights
