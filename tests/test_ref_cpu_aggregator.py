@@ -83,6 +83,36 @@ def test_reference_cpu_process_serves_c1_bit_exact():
     assert status is None  # still serving
 
 
+def test_reference_cpu_process_serves_c2_eight_owners(tmp_path):
+    """BASELINE C2 (ResNet-18 split "3,8", 8 owners) through the reference's process: receipt templates from
+    the reference's own builders (ref_harness golden), the owners' addresses in the refactor message
+    (fake_owners --routing-table; without it the reference cannot reach owner ids above 3), one round,
+    every reply bit-exact.  tools/e2e_c2_ref.py times the same pairing against fa_aggregator."""
+    harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    for mp in ("-1", "2"):
+        subprocess.run([harness, "golden", "1", "1", "9", "3", "10", "8", "24301", "7", str(tmp_path), mp],
+                       check=True, capture_output=True, timeout=600)
+    if not ports_free():
+        pytest.skip("the reference's fixed ports 8080-8083 are in use")
+    with tempfile.TemporaryDirectory() as cwd:
+        agg = subprocess.Popen([REF_CPU_AGG, "8", "1"], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, cwd=cwd,
+                               start_new_session=True)
+        try:
+            time.sleep(2.5)
+            assert agg.poll() is None, agg.stderr.read()
+            r = subprocess.run([OWNERS, "--blobs", str(tmp_path), "--parts", "1,2,3", "-d", "8", "-c", "1",
+                                "--rounds", "1", "--port-base", "8079", "--model-name", "1", "--model-type", "1",
+                                "--start", "9", "--end", "3", "--mode", "literal", "--reply-timeout", "120",
+                                "--routing-table"], capture_output=True, text=True, timeout=300, cwd=cwd)
+        finally:
+            if agg.poll() is None:
+                os.killpg(agg.pid, 9)
+            agg.wait(timeout=30)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["ok"] and res["checked_elems"] == 8 * (83_584 + 9_442_304 + 5_130)
+
+
 def test_reference_cpu_process_takes_a_late_copy():
     r, status = run_pair(["--retransmit-late", "1"], rounds=2, reply_timeout=5)
     res = json.loads(r.stdout.strip().splitlines()[-1])
