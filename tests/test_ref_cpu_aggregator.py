@@ -87,7 +87,7 @@ def test_reference_cpu_process_serves_c2_eight_owners(tmp_path):
     """BASELINE C2 (ResNet-18 split "3,8", 8 owners) through the reference's process: receipt templates from
     the reference's own builders (ref_harness golden), the owners' addresses in the refactor message
     (fake_owners --routing-table; without it the reference cannot reach owner ids above 3), one round,
-    every reply bit-exact.  tools/e2e_c2_ref.py times the same pairing against fa_aggregator."""
+    every reply bit-exact.  tools/e2e_ref.py c2 times the same pairing against fa_aggregator."""
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
     for mp in ("-1", "2"):
         subprocess.run([harness, "golden", "1", "1", "9", "3", "10", "8", "24301", "7", str(tmp_path), mp],

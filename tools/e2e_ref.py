@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
-"""BASELINE C2 end to end: the reference's own aggregator process against the drop-in, same blobs (GPU box).
+"""A BASELINE config end to end: the reference's own aggregator process against the drop-in, same receipts.
 
-  python tools/e2e_c2_ref.py [ref_rounds=3] [rounds=10]
+  python tools/e2e_ref.py [c2|c3] [ref_rounds=3] [rounds=10]     (GPU box)
 
-C2 is ResNet-18 split "3,8" with 8 data owners (buckets 83 584 / 9 442 304 / 5 130 fp32).  The receipt
-templates are made here by oracle/_ref/ref_harness (the reference's own model builders and torch::save), so
-the reference process can torch::load them into its modules.  Then, over loopback with the fake data owners
+C2 is ResNet-18 split "3,8" with 8 data owners (buckets 83 584 / 9 442 304 / 5 130), C3 ResNet-101 split
+"10,19" with 32 (2 594 688 / 29 511 680 / 5 130), both fp32 here: the reference has no bf16 path.  The
+receipt templates are made here by oracle/_ref/ref_harness (the reference's own model builders and
+torch::save), so the reference process can torch::load them into its modules.  Then, over loopback with the fake data owners
 (tests/tools, every reply checked against the oracle):
   * oracle/_ref/ref_cpu_aggregator 8 1 -- the reference's systemAPI / network_layer process on CPU libtorch,
     aggregator.cpp:55-167 restated (literal mode: the owners send in turn, as its result depends on order);
@@ -28,19 +29,22 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
-SPEC = ["1", "1", "9", "3", "10"]  # resnet, resnet18, start 9, end 3 (split "3,8"), 10 classes
-D = 8
+# name -> (ref_harness spec: model_name, model_type, start, end, classes; D; template model parts to write)
+CONFIGS = {
+    "c2": (["1", "1", "9", "3", "10"], 8, ["-1", "2"]),         # ResNet-18 split "3,8"
+    "c3": (["1", "4", "20", "10", "10"], 32, ["-1", "1", "2"]),  # ResNet-101 split "10,19"
+}
 
 
-def owners(blobs, mode, port_base, rounds, cwd, extra=()):
+def owners(spec, D, blobs, mode, port_base, rounds, cwd):
     return subprocess.run([bench.FAKE_OWNERS, "--blobs", blobs, "--parts", "1,2,3", "-d", str(D), "-c", "1",
-                           "--rounds", str(rounds), "--port-base", str(port_base), "--model-name", "1",
-                           "--model-type", "1", "--start", "9", "--end", "3", "--mode", mode,
-                           "--reply-timeout", "120", "--routing-table"] + list(extra),
-                          capture_output=True, text=True, timeout=900, cwd=cwd)
+                           "--rounds", str(rounds), "--port-base", str(port_base), "--model-name", spec[0],
+                           "--model-type", spec[1], "--start", spec[2], "--end", spec[3], "--mode", mode,
+                           "--reply-timeout", "300", "--routing-table"],
+                          capture_output=True, text=True, timeout=1500, cwd=cwd)
 
 
-def leg(name, agg_cmd, mode, port_base, rounds, blobs, startup_s):
+def leg(name, spec, D, agg_cmd, mode, port_base, rounds, blobs, startup_s):
     with tempfile.TemporaryDirectory(prefix="fa_c2_") as tmp:
         agg = subprocess.Popen(agg_cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, cwd=tmp,
                                start_new_session=True)
@@ -48,7 +52,7 @@ def leg(name, agg_cmd, mode, port_base, rounds, blobs, startup_s):
             time.sleep(startup_s)
             if agg.poll() is not None:
                 raise RuntimeError("%s exited early (rc %s)" % (name, agg.returncode))
-            r = owners(blobs, mode, port_base, rounds, tmp)
+            r = owners(spec, D, blobs, mode, port_base, rounds, tmp)
         finally:
             if agg.poll() is None:
                 try:
@@ -64,23 +68,26 @@ def leg(name, agg_cmd, mode, port_base, rounds, blobs, startup_s):
 
 
 def main():
-    ref_rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
-    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 10
-    with tempfile.TemporaryDirectory(prefix="fa_c2_blobs_") as blobs:
-        for mp in ("-1", "2"):  # the small buckets' templates, then the 9.4 M one
-            subprocess.run([HARNESS, "golden"] + SPEC + [str(D), "24301", "7", blobs, mp], check=True,
-                           capture_output=True, timeout=600)
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
+    ref_rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 10
+    spec, D, mps = CONFIGS[cfg]
+    with tempfile.TemporaryDirectory(prefix="fa_%s_blobs_" % cfg) as blobs:
+        for mp in mps:  # the small buckets' templates (-1), then the large ones one by one
+            subprocess.run([HARNESS, "golden"] + spec + [str(D), "24301", "7", blobs, mp], check=True,
+                           capture_output=True, timeout=1200)
         if bench.ports_free(bench.REF_PORTS):
-            print(json.dumps(dict(leg("reference_process_cpu", [bench.REF_CPU_AGGREGATOR, str(D), "1"], "literal",
-                                      8079, ref_rounds + 1, blobs, 2.5),
+            print(json.dumps(dict(leg("reference_process_cpu", spec, D, [bench.REF_CPU_AGGREGATOR, str(D), "1"],
+                                      "literal", 8079, ref_rounds + 1, blobs, 2.5), config=cfg,
                                   path="oracle/_ref/ref_cpu_aggregator: the reference's systemAPI / network_layer / "
                                        "torch::load / torch::save, aggregator.cpp:55-167 restated on CPU libtorch")),
                   flush=True)
         for mode in ("literal", "fedavg"):
             base = bench.free_port_base()
-            print(json.dumps(leg("fa_aggregator", [bench.FA_AGGREGATOR, "-i", "-1", "-d", str(D), "-c", "1", "--mode",
-                                                   mode, "--rounds", str(rounds + 1), "--port-base", str(base)],
-                                 mode, base, rounds + 1, blobs, 0.5)), flush=True)
+            print(json.dumps(dict(leg("fa_aggregator", spec, D, [bench.FA_AGGREGATOR, "-i", "-1", "-d", str(D), "-c",
+                                                                 "1", "--mode", mode, "--rounds", str(rounds + 1),
+                                                                 "--port-base", str(base)],
+                                      mode, base, rounds + 1, blobs, 0.5), config=cfg)), flush=True)
 
 
 if __name__ == "__main__":
