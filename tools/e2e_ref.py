@@ -11,6 +11,7 @@ torch::save), so the reference process can torch::load them into its modules.  T
   * oracle/_ref/ref_cpu_aggregator 8 1 -- the reference's systemAPI / network_layer process on CPU libtorch,
     aggregator.cpp:55-167 restated (literal mode: the owners send in turn, as its result depends on order);
   * bin/fa_aggregator -d 8 in literal mode (the same exchange) and in FedAvg mode (owners at once).
+  * oracle/_ref/ref_aggregator -- the same process with the INTEGRATION.md 2 binding on libfa (FedAvg).
 The owners send the routing table in the refactor message (--routing-table): the reference cannot reach an
 owner id above 3 without it.  One JSON line per leg.
 """
@@ -36,15 +37,15 @@ CONFIGS = {
 }
 
 
-def owners(spec, D, blobs, mode, port_base, rounds, cwd):
+def owners(spec, D, blobs, mode, port_base, rounds, cwd, extra=()):
     return subprocess.run([bench.FAKE_OWNERS, "--blobs", blobs, "--parts", "1,2,3", "-d", str(D), "-c", "1",
                            "--rounds", str(rounds), "--port-base", str(port_base), "--model-name", spec[0],
                            "--model-type", spec[1], "--start", spec[2], "--end", spec[3], "--mode", mode,
-                           "--reply-timeout", "300", "--routing-table"],
+                           "--reply-timeout", "300", "--routing-table"] + list(extra),
                           capture_output=True, text=True, timeout=1500, cwd=cwd)
 
 
-def leg(name, spec, D, agg_cmd, mode, port_base, rounds, blobs, startup_s):
+def leg(name, spec, D, agg_cmd, mode, port_base, rounds, blobs, startup_s, extra=()):
     with tempfile.TemporaryDirectory(prefix="fa_c2_") as tmp:
         agg = subprocess.Popen(agg_cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, cwd=tmp,
                                start_new_session=True)
@@ -52,7 +53,7 @@ def leg(name, spec, D, agg_cmd, mode, port_base, rounds, blobs, startup_s):
             time.sleep(startup_s)
             if agg.poll() is not None:
                 raise RuntimeError("%s exited early (rc %s)" % (name, agg.returncode))
-            r = owners(spec, D, blobs, mode, port_base, rounds, tmp)
+            r = owners(spec, D, blobs, mode, port_base, rounds, tmp, extra)
         finally:
             if agg.poll() is None:
                 try:
@@ -82,6 +83,13 @@ def main():
                                   path="oracle/_ref/ref_cpu_aggregator: the reference's systemAPI / network_layer / "
                                        "torch::load / torch::save, aggregator.cpp:55-167 restated on CPU libtorch")),
                   flush=True)
+        if os.access(bench.REF_BINDING_AGGREGATOR, os.X_OK) and bench.ports_free(bench.REF_PORTS):
+            print(json.dumps(dict(leg("reference_process_with_binding", spec, D,
+                                      [bench.REF_BINDING_AGGREGATOR, str(D), "1"], "fedavg", 8079, ref_rounds + 1,
+                                      blobs, 2.5, ["--sequential"]), config=cfg,
+                                  path="oracle/_ref/ref_aggregator: the reference's process with aggregator.cpp:55-167 "
+                                       "replaced by the INTEGRATION.md 2 binding on libfa (torch::load / torch::save "
+                                       "stay)")), flush=True)
         for mode in ("literal", "fedavg"):
             base = bench.free_port_base()
             print(json.dumps(dict(leg("fa_aggregator", spec, D, [bench.FA_AGGREGATOR, "-i", "-1", "-d", str(D), "-c",
