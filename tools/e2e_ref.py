@@ -46,9 +46,9 @@ def owners(spec, D, blobs, mode, port_base, rounds, cwd, extra=()):
 
 
 def leg(name, spec, D, agg_cmd, mode, port_base, rounds, blobs, startup_s, extra=()):
-    with tempfile.TemporaryDirectory(prefix="fa_c2_") as tmp:
-        agg = subprocess.Popen(agg_cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, cwd=tmp,
-                               start_new_session=True)
+    with tempfile.TemporaryDirectory(prefix="fa_e2e_") as tmp:
+        agg_out = open(os.path.join(tmp, "agg.out"), "w+")
+        agg = subprocess.Popen(agg_cmd, stdout=agg_out, stderr=subprocess.DEVNULL, cwd=tmp, start_new_session=True)
         try:
             time.sleep(startup_s)
             if agg.poll() is not None:
@@ -61,9 +61,18 @@ def leg(name, spec, D, agg_cmd, mode, port_base, rounds, blobs, startup_s, extra
                 except subprocess.TimeoutExpired:
                     os.killpg(agg.pid, signal.SIGKILL)  # the reference's loop never returns
                     agg.wait()
+        agg_out.seek(0)
+        lines = [json.loads(l) for l in agg_out.read().splitlines() if l.startswith("{")]  # fa_aggregator's
+        agg_out.close()
     res = json.loads(r.stdout.strip().splitlines()[-1])
     ms = res["round_ms"][1:]
-    return {"leg": name, "mode": mode, "ok": res["ok"], "rounds_timed": len(ms),
+    view = None
+    if len(lines) > 1:  # medians over rounds 1.. of the aggregator's own phase times
+        med = lambda f: round(statistics.median(f(p) for p in lines[1:]) * 1e3, 3)  # noqa: E731
+        view = {k: med(lambda p, k=k: p[k.split(".")[0]][k.split(".")[1]])
+                for k in ("phase1.receive_s", "phase1.absorb_s", "phase1.reduce_s", "phase2.receive_s",
+                          "phase2.absorb_s", "phase2.reduce_s", "phase2.send_s")}
+    return {"leg": name, "mode": mode, "ok": res["ok"], "rounds_timed": len(ms), "aggregator_view_ms": view,
             "round_ms_median": round(statistics.median(ms), 3), "round_ms_min": min(ms),
             "round0_ms": res["round_ms"][0], "checked_elems": res["checked_elems"]}
 
@@ -77,13 +86,14 @@ def main():
         for mp in mps:  # the small buckets' templates (-1), then the large ones one by one
             subprocess.run([HARNESS, "golden"] + spec + [str(D), "24301", "7", blobs, mp], check=True,
                            capture_output=True, timeout=1200)
-        if bench.ports_free(bench.REF_PORTS):
+        only_fa = os.environ.get("E2E_ONLY_FA") == "1"  # the drop-in's legs alone
+        if not only_fa and bench.ports_free(bench.REF_PORTS):
             print(json.dumps(dict(leg("reference_process_cpu", spec, D, [bench.REF_CPU_AGGREGATOR, str(D), "1"],
                                       "literal", 8079, ref_rounds + 1, blobs, 2.5), config=cfg,
                                   path="oracle/_ref/ref_cpu_aggregator: the reference's systemAPI / network_layer / "
                                        "torch::load / torch::save, aggregator.cpp:55-167 restated on CPU libtorch")),
                   flush=True)
-        if os.access(bench.REF_BINDING_AGGREGATOR, os.X_OK) and bench.ports_free(bench.REF_PORTS):
+        if not only_fa and os.access(bench.REF_BINDING_AGGREGATOR, os.X_OK) and bench.ports_free(bench.REF_PORTS):
             print(json.dumps(dict(leg("reference_process_with_binding", spec, D,
                                       [bench.REF_BINDING_AGGREGATOR, str(D), "1"], "fedavg", 8079, ref_rounds + 1,
                                       blobs, 2.5, ["--sequential"]), config=cfg,
@@ -94,7 +104,8 @@ def main():
             base = bench.free_port_base()
             print(json.dumps(dict(leg("fa_aggregator", spec, D, [bench.FA_AGGREGATOR, "-i", "-1", "-d", str(D), "-c",
                                                                  "1", "--mode", mode, "--rounds", str(rounds + 1),
-                                                                 "--port-base", str(base)],
+                                                                 "--port-base", str(base)] +
+                                      os.environ.get("E2E_AGG_ARGS", "").split(),
                                       mode, base, rounds + 1, blobs, 0.5), config=cfg)), flush=True)
 
 
