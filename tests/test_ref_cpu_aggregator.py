@@ -90,7 +90,7 @@ def test_reference_cpu_process_serves_c2_eight_owners(tmp_path):
     every reply bit-exact.  tools/e2e_ref.py c2 times the same pairing against fa_aggregator."""
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
     for mp in ("-1", "2"):
-        subprocess.run([harness, "golden", "1", "1", "9", "3", "10", "8", "24301", "7", str(tmp_path), mp],
+        subprocess.run([harness, "golden", "1", "1", "9", "3", "10", "1", "24301", "7", str(tmp_path), mp],
                        check=True, capture_output=True, timeout=600)
     if not ports_free():
         pytest.skip("the reference's fixed ports 8080-8083 are in use")

@@ -83,8 +83,9 @@ def main():
     rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 10
     spec, D, mps = CONFIGS[cfg]
     with tempfile.TemporaryDirectory(prefix="fa_%s_blobs_" % cfg) as blobs:
-        for mp in mps:  # the small buckets' templates (-1), then the large ones one by one
-            subprocess.run([HARNESS, "golden"] + spec + [str(D), "24301", "7", blobs, mp], check=True,
+        for mp in mps:  # the small buckets' templates (-1), then the large ones one by one; client 0's archive
+            # is the template whatever D is (the owners write their own values into it), so D = 1 here
+            subprocess.run([HARNESS, "golden"] + spec + ["1", "24301", "7", blobs, mp], check=True,
                            capture_output=True, timeout=1200)
         only_fa = os.environ.get("E2E_ONLY_FA") == "1"  # the drop-in's legs alone
         if not only_fa and bench.ports_free(bench.REF_PORTS):
