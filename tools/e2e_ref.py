@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A BASELINE config end to end: the reference's own aggregator process against the drop-in, same receipts.
 
-  python tools/e2e_ref.py [c2|c3] [ref_rounds=3] [rounds=10]     (GPU box)
+  python tools/e2e_ref.py [c2|c3|c4] [ref_rounds=3] [rounds=10]     (GPU box)
 
 C2 is ResNet-18 split "3,8" with 8 data owners (buckets 83 584 / 9 442 304 / 5 130), C3 ResNet-101 split
 "10,19" with 32 (2 594 688 / 29 511 680 / 5 130), both fp32 here: the reference has no bf16 path.  The
@@ -34,7 +34,12 @@ HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
 CONFIGS = {
     "c2": (["1", "1", "9", "3", "10"], 8, ["-1", "2"]),         # ResNet-18 split "3,8"
     "c3": (["1", "4", "20", "10", "10"], 32, ["-1", "1", "2"]),  # ResNet-101 split "10,19"
+    "c4": (["0", "6", "20", "3", "10"], 64, ["-1", "2", "3"]),    # VGG-19 split "3,19"
 }
+# The reference process holds ~3x a phase's receipts (C2: 0.94 GB peak RSS for 302 MB) and queues its
+# replies: its address space is capped so that C4 (30.6 GB of FC receipts per phase) fails by itself
+# rather than crowd the host.
+REF_AS_LIMIT = 160 << 30
 
 
 def owners(spec, D, blobs, mode, port_base, rounds, cwd, extra=()):
@@ -45,10 +50,16 @@ def owners(spec, D, blobs, mode, port_base, rounds, cwd, extra=()):
                           capture_output=True, text=True, timeout=1500, cwd=cwd)
 
 
-def leg(name, spec, D, agg_cmd, mode, port_base, rounds, blobs, startup_s, extra=()):
+def cap_address_space():
+    import resource
+    resource.setrlimit(resource.RLIMIT_AS, (REF_AS_LIMIT, REF_AS_LIMIT))
+
+
+def leg(name, spec, D, agg_cmd, mode, port_base, rounds, blobs, startup_s, extra=(), cap=False):
     with tempfile.TemporaryDirectory(prefix="fa_e2e_") as tmp:
         agg_out = open(os.path.join(tmp, "agg.out"), "w+")
-        agg = subprocess.Popen(agg_cmd, stdout=agg_out, stderr=subprocess.DEVNULL, cwd=tmp, start_new_session=True)
+        agg = subprocess.Popen(agg_cmd, stdout=agg_out, stderr=subprocess.DEVNULL, cwd=tmp, start_new_session=True,
+                               preexec_fn=cap_address_space if cap else None)
         try:
             time.sleep(startup_s)
             if agg.poll() is not None:
@@ -90,14 +101,16 @@ def main():
         only_fa = os.environ.get("E2E_ONLY_FA") == "1"  # the drop-in's legs alone
         if not only_fa and bench.ports_free(bench.REF_PORTS):
             print(json.dumps(dict(leg("reference_process_cpu", spec, D, [bench.REF_CPU_AGGREGATOR, str(D), "1"],
-                                      "literal", 8079, ref_rounds + 1, blobs, 2.5), config=cfg,
+                                      "literal", 8079, ref_rounds + 1, blobs, 2.5, cap=True), config=cfg,
                                   path="oracle/_ref/ref_cpu_aggregator: the reference's systemAPI / network_layer / "
                                        "torch::load / torch::save, aggregator.cpp:55-167 restated on CPU libtorch")),
                   flush=True)
-        if not only_fa and os.access(bench.REF_BINDING_AGGREGATOR, os.X_OK) and bench.ports_free(bench.REF_PORTS):
+        binding = os.environ.get("E2E_NO_BINDING") != "1"
+        if not only_fa and binding and os.access(bench.REF_BINDING_AGGREGATOR, os.X_OK) and \
+                bench.ports_free(bench.REF_PORTS):
             print(json.dumps(dict(leg("reference_process_with_binding", spec, D,
                                       [bench.REF_BINDING_AGGREGATOR, str(D), "1"], "fedavg", 8079, ref_rounds + 1,
-                                      blobs, 2.5, ["--sequential"]), config=cfg,
+                                      blobs, 2.5, ["--sequential"], cap=True), config=cfg,
                                   path="oracle/_ref/ref_aggregator: the reference's process with aggregator.cpp:55-167 "
                                        "replaced by the INTEGRATION.md 2 binding on libfa (torch::load / torch::save "
                                        "stay)")), flush=True)
