@@ -389,6 +389,10 @@ int main(int argc, char** argv) {
                 prev_frames[kv.first][retransmit_late] = kv.second[retransmit_late];
             }
         round_ms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+        // every destination of a bucket gets the same reply: the oracle's result (and, with --rel-tol, the
+        // bound's sum_k |w_k x_k|) is computed once per bucket and round, not once per reply
+        std::map<int, std::vector<uint8_t>> want_of;
+        std::map<int, std::vector<double>> sabs_of;
         for (auto& r : replies) {
             const Part* p = nullptr;
             for (auto& q : parts)
@@ -401,35 +405,43 @@ int main(int argc, char** argv) {
                 continue;
             }
             const size_t es = (size_t)p->es;
-            std::vector<uint8_t> got(p->n * es), want(p->n * es);
+            std::vector<uint8_t> got(p->n * es);
             if (ar.param_elem_size() != p->es || !ar.gather_param_bytes(got.data(), &err)) {
                 std::cerr << "reply for part " << p->mp << " changed dtype: " << err << "\n";
                 ok = false;
                 continue;
             }
             const auto& xs = values[p->mp];
-            if (mode == "literal") {
-                if (es == 4) fa_oracle_literal_f32((const float*)xs[D - 1].data(), p->n, divisor, (float*)want.data());
-                else fa_oracle_literal_bf16((const uint16_t*)xs[D - 1].data(), p->n, divisor, want.data(), 1);
-            } else if (es == 4) {
-                std::vector<const float*> ptrs;
-                for (auto& x : xs) ptrs.push_back((const float*)x.data());
-                fa_oracle_fedavg_f32(ptrs.data(), w.data(), D, p->n, nullptr, (float*)want.data(), threads);
-            } else {  // bf16 buckets: the fp32 chain, rounded once to bf16 (RNE)
-                std::vector<const uint16_t*> ptrs;
-                for (auto& x : xs) ptrs.push_back((const uint16_t*)x.data());
-                fa_oracle_fedavg_bf16(ptrs.data(), w.data(), D, p->n, nullptr, want.data(), 1, threads);
+            std::vector<uint8_t>& want = want_of[p->mp];
+            if (want.empty()) {
+                want.resize(p->n * es);
+                if (mode == "literal") {
+                    if (es == 4) fa_oracle_literal_f32((const float*)xs[D - 1].data(), p->n, divisor, (float*)want.data());
+                    else fa_oracle_literal_bf16((const uint16_t*)xs[D - 1].data(), p->n, divisor, want.data(), 1);
+                } else if (es == 4) {
+                    std::vector<const float*> ptrs;
+                    for (auto& x : xs) ptrs.push_back((const float*)x.data());
+                    fa_oracle_fedavg_f32(ptrs.data(), w.data(), D, p->n, nullptr, (float*)want.data(), threads);
+                } else {  // bf16 buckets: the fp32 chain, rounded once to bf16 (RNE)
+                    std::vector<const uint16_t*> ptrs;
+                    for (auto& x : xs) ptrs.push_back((const uint16_t*)x.data());
+                    fa_oracle_fedavg_bf16(ptrs.data(), w.data(), D, p->n, nullptr, want.data(), 1, threads);
+                }
             }
             if (rel_tol > 0 && es == 4 && mode != "literal") {
                 // the client-sharded layout sums in the exchange's order: |got - want| <= tol * sum_k |w_k x_k|
                 const float* g = (const float*)got.data();
                 const float* h = (const float*)want.data();
+                std::vector<double>& sabs = sabs_of[p->mp];
+                if (sabs.empty()) {
+                    sabs.assign(p->n, 0.0);
+                    for (size_t i = 0; i < p->n; ++i)
+                        for (int k = 0; k < D; ++k) sabs[i] += std::fabs((double)w[k] * ((const float*)xs[k].data())[i]);
+                }
                 size_t bad = 0;
                 double worst = 0;
                 for (size_t i = 0; i < p->n; ++i) {
-                    double sabs = 0;
-                    for (int k = 0; k < D; ++k) sabs += std::fabs((double)w[k] * ((const float*)xs[k].data())[i]);
-                    const double r = std::fabs((double)g[i] - (double)h[i]) / (rel_tol * sabs + 1e-30);
+                    const double r = std::fabs((double)g[i] - (double)h[i]) / (rel_tol * sabs[i] + 1e-30);
                     if (!(r <= 1.0)) ++bad;
                     if (r > worst) worst = r;
                 }
