@@ -47,8 +47,11 @@ def built():
     assert os.access(AGG, os.X_OK), "build the package first (make -C %s)" % PKG_DIR
 
 
-@pytest.mark.parametrize("mode,D,rounds", [("fedavg", 2, 3), ("literal", 2, 2), ("fedavg", 5, 2)])
-def test_lenet_rounds_over_tcp(torch_gpu, mode, D, rounds):
+@pytest.mark.parametrize("mode,D,rounds,table", [("fedavg", 2, 3, False), ("literal", 2, 2, False),
+                                                  ("fedavg", 5, 2, False), ("fedavg", 21, 2, True)])
+def test_lenet_rounds_over_tcp(torch_gpu, mode, D, rounds, table):
+    """table: the refactor message carries the owners' addresses (read_table 1, owner ids 4..21: both of the
+    reference's port ranges, network_layer.cpp:510-534), as the reference's init node sends it."""
     base = pick_base()
     agg = subprocess.Popen([AGG, "-i", "-1", "-d", str(D), "-c", "1", "--mode", mode, "--rounds", str(rounds),
                             "--port-base", str(base)], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
@@ -56,7 +59,7 @@ def test_lenet_rounds_over_tcp(torch_gpu, mode, D, rounds):
         time.sleep(0.5)
         r = subprocess.run([OWNERS, "--blobs", os.path.join(GOLDEN, "lenet5_c1"), "--parts", "1,2,3", "-d", str(D),
                             "-c", "1", "--rounds", str(rounds), "--mode", mode, "--port-base", str(base),
-                            "--model-name", "2", "--start", "6", "--end", "1"],
+                            "--model-name", "2", "--start", "6", "--end", "1"] + (["--routing-table"] if table else []),
                            capture_output=True, text=True, timeout=240)
         assert r.returncode == 0, r.stderr[-2000:]
         res = json.loads(r.stdout.strip().splitlines()[-1])
