@@ -3,7 +3,7 @@
 # Every GPU step has its own time limit; a crash, abort or timeout (exit code
 # other than 0, or 1 = "tests failed") ends the session so nothing else runs on
 # a possibly faulted GPU.  Output lands in gpurun_out/<tag>/.
-#   tools/gpu_session.sh <tag> [steps...]   steps: test smoke bench prof pmc
+#   tools/gpu_session.sh <tag> [steps...]   steps: test smoke bench prof pmc e2e_c4 e2e_ref ...
 set -u
 TAG=${1:-r01}
 shift || true
@@ -95,6 +95,11 @@ for s in $STEPS; do
         for L in "" "--eager" "--layout rs"; do
             E2E_NO_REF=1 timeout -k 10 600 python tools/e2e_bench.py 64 3 $L >> "$OUT/e2e_c4.jsonl" 2>> "$OUT/e2e_c4.err"
             rc=$?; tail -c 600 "$OUT/e2e_c4.jsonl"; echo; ok_or_fail $rc "e2e_c4 $L"
+        done ;;
+    e2e_ref)  # C2 and C3 through the reference's own process and through fa_aggregator, same receipts
+        for C in c2 c3; do
+            timeout -k 10 900 python -u tools/e2e_ref.py $C 2 5 >> "$OUT/e2e_ref.jsonl" 2>> "$OUT/e2e_ref.err"
+            rc=$?; tail -c 600 "$OUT/e2e_ref.jsonl"; echo; ok_or_fail $rc "e2e_ref $C"
         done ;;
     probe)
         hipcc --offload-arch=gfx950 -O3 tools/hbm_probe.hip -o "$OUT/hbm_probe" > "$OUT/probe_build.log" 2>&1 &&
