@@ -97,10 +97,15 @@ for s in $STEPS; do
             rc=$?; tail -c 600 "$OUT/e2e_c4.jsonl"; echo; ok_or_fail $rc "e2e_c4 $L"
         done ;;
     e2e_ref)  # C2 and C3 through the reference's own process and through fa_aggregator, same receipts
+        (while true; do date >> "$OUT/heartbeat"; sleep 45; done) &  # a reference leg is silent for minutes
+        HB=$!
         for C in c2 c3; do
             timeout -k 10 900 python -u tools/e2e_ref.py $C 2 5 >> "$OUT/e2e_ref.jsonl" 2>> "$OUT/e2e_ref.err"
-            rc=$?; tail -c 600 "$OUT/e2e_ref.jsonl"; echo; ok_or_fail $rc "e2e_ref $C"
-        done ;;
+            rc=$?; tail -c 600 "$OUT/e2e_ref.jsonl"; echo
+            [ "$rc" -ne 0 ] && kill $HB
+            ok_or_fail $rc "e2e_ref $C"
+        done
+        kill $HB ;;
     probe)
         hipcc --offload-arch=gfx950 -O3 tools/hbm_probe.hip -o "$OUT/hbm_probe" > "$OUT/probe_build.log" 2>&1 &&
         timeout -k 10 300 "$OUT/hbm_probe" > "$OUT/hbm_probe.json" 2> "$OUT/probe.err"
