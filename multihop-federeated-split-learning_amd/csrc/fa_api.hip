@@ -122,6 +122,19 @@ constexpr int kSegRing = 4;                // device segment tables per GPU (Gpu
 // in at most kHostReadPieces launches (the pieces on which every receipt and the destination are contiguous)
 constexpr size_t kHostReadMax = FA_HOST_READ_MAX_BYTES;
 constexpr int kHostReadPieces = 16;
+// Experiment knobs (tools/): FA_HOST_READ_MAX / FA_HOST_READ_PIECES override the two limits above.
+size_t env_size(const char* name, size_t dflt) {
+    const char* e = std::getenv(name);
+    return e ? (size_t)std::strtoull(e, nullptr, 0) : dflt;
+}
+size_t host_read_max() {
+    static const size_t v = env_size("FA_HOST_READ_MAX", kHostReadMax);
+    return v;
+}
+size_t host_read_pieces() {
+    static const size_t v = env_size("FA_HOST_READ_PIECES", (size_t)kHostReadPieces);
+    return v;
+}
 constexpr int kNotHostReadable = 1;  // host_reduce: the path does not apply (nothing was launched)
 
 // Host memcpy into / out of the pinned staging chunks, split over worker threads:
@@ -743,13 +756,13 @@ const char* device_visible(const void* ptr) {
 
 bool host_read_part(const fa_ctx* ctx, const Part& p) {
     return host_read_enabled() && ctx->G == 1 && !p.rs && !(ctx->flags & FA_ACCUMULATE_ON_ARRIVAL) &&
-           p.npiece[0] == 1 && p.n > 0 && (size_t)p.D * p.n * dsize(p.in) <= kHostReadMax;
+           p.npiece[0] == 1 && p.n > 0 && (size_t)p.D * p.n * dsize(p.in) <= host_read_max();
 }
 
 // Keeps a pinned receipt of slot `slot` where it is, if the part and every segment allow it (element-aligned,
 // device-visible); false = submit it the plain way.
 bool host_keep(fa_ctx* ctx, Part& p, int slot, const Gather& src) {
-    if (!host_read_part(ctx, p) || src.n > 4 * kHostReadPieces) return false;
+    if (!host_read_part(ctx, p) || (size_t)src.n > 4 * host_read_pieces()) return false;
     const size_t si = dsize(p.in);
     std::vector<Part::HostSeg> segs;
     DeviceGuard dg(ctx->gpu[0].dev);
@@ -826,7 +839,7 @@ int host_reduce(fa_ctx* ctx, Part& p, const float* w, hipStream_t s, const Gathe
     std::sort(cuts.begin(), cuts.end());
     cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
     while (!cuts.empty() && cuts.back() > p.n) cuts.pop_back();
-    if (cuts.size() - 1 > (size_t)kHostReadPieces) return kNotHostReadable;
+    if (cuts.size() - 1 > host_read_pieces()) return kNotHostReadable;
     // element e of a segment list (si bytes per element) -> its device-visible address
     auto at = [](const std::vector<Part::HostSeg>& segs, size_t e, size_t es) -> const char* {
         size_t b = e * es;

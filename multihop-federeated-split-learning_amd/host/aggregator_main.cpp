@@ -363,10 +363,14 @@ public:
         if (o_.eager || mps.size() < 2) return;
         // small parts whose receipts the library reads in place (FA_HOST_READ_MAX_BYTES): each finalize then
         // reduces straight into its reply, one round trip per part instead of a launch here and a copy there
+        static const size_t host_read_max = [] {  // FA_HOST_READ_MAX: the library's experiment knob
+            const char* e = std::getenv("FA_HOST_READ_MAX");
+            return e ? (size_t)std::strtoull(e, nullptr, 0) : (size_t)FA_HOST_READ_MAX_BYTES;
+        }();
         if (o_.gpus == 1 && !o_.rs && o_.pinned &&
             std::all_of(mps.begin(), mps.end(), [&](int mp) {
                 const Bucket& b = buckets_[mp];
-                return (size_t)o_.data_owners * b.numel * (size_t)b.elem <= FA_HOST_READ_MAX_BYTES;
+                return (size_t)o_.data_owners * b.numel * (size_t)b.elem <= host_read_max;
             }))
             return;
         const auto t0 = std::chrono::steady_clock::now();
