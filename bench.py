@@ -61,6 +61,7 @@ WORKLOADS = {
     "ns_w4": (32, 16 << 20, "f32", "f32", "north star, one rank's share at 4 GPUs (strong scaling): 32 x 64 MiB"),
     "ns_w8": (32, 8 << 20, "f32", "f32", "north star, one rank's share at 8 GPUs (strong scaling): 32 x 32 MiB"),
 }
+H2D_DISTINCT_MAX_BYTES = 16 << 30  # host-inclusive legs: one pinned buffer per client up to this many bytes
 ROTATE_MIN_BYTES = 1 << 30  # rotate input sets until a step's working set no longer fits the 256 MiB MALL
 T_START = time.monotonic()
 # Wall-clock budget of one bench run (the driver stops a bench at 600 s).  Every optional leg is bounded by
@@ -92,6 +93,54 @@ def cpu_threads():
     n = len(os.sched_getaffinity(0))
     cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     return max(1, min(n, cap) if cap > 0 else n)
+
+
+def pick_cores(n):
+    """`n` CPUs of this process's affinity mask, one per physical core where the topology says so (an SMT
+    sibling of a chosen CPU is taken only when the mask has no other core left)."""
+    mask = sorted(os.sched_getaffinity(0))
+    chosen, seen, spare = [], set(), []
+    for c in mask:
+        try:
+            with open("/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list" % c) as f:
+                core = f.read().strip()
+        except OSError:
+            core = str(c)
+        if core in seen:
+            spare.append(c)
+            continue
+        seen.add(core)
+        chosen.append(c)
+    return (chosen + spare)[:max(1, n)]
+
+
+def compact_cpus(cpus):
+    """[0,1,2,3,8] -> "0-3,8"."""
+    out, run = [], []
+    for c in sorted(cpus):
+        if run and c == run[-1] + 1:
+            run.append(c)
+            continue
+        if run:
+            out.append("%d-%d" % (run[0], run[-1]) if len(run) > 1 else str(run[0]))
+        run = [c]
+    if run:
+        out.append("%d-%d" % (run[0], run[-1]) if len(run) > 1 else str(run[0]))
+    return ",".join(out)
+
+
+def pinned_child(cores):
+    """subprocess kwargs that run a CPU leg on exactly `cores` with its OpenMP threads bound one per core."""
+    env = dict(os.environ, OMP_NUM_THREADS=str(len(cores)), OMP_PROC_BIND="close", OMP_PLACES="cores")
+    return {"env": env, "preexec_fn": lambda: os.sched_setaffinity(0, cores)}
+
+
+def spread(rep_s, bytes_per_rep):
+    """min / median / max GiB/s over the timed reps of one CPU leg."""
+    r = sorted(bytes_per_rep / t / 2**30 for t in rep_s if t > 0)
+    if not r:
+        return None
+    return {"min": round(r[0], 3), "median": round(statistics.median(r), 3), "max": round(r[-1], 3), "reps": len(r)}
 
 
 def host_cpu():
@@ -247,6 +296,7 @@ def cpu_c1(threads, cpu_model):
     return out
 
 
+CPU_REPS = 20  # timed reps of the main CPU leg (its min / median / max go in cpu_baseline.spread)
 CPU_MAX_SAMPLE_BYTES = 36 << 30  # host memory one CPU leg may fill (C4's whole config, 35.7 GB, fits)
 
 
@@ -264,6 +314,7 @@ def cpu_baseline(D, n, reps, dt="f32", skip=None):
     """
     threads = cpu_threads()
     cpu_model = host_cpu()
+    cores = pick_cores(threads)
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
     s = 4 if dt == "f32" else 2
     D0 = D
@@ -274,9 +325,10 @@ def cpu_baseline(D, n, reps, dt="f32", skip=None):
                           n * s / 2**20, D * n * s / 2**30, reps)
     bf = ["bf16"] if dt == "bf16" else []
 
-    def run(args, timeout=120):
+    def run(args, timeout=120, ncores=None):
+        use = cores if ncores is None else cores[:ncores]
         out = subprocess.run([harness] + [str(a) for a in args], capture_output=True, text=True, timeout=timeout,
-                             check=True).stdout
+                             check=True, **pinned_child(use)).stdout
         return json.loads(out.strip().splitlines()[-1])
 
     def leg_timeout(cap=90):
@@ -286,18 +338,20 @@ def cpu_baseline(D, n, reps, dt="f32", skip=None):
         return min(cap, left)
     if os.access(harness, os.X_OK):
         try:
-            r = run(["bench-fedavg", n, D, threads, reps] + bf)
-            res = {"value": round(r["gib_s"], 3), "unit": "GiB/s", "cores": threads, "kind": "reference",
+            r = run(["bench-fedavg", n, D, len(cores), reps] + bf)
+            res = {"value": round(r["gib_s"], 3), "unit": "GiB/s", "cores": len(cores), "kind": "reference",
                    "path": "restatement in the reference's library: libtorch acc.add_(x_k, w_k) chain, "
-                           "at::set_num_threads(%d)" % threads,
-                   "sample": sample, "host_cpu": cpu_model}
+                           "at::set_num_threads(%d)" % len(cores),
+                   "sample": sample, "host_cpu": cpu_model,
+                   "spread": spread(r.get("rep_s", []), D * n * s),
+                   "pinned": "cores %s, OMP_PROC_BIND=close" % compact_cpus(cores)}
         except Exception as e:  # noqa: BLE001 -- fall through to the port
             print("cpu baseline: ref_harness failed (%s), timing the oracle port" % e, file=sys.stderr)
             res = None
         if res is not None:
             per = {}
             try:
-                r1 = run(["bench-fedavg", n, D, 1, 2] + bf, timeout=leg_timeout(120))
+                r1 = run(["bench-fedavg", n, D, 1, 2] + bf, timeout=leg_timeout(120), ncores=1)
                 res["fedavg_1_core"] = {"value": round(r1["gib_s"], 3), "unit": "GiB/s", "cores": 1,
                                         "sample": "the whole workload, 2 timed reps"}
             except Exception as e:  # noqa: BLE001 -- optional figures
@@ -332,7 +386,7 @@ def cpu_baseline(D, n, reps, dt="f32", skip=None):
                         continue  # = per["round_c2"]
                     try:
                         lit = run(["bench-literal", 1, 1, 9, 3, 10, 8, t, 2] + ([mode] if mode else []),
-                                  timeout=leg_timeout(60))
+                                  timeout=leg_timeout(60), ncores=t)
                         k = "reference_receive_loop" + ("_arith_only" if mode else "") + ("_1_core" if t == 1 else "")
                         res[k] = {"value": round(lit["gib_s"], 3), "unit": "GiB/s of parameters received", "cores": t,
                                   "path": "the reference's receive loop (aggregator.cpp:59-93): " +
@@ -606,23 +660,15 @@ class Setup:
         self.nsets = max(1, -(-min_rotate_bytes // set_bytes))
         self.agg = fa.Aggregator(devices=[device])
         # contiguous: every client slot one range of device memory (the client-sharded legs hand raw slot
-        # addresses to fa_reduce_device), i.e. no range pieces (FA_PIECE_SPAN=0 while the parts are defined)
-        span0 = os.environ.get("FA_PIECE_SPAN")
+        # addresses to fa_reduce_device), i.e. no range pieces in this context
         if contiguous:
-            os.environ["FA_PIECE_SPAN"] = "0"
-        try:
-            for s in range(self.nsets):
-                self.agg.define(s, n, self.in_dt, self.out_dt, D, fa.FEDAVG if mode is None else mode)
-                for k in range(D):
-                    for ptr, cnt, off in self.agg.pieces(s, 0, k):
-                        # global client id and element offset: ranks hold disjoint clients or slices of one bucket
-                        fa.fill_uniform(ptr, cnt, self.in_dt, seed + s, client0 + k, idx0=elem0 + off)
-        finally:
-            if contiguous:
-                if span0 is None:
-                    os.environ.pop("FA_PIECE_SPAN", None)
-                else:
-                    os.environ["FA_PIECE_SPAN"] = span0
+            self.agg.set_tuning(piece_span_kib=-1)
+        for s in range(self.nsets):
+            self.agg.define(s, n, self.in_dt, self.out_dt, D, fa.FEDAVG if mode is None else mode)
+            for k in range(D):
+                for ptr, cnt, off in self.agg.pieces(s, 0, k):
+                    # global client id and element offset: ranks hold disjoint clients or slices of one bucket
+                    fa.fill_uniform(ptr, cnt, self.in_dt, seed + s, client0 + k, idx0=elem0 + off)
         self.w = self._weights(D)
 
     @staticmethod
@@ -942,21 +988,141 @@ def layout_desc_of(layout, D, world, chunks):
             "next rank over RCCL p2p in %d chunks, last rank scatters the ranges" % (D, chunks))
 
 
+# ------------------------------------------------------------------ the printed line
+#
+# The driver parses ONE stdout line, and a line past ~16 KB was not parsed (BENCH_r05: 20.3 KB, parsed null).
+# stdout carries a compact line of at most LINE_MAX_BYTES: the required keys, roofline, cpu_baseline with its
+# spread, parity, and one small object per secondary leg.  The full object (every leg's detail) goes to
+# FULL_RECORD, which the compact line names.
+
+LINE_MAX_BYTES = 6000
+FULL_RECORD = os.environ.get("FA_BENCH_FULL") or os.path.join(ROOT, "gpurun_out", "bench_full.json")
+ROOFLINE_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "algorithmic_bytes_per_launch",
+                 "kernel_ms_avg", "kernel_ms_min", "kernel_ms_median", "kernel_ms_avg_max_over_ranks",
+                 "phased_meeting_timeouts", "read_stream_peak", "frac_of_read_stream",
+                 "read_stream_peak_independent", "frac_of_read_stream_independent")
+CPU_KEYS = ("value", "unit", "cores", "kind", "sample", "host_cpu", "spread", "pinned")
+CONFIG_KEYS = ("workload", "description", "clients", "elems_per_client", "in_dtype", "out_dtype", "parallelism",
+               "world_size", "dist_backend", "ranks_share_gpus", "input_sets_rotated")
+# a leg's figure -> its key in the compact line
+LEG_KEYS = (("gib_s", "gib_s"), ("frac", "frac"), ("kernel_ms_avg", "ms"), ("round_ms_avg", "ms"),
+            ("ms_per_round", "ms"), ("ms_per_step", "ms"), ("frac_of_read_stream_independent", "frac_ind"),
+            ("cpu_gib_s", "cpu_gib_s"), ("gpus", "gpus"), ("h2d_ms", "h2d_ms"), ("reduce_ms", "reduce_ms"),
+            ("d2h_ms", "d2h_ms"), ("pcie_GBs", "pcie_GBs"))
+E2E_KEYS = (("e2e_loopback_literal", "e2e_literal_ms"), ("e2e_loopback_fedavg", "e2e_fedavg_ms"),
+            ("e2e_loopback_reference_process_with_binding", "e2e_ref_binding_ms"), ("cpu_e2e_loopback", "cpu_e2e_ms"))
+
+
+def _parity_brief(p):
+    """{ok[, err_over_bound]} of a parity object (None when there is none)."""
+    if not isinstance(p, dict):
+        return None
+    out = {"ok": bool(p.get("ok"))}
+    if p.get("max_err_over_bound") is not None:
+        out["err_over_bound"] = round(p["max_err_over_bound"], 3)
+    return out
+
+
+def compact_leg(v):
+    """One secondary leg in a few figures: gib_s / frac / ms / frac_ind / cpu_gib_s, parity ok."""
+    if not isinstance(v, dict):
+        return v
+    if "error" in v:
+        return {"error": str(v["error"])[:80]}
+    if "skipped" in v:
+        return {"skipped": True}
+    out = {}
+    for src, dst in LEG_KEYS:
+        if v.get(src) is not None and dst not in out:
+            out[dst] = v[src]
+    if v.get("cpu_error"):
+        out["cpu_error"] = True
+    if v.get("shared_device_rehearsal"):
+        out["rehearsal"] = True
+    if v.get("phased_meeting_timeouts"):
+        out["meeting_timeouts"] = v["phased_meeting_timeouts"]
+    par = _parity_brief(v.get("parity"))
+    if par is not None:
+        out["parity_ok"] = par["ok"]
+        if "err_over_bound" in par:
+            out["err_over_bound"] = par["err_over_bound"]
+    for src, dst in E2E_KEYS:  # BASELINE C1's end-to-end rounds (owner view, medians)
+        e = v.get(src)
+        if isinstance(e, dict):
+            if "error" in e:
+                out[dst] = None
+            else:
+                out[dst] = e.get("round_ms_median")
+                p = e.get("parity")
+                out["e2e_parity_ok"] = out.get("e2e_parity_ok", True) and bool(p and p.get("ok"))
+    return out
+
+
+def compact_line(line, full_record=None):
+    """The stdout line from the full object: what the driver checks, in at most LINE_MAX_BYTES."""
+    out = {k: line[k] for k in line if k not in ("config", "roofline", "cpu_baseline", "parity", "secondary")}
+    cfg = line.get("config") or {}
+    out["config"] = {k: cfg[k] for k in CONFIG_KEYS if k in cfg}
+    rl = line.get("roofline") or {}
+    out["roofline"] = {k: rl[k] for k in ROOFLINE_KEYS if k in rl}
+    if rl.get("traffic_source"):
+        out["roofline"]["traffic_source"] = "live PMC" if str(rl["traffic_source"]).startswith("live") \
+            else "committed profile"
+    cpu = line.get("cpu_baseline")
+    if isinstance(cpu, dict):
+        out["cpu_baseline"] = {k: cpu[k] for k in CPU_KEYS if k in cpu}
+        if isinstance(cpu.get("fedavg_1_core"), dict):
+            out["cpu_baseline"]["value_1_core"] = cpu["fedavg_1_core"].get("value")
+    else:
+        out["cpu_baseline"] = cpu
+    par = line.get("parity")
+    if isinstance(par, dict):
+        out["parity"] = {k: par[k] for k in ("check", "samples", "mismatches", "max_abs_err", "max_err_over_bound",
+                                             "ranks", "ok", "error") if k in par}
+    else:
+        out["parity"] = par
+    if "secondary" in line:
+        out["secondary"] = {k: compact_leg(v) for k, v in (line["secondary"] or {}).items()}
+    if full_record:
+        out["full_record"] = full_record
+    s = json.dumps(out)
+    if len(s) > LINE_MAX_BYTES and "secondary" in out:  # never expected: keep the required part parseable
+        out["secondary"] = {k: (v.get("gib_s") if isinstance(v, dict) else v) for k, v in out["secondary"].items()}
+        out["secondary_truncated"] = True
+    return out
+
+
+def write_full_record(line, path=FULL_RECORD):
+    """The whole object (every leg's detail) beside the run; returns the path written, or None."""
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(line, f)
+            f.write("\n")
+        return os.path.relpath(path, ROOT)
+    except OSError as e:
+        print("bench: full record not written (%s)" % e, file=sys.stderr)
+        return None
+
+
 class LinePrinter:
     """Rank 0 prints the one JSON line exactly once (from the main thread or the watchdog), on the process's
     original stdout; everything else that writes to fd 1 (RCCL's version banner, library chatter) has been
-    moved to stderr by quiet_stdout(), so the driver's stdout carries that one line only."""
+    moved to stderr by quiet_stdout(), so the driver's stdout carries that one line only.  The line is the
+    compact form (compact_line); the full object goes to FULL_RECORD first."""
 
-    def __init__(self, rank, out=None):
+    def __init__(self, rank, out=None, full_path=FULL_RECORD):
         self.rank = rank
         self.out = out or sys.stdout
+        self.full_path = full_path
         self.lock = threading.Lock()
         self.done = False
 
     def emit(self, line):
         with self.lock:
             if self.rank == 0 and not self.done:
-                self.out.write(json.dumps(line) + "\n")
+                rec = write_full_record(line, self.full_path) if self.full_path else None
+                self.out.write(json.dumps(compact_line(line, rec)) + "\n")
                 self.out.flush()
             self.done = True
 
@@ -1034,6 +1200,9 @@ def main():
     ap.add_argument("--dist-backend", default="auto",
                     help="auto (nccl = RCCL over xGMI when every rank has its own GPU, else gloo), nccl or gloo")
     ap.add_argument("--tune", default="", help="block,max_blocks,unroll,load_policy,store_policy (fa_tuning)")
+    ap.add_argument("--piece-span-kib", type=int, default=0,
+                    help="fa_tuning.piece_span_kib for every context (range pieces; tests force small pieces)")
+    ap.add_argument("--piece-split-kib", type=int, default=0, help="fa_tuning.piece_split_kib (-1: always cut)")
     ap.add_argument("--ctx-multi", default="", choices=["", "range", "rs"],
                     help="one process over every visible GPU through the C ABI: FA_SHARD_RANGE or FA_SHARD_CLIENT_RS "
                          "(RCCL reduce-scatter); prints one JSON object (a secondary of the N = 1 run)")
@@ -1081,7 +1250,7 @@ def main():
 
     cpu, cpu_per = None, {}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu, cpu_per = cpu_baseline(D, n, 5, in_dt, skip=args.workload)
+        cpu, cpu_per = cpu_baseline(D, n, CPU_REPS, in_dt, skip=args.workload)
 
     import torch
     import torch.distributed as dist
@@ -1100,6 +1269,8 @@ def main():
     if args.tune:
         b, mb, u, lp, sp = [int(x) for x in args.tune.split(",")]
         fa.set_tuning(block=b, max_blocks=mb, unroll=u, load_policy=lp, store_policy=sp)
+    if args.piece_span_kib or args.piece_split_kib:
+        fa.set_tuning(piece_span_kib=args.piece_span_kib, piece_split_kib=args.piece_split_kib)
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
@@ -1334,10 +1505,13 @@ def ctx_multi(args):
     import numpy as np
     clients = None  # chain position k holds generator client k
     if args.h2d:
-        # client buckets in pinned host memory (8 distinct buffers, client k uses k % 8, so C5 stays at 8 GiB of
-        # host memory), submitted each round; the result lands in host memory.  Buffer i holds generator client
-        # i (filled on the device, copied once, outside the timed region), so the result can be checked.
-        hosts = [fa.PinnedBuffer(n * s_in) for _ in range(min(D, 8))]
+        # client buckets in pinned host memory, submitted each round (fa_submit_pinned); the result lands in a
+        # pinned host buffer (fa_finalize_gather, FA_HOST_PINNED).  One buffer per client while the round's
+        # receipts fit 16 GiB of host memory (the north star: 32 x 256 MiB), else 8 distinct buffers that client
+        # k takes k % 8 of (C5 stays at 8 GiB).  Buffer i holds generator client i (filled on the device, copied
+        # once, outside the timed region), so the result can be checked.
+        nbuf = D if D * n * s_in <= H2D_DISTINCT_MAX_BYTES else min(D, 8)
+        hosts = [fa.PinnedBuffer(n * s_in) for _ in range(nbuf)]
         tmp = torch.empty(n * s_in // 4, dtype=torch.float32, device="cuda:0")
         for i, h in enumerate(hosts):
             fa.fill_uniform(tmp, n, idt, 0x5EED, i)
@@ -1345,12 +1519,16 @@ def ctx_multi(args):
         del tmp
         torch.cuda.synchronize(0)
         clients = [k % len(hosts) for k in range(D)]
-        res = np.empty(n, np.float32)
+        res_buf = fa.PinnedBuffer(n * 4)
+        res = res_buf.view(np.float32, count=n)
 
-        def step():
+        def submit_all():
             for k in range(D):
                 agg.submit(1, k, hosts[k % len(hosts)].view(np.uint8), w[k], pinned=True)
-            agg.finalize(1, res)
+
+        def step():
+            submit_all()
+            agg.finalize_gather(1, [res], pinned=True)
     else:
         def step():
             agg.reduce(1, w)
@@ -1364,6 +1542,24 @@ def ctx_multi(args):
         step()
     agg.sync()
     dt = (time.perf_counter() - t0) / args.steps
+    split = None
+    if args.h2d:
+        # where a host-inclusive round goes, from one more round run phase by phase after the timed ones:
+        # every receipt's H2D (submits + fa_sync), the reduction alone (fa_reduce_parts + fa_sync), the D2H of
+        # the result into the pinned reply (fa_finalize_gather, which then only copies)
+        ta = time.perf_counter()
+        submit_all()
+        agg.sync()
+        tb = time.perf_counter()
+        agg.reduce_parts([1])
+        agg.sync()
+        tc = time.perf_counter()
+        agg.finalize_gather(1, [res], pinned=True)
+        td = time.perf_counter()
+        pcie = D * n * s_in + n * 4
+        split = {"h2d_ms": round((tb - ta) * 1e3, 3), "reduce_ms": round((tc - tb) * 1e3, 3),
+                 "d2h_ms": round((td - tc) * 1e3, 3), "pcie_bytes_per_round": pcie,
+                 "pcie_GBs": round(pcie / dt / 1e9, 2), "distinct_host_buffers": len(hosts)}
     # > 0: a phased launch's grid was not co-resident on some GPU (the rs layout never takes that kernel)
     timeouts = sum(fa.phased_timeouts(d) - t_before[d] for d in devs)
     tuning = agg.get_tuning()
@@ -1391,6 +1587,8 @@ def ctx_multi(args):
            "elems_per_client": n, "host_inclusive": args.h2d, "ms_per_round": round(dt * 1e3, 4),
            "gib_s": round(D * n * s_in / dt / 2**30, 1), "steps": args.steps,
            "phased_meeting_timeouts": timeouts, "parity": parity, "tuning": tuning}
+    if split:
+        out.update(split)
     agg.close()
     print(json.dumps(out), flush=True)
 
@@ -1404,20 +1602,25 @@ def ctx_multi_secondaries(n_dev, deadline, timeout=120):
     the layouts' code paths with the exchange replaced by its definition; a parity check, not a timing)."""
     # BASELINE C4 is quoted on 4 GPUs (RCCL reduce-scatter), C5 on 8 (128 x 1 GiB buckets arriving from host
     # memory, H2D overlapped over every GPU's link); the north star on all of them
+    # the north star host-inclusive on one GPU (pinned host -> GPU -> pinned host, every receipt's H2D in the
+    # round; network_layer.cpp:33-74 in, aggregator.cpp:96-106 out): reported as ns_h2d with its split
+    legs = [("range", "northstar", True, 1, 0, 0)]
     if n_dev >= 2:
-        legs = [("range", "northstar", False, n_dev, 0, 0), ("rs", "northstar", False, n_dev, 0, 0),
+        legs += [("range", "northstar", False, n_dev, 0, 0), ("rs", "northstar", False, n_dev, 0, 0),
                 ("rs", "c4", False, min(4, n_dev), 0, 0), ("rs", "c4", False, n_dev, 0, 0),
                 ("range", "c5", True, min(8, n_dev), 0, 0)]
         # the rs overlap depth on real xGMI (untuned so far: one-GPU boxes have no exchange to overlap): C4's
         # 4-GPU reduce-scatter at other piece counts than the default, last, so the budget drops them first
         legs += [("rs", "c4", False, min(4, n_dev), 0, c) for c in RS_CHUNK_SWEEP]
     else:  # C5's per-GPU share (c5r) keeps the host-inclusive rehearsal at 16 GiB of input per round
-        legs = [("rs", "c4", False, 8, 8, 0), ("range", "c5r", True, 8, 8, 0)]
+        legs += [("rs", "c4", False, 8, 8, 0), ("range", "c5r", True, 8, 8, 0)]
     res = {}
     for layout, workload, h2d, gpus, shared, chunks in legs:
         key = "ctx_%s_%s%s_%d%s%s" % (layout, workload, "_h2d" if h2d else "", gpus,
                                      "shard_rehearsal_on_one_gpu" if shared else "gpu",
                                      "_rschunks%d" % chunks if chunks else "")
+        if (layout, workload, h2d, gpus, shared) == ("range", "northstar", True, 1, 0):
+            key = "ns_h2d"
         if key in res:
             continue
         left = deadline - time.monotonic() - 30  # deadline = T_START + BUDGET_S

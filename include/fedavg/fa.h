@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FA_ABI_VERSION 6
+#define FA_ABI_VERSION 7
 
 typedef struct fa_ctx fa_ctx; /* opaque: device slots, streams, pinned staging */
 
@@ -113,8 +113,10 @@ int fa_submit(fa_ctx* ctx, int part_id, int client_slot, const void* host_src, f
  * bits.  Calls before it that need the device slots (fa_reduce_part(s),
  * fa_sync_part, fa_bucket_slot/_piece, a pageable submit to the part) copy the
  * kept receipts in first.  A finalize that wrote a pinned destination this way
- * leaves the part's device output (fa_bucket_output) as it was.  FA_HOST_READ=0
- * in the environment turns this off. */
+ * leaves the part's device output (fa_bucket_output) as it was, and
+ * fa_copy_output of the part then fails with FA_ERR_STATE until its next
+ * reduction.  fa_bucket_host_read tells whether a part's round is being kept
+ * this way.  FA_HOST_READ=0 in the environment turns this off. */
 #define FA_HOST_READ_MAX_BYTES (1u << 20)
 int fa_submit_pinned(fa_ctx* ctx, int part_id, int client_slot, const void* host_src, float weight);
 
@@ -162,8 +164,8 @@ int fa_reduce_part(fa_ctx* ctx, int part_id, const float* h_weights, void* hip_s
 int fa_bucket_slot(fa_ctx* ctx, int part_id, int gpu, int client_slot, void** d_ptr, size_t* n_elems,
                    size_t* elem_offset);
 /* Range layout: a GPU whose client slots would span more than 48 GiB holds them as pieces of <= 16 GiB of
- * slots each (FA_PIECE_SPAN / FA_PIECE_SPLIT override at fa_bucket_define), reduced one launch
- * per piece.  fa_bucket_slot then fails (FA_ERR_STATE); a slot is written piece by piece instead.
+ * slots each (fa_tuning.piece_span_kib / piece_split_kib, taken at fa_bucket_define), reduced
+ * one launch per piece.  fa_bucket_slot then fails (FA_ERR_STATE); a slot is written piece by piece instead.
  * n_pieces: 1 for every other part. */
 int fa_bucket_pieces(fa_ctx* ctx, int part_id, int gpu, int* n_pieces);
 /* Piece `piece` of client slot `client_slot` on GPU `gpu`: n_elems elements of the input dtype covering
@@ -176,6 +178,10 @@ int fa_bucket_output(fa_ctx* ctx, int part_id, int gpu, void** d_ptr);
 /* This round's receipts so far and how many leading client slots are already reduced
  * (FA_ACCUMULATE_ON_ARRIVAL; n_reduced == D once the round's result is ready). */
 int fa_bucket_progress(fa_ctx* ctx, int part_id, int* n_submitted, int* n_reduced);
+/* Whether the part's round so far is kept host-side to be read in place (fa_submit_pinned, small receipts):
+ * *kept = 1 when every receipt its reduction reads is held that way, so the fa_finalize* ending the round
+ * reduces them itself (a caller then skips fa_reduce_parts for it, which would copy them in first); else 0. */
+int fa_bucket_host_read(fa_ctx* ctx, int part_id, int* kept);
 /* Batched device-resident reduction of several parts (e.g. all last-part layers of a phase,
  * aggregator.cpp:108-150): one launch per GPU covers every part that is FedAvg, range-laid-out, has at
  * most 128 clients and is below the phased kernel's size (a segment table: one bucket per segment,
@@ -183,7 +189,9 @@ int fa_bucket_progress(fa_ctx* ctx, int part_id, int* n_submitted, int* n_reduce
  * entry per part (NULL entry = the weights given to fa_submit).  A following fa_finalize* of these
  * parts only copies the result out.  Async on hip_stream (NULL = ctx compute streams). */
 int fa_reduce_parts(fa_ctx* ctx, int n_parts, const int* part_ids, const float* const* h_weights, void* hip_stream);
-/* D2H of the part's current device output (after fa_reduce_part), waiting for it. */
+/* D2H of the part's current device output (after fa_reduce_part), waiting for it.  FA_ERR_STATE when the
+ * part has no device output: never reduced, or its last round was read in place straight into a pinned
+ * reply (fa_submit_pinned). */
 int fa_copy_output(fa_ctx* ctx, int part_id, void* host_dst);
 /* Wait for all copy and compute work of the ctx. */
 int fa_sync(fa_ctx* ctx);
@@ -259,6 +267,8 @@ typedef struct {
                          kernels always use nt loads and sc1 stores.  With walk 5, a bucket below one
                          phase with >= 16 clients takes one phase sized to it */
     int rs_chunks;    /* FA_SHARD_CLIENT_RS: pieces per round (default 8) */
+    int piece_span_kib;  /* range pieces: KiB of a GPU's slots per piece (default 16 GiB); -1 = never cut */
+    int piece_split_kib; /* range pieces: a GPU's slots are cut above this many KiB (default 48 GiB); -1 = always */
 } fa_tuning;
 /* Process defaults: every fa_ctx created afterwards starts from them, and fa_reduce_device /
  * fa_sync_device without a ctx use them. */

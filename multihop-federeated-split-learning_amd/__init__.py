@@ -36,7 +36,8 @@ class FaError(RuntimeError):
 class _Tuning(ctypes.Structure):
     _fields_ = [("block", ctypes.c_int), ("max_blocks", ctypes.c_int), ("unroll", ctypes.c_int),
                 ("load_policy", ctypes.c_int), ("store_policy", ctypes.c_int), ("slot_skew", ctypes.c_int),
-                ("walk", ctypes.c_int), ("rs_chunks", ctypes.c_int)]
+                ("walk", ctypes.c_int), ("rs_chunks", ctypes.c_int), ("piece_span_kib", ctypes.c_int),
+                ("piece_split_kib", ctypes.c_int)]
 
 
 def build():
@@ -82,6 +83,7 @@ def lib():
         "fa_sync_device": (I, [P, I, P, P, I, S, I, P]),
         "fa_sync_part": (I, [P, I, P, P]),
         "fa_bucket_progress": (I, [P, I, ctypes.POINTER(I), ctypes.POINTER(I)]),
+        "fa_bucket_host_read": (I, [P, I, ctypes.POINTER(I)]),
         "fa_reduce_parts": (I, [P, I, ctypes.POINTER(I), P, P]),
         "fa_ctx_set_tuning": (I, [P, ctypes.POINTER(_Tuning)]),
         "fa_ctx_get_tuning": (I, [P, ctypes.POINTER(_Tuning)]),
@@ -260,7 +262,7 @@ def rs_plan(n, n_gpus, n_clients, chunks=0, in_dtype=F32, out_dtype=F32, cus=256
 
 def piece_plan(n, held, in_dtype=F32):
     """fa_diag_pieces (diagnostic): (pieces, elements per piece) of a range-layout GPU holding `held` slots of
-    n elements (the current FA_PIECE_SPAN / FA_PIECE_SPLIT environment)."""
+    n elements (under the process-default piece_span_kib / piece_split_kib, set_tuning)."""
     a, b = ctypes.c_int(), ctypes.c_size_t()
     check(lib().fa_diag_pieces(n, held, in_dtype, ctypes.byref(a), ctypes.byref(b)))
     return a.value, b.value
@@ -268,7 +270,8 @@ def piece_plan(n, held, in_dtype=F32):
 
 def _tuning_dict(t):
     return {"block": t.block, "max_blocks": t.max_blocks, "unroll": t.unroll, "load_policy": t.load_policy,
-            "store_policy": t.store_policy, "slot_skew": t.slot_skew, "walk": t.walk, "rs_chunks": t.rs_chunks}
+            "store_policy": t.store_policy, "slot_skew": t.slot_skew, "walk": t.walk, "rs_chunks": t.rs_chunks,
+            "piece_span_kib": t.piece_span_kib, "piece_split_kib": t.piece_split_kib}
 
 
 def get_tuning():
@@ -282,10 +285,13 @@ LOAD_DEFAULT, LOAD_NT = 1, 2
 STORE_PLAIN, STORE_NT, STORE_SC1, STORE_SC01 = 1, 2, 3, 4
 
 
-def set_tuning(block=0, max_blocks=0, unroll=0, load_policy=0, store_policy=0, slot_skew=0, walk=0, rs_chunks=0):
+def set_tuning(block=0, max_blocks=0, unroll=0, load_policy=0, store_policy=0, slot_skew=0, walk=0, rs_chunks=0,
+               piece_span_kib=0, piece_split_kib=0):
     """fa_set_tuning (process defaults); every argument 0 = keep.  max_blocks -1 = one-shot grid,
-    slot_skew -1 = none, -2 = by slot size (the default: 512 B from 48 MiB slots up, else 2048)."""
-    t = _Tuning(block, max_blocks, unroll, load_policy, store_policy, slot_skew, walk, rs_chunks)
+    slot_skew -1 = none, -2 = by slot size (the default: 512 B from 48 MiB slots up, else 2048);
+    piece_span_kib -1 = never cut a GPU's slots into range pieces, piece_split_kib -1 = always cut them."""
+    t = _Tuning(block, max_blocks, unroll, load_policy, store_policy, slot_skew, walk, rs_chunks, piece_span_kib,
+                piece_split_kib)
     check(lib().fa_set_tuning(ctypes.byref(t)))
 
 
@@ -459,6 +465,12 @@ class Aggregator:
         a, b = ctypes.c_int(), ctypes.c_int()
         check(lib().fa_bucket_progress(self.handle, part_id, ctypes.byref(a), ctypes.byref(b)))
         return a.value, b.value
+
+    def host_read_kept(self, part_id):
+        """fa_bucket_host_read: True when the part's round so far is kept host-side to be read in place."""
+        k = ctypes.c_int()
+        check(lib().fa_bucket_host_read(self.handle, part_id, ctypes.byref(k)))
+        return bool(k.value)
 
     def reduce_parts(self, part_ids, weights=None, stream=None):
         """fa_reduce_parts: one batched reduction of several parts (async); weights: None or one array per

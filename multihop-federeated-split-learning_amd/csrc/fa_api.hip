@@ -54,6 +54,10 @@ struct CtxTuning {
     size_t slot_skew = kSkewAuto;
     // FA_SHARD_CLIENT_RS: pieces per round (the reduce-scatter of piece c overlaps the reduce of c+1).
     int rs_chunks = 8;
+    // Range pieces (piece_len_for): bytes of slots per piece (0 = never cut) and the span of a GPU's slots
+    // above which they are cut.
+    size_t piece_span = size_t(16) << 30;
+    size_t piece_split = size_t(48) << 30;
 };
 std::mutex g_defaults_mu;
 CtxTuning g_defaults;
@@ -121,20 +125,7 @@ constexpr int kSegRing = 4;                // device segment tables per GPU (Gpu
 // kHostReadMax bytes, in pinned memory, is reduced by kernels that read the receipts' segments over PCIe,
 // in at most kHostReadPieces launches (the pieces on which every receipt and the destination are contiguous)
 constexpr size_t kHostReadMax = FA_HOST_READ_MAX_BYTES;
-constexpr int kHostReadPieces = 16;
-// Experiment knobs (tools/): FA_HOST_READ_MAX / FA_HOST_READ_PIECES override the two limits above.
-size_t env_size(const char* name, size_t dflt) {
-    const char* e = std::getenv(name);
-    return e ? (size_t)std::strtoull(e, nullptr, 0) : dflt;
-}
-size_t host_read_max() {
-    static const size_t v = env_size("FA_HOST_READ_MAX", kHostReadMax);
-    return v;
-}
-size_t host_read_pieces() {
-    static const size_t v = env_size("FA_HOST_READ_PIECES", (size_t)kHostReadPieces);
-    return v;
-}
+constexpr size_t kHostReadPieces = 16;
 constexpr int kNotHostReadable = 1;  // host_reduce: the path does not apply (nothing was launched)
 
 // Host memcpy into / out of the pinned staging chunks, split over worker threads:
@@ -216,7 +207,6 @@ private:
 };
 
 int default_copy_threads() {
-    if (const char* e = std::getenv("FA_COPY_THREADS")) return std::max(1, std::atoi(e));
     const unsigned hw = std::thread::hardware_concurrency();
     return (int)std::max(1u, std::min(8u, hw / 2));
 }
@@ -493,50 +483,28 @@ size_t slot_skew_for(size_t bytes, size_t skew) {
     if (skew != kSkewAuto) return skew;
     return bytes >= (size_t(48) << 20) ? 512 : 2048;
 }
-// experiment knob (tools/): FA_SLOT_ALIGN overrides the 4 KiB alignment of a slot's length before the skew
-size_t slot_align() {
-    static const size_t v = [] {
-        const char* e = std::getenv("FA_SLOT_ALIGN");
-        const long long a = e ? std::atoll(e) : 0;
-        return a >= 4096 && a % 4096 == 0 ? (size_t)a : (size_t)4096;
-    }();
-    return v;
-}
+// A slot's length rounded up to 4 KiB, then the skew.
 size_t slot_stride(size_t bytes, size_t skew) {
-    const size_t a = slot_align();
+    constexpr size_t a = 4096;
     return (bytes + a - 1) / a * a + slot_skew_for(bytes, skew);
-}
-
-// A part's device pool.  Experiment knob (tools/): FA_ALLOC_CONTIG=1 asks for physically contiguous memory
-// (hipDeviceMallocContiguous) and falls back to hipMalloc when that fails.
-hipError_t pool_alloc(void** p, size_t bytes) {
-    static const bool contig = [] {
-        const char* e = std::getenv("FA_ALLOC_CONTIG");
-        return e && std::atoi(e) > 0;
-    }();
-    if (contig && hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) return hipSuccess;
-    (void)hipGetLastError();
-    return hipMalloc(p, bytes);
 }
 
 // Range pieces ("the address span").  A GPU whose held slots span more than 48 GiB reads
 // them much slower than their bytes say (C5, 128 x 1 GiB: 0.76-0.80 of HBM; the same bytes as 8 pools of
 // 16 GiB: +6-13%, gpurun_out r03s19): the range layout then cuts its elements into pieces of <= 16 GiB of
 // slots each (a multiple of 64 elements) and reduces them one launch after another.  Below the threshold
-// (C4's 34 GiB included: no gain measured) a part is one piece.  Knobs (tests and tools/): FA_PIECE_SPAN
-// = bytes of slots per piece (0: never cut), FA_PIECE_SPLIT = the span above which a GPU's slots are cut;
-// read at each fa_bucket_define.
-size_t piece_len_for(size_t held, size_t cnt, size_t si) {
-    auto env = [](const char* k, long long d) {
-        const char* e = std::getenv(k);
-        return e ? std::atoll(e) : d;
-    };
-    const long long piece = env("FA_PIECE_SPAN", 16LL << 30), split = env("FA_PIECE_SPLIT", 48LL << 30);
+// (C4's 34 GiB included: no gain measured) a part is one piece.  The two sizes are the context's tuning
+// (fa_tuning.piece_span_kib / piece_split_kib, taken at each fa_bucket_define): `piece` bytes of slots per
+// piece (0: never cut), `split` the span above which a GPU's slots are cut.
+size_t piece_len_for(size_t held, size_t cnt, size_t si, size_t piece, size_t split) {
     const size_t span = held * cnt * si;
-    if (piece <= 0 || held == 0 || cnt == 0 || span <= (size_t)std::max(0LL, split)) return std::max<size_t>(cnt, 1);
-    const size_t n = (span + (size_t)piece - 1) / (size_t)piece;
+    if (piece == 0 || held == 0 || cnt == 0 || span <= split) return std::max<size_t>(cnt, 1);
+    const size_t n = (span + piece - 1) / piece;
     const size_t len = ((cnt + n - 1) / n + 63) / 64 * 64;
     return std::max<size_t>(64, std::min(len, cnt));
+}
+size_t piece_len_for(size_t held, size_t cnt, size_t si, const CtxTuning& t) {
+    return piece_len_for(held, cnt, si, t.piece_span, t.piece_split);
 }
 
 inline bool holds(const Part& p, int g, int k) { return k >= p.c0[(size_t)g] && k < p.c1[(size_t)g]; }
@@ -733,7 +701,7 @@ struct Gather {
 // kernels, same chain, same bits.  The caller keeps pinned receipts until that finalize returns (fa.h), and
 // anything before it that needs the slots -- a reduction, a state sync, a slot address, a pageable submit --
 // first copies the kept receipts in (host_flush), so every other path sees exactly what the plain submit gives.
-// FA_HOST_READ=0 turns it off (experiments).
+// FA_HOST_READ=0 in the environment turns it off (fa.h).
 
 bool host_read_enabled() {
     static const bool on = [] {
@@ -756,13 +724,13 @@ const char* device_visible(const void* ptr) {
 
 bool host_read_part(const fa_ctx* ctx, const Part& p) {
     return host_read_enabled() && ctx->G == 1 && !p.rs && !(ctx->flags & FA_ACCUMULATE_ON_ARRIVAL) &&
-           p.npiece[0] == 1 && p.n > 0 && (size_t)p.D * p.n * dsize(p.in) <= host_read_max();
+           p.npiece[0] == 1 && p.n > 0 && (size_t)p.D * p.n * dsize(p.in) <= kHostReadMax;
 }
 
 // Keeps a pinned receipt of slot `slot` where it is, if the part and every segment allow it (element-aligned,
 // device-visible); false = submit it the plain way.
 bool host_keep(fa_ctx* ctx, Part& p, int slot, const Gather& src) {
-    if (!host_read_part(ctx, p) || (size_t)src.n > 4 * host_read_pieces()) return false;
+    if (!host_read_part(ctx, p) || (size_t)src.n > 4 * kHostReadPieces) return false;
     const size_t si = dsize(p.in);
     std::vector<Part::HostSeg> segs;
     DeviceGuard dg(ctx->gpu[0].dev);
@@ -839,7 +807,7 @@ int host_reduce(fa_ctx* ctx, Part& p, const float* w, hipStream_t s, const Gathe
     std::sort(cuts.begin(), cuts.end());
     cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
     while (!cuts.empty() && cuts.back() > p.n) cuts.pop_back();
-    if (cuts.size() - 1 > host_read_pieces()) return kNotHostReadable;
+    if (cuts.size() - 1 > kHostReadPieces) return kNotHostReadable;
     // element e of a segment list (si bytes per element) -> its device-visible address
     auto at = [](const std::vector<Part::HostSeg>& segs, size_t e, size_t es) -> const char* {
         size_t b = e * es;
@@ -1223,6 +1191,7 @@ int finalize_impl(fa_ctx* ctx, int part_id, const Gather& dst, bool pinned) {
                     dst.total());
     if (!p->ready && p->reduced == 0 && host_read_all(*p)) {  // the kept receipts, read where they are:
         rc = pinned ? host_reduce(ctx, *p, p->w.data(), nullptr, &dst) : kNotHostReadable;  // into the reply,
+        const bool into_reply = rc == FA_OK;
         if (rc == kNotHostReadable) {                                                      // or the output
             if ((rc = host_reduce(ctx, *p, p->w.data(), nullptr, nullptr)) == FA_OK) rc = copy_output(ctx, *p, dst, pinned);
         }
@@ -1230,6 +1199,9 @@ int finalize_impl(fa_ctx* ctx, int part_id, const Gather& dst, bool pinned) {
             rc = FA_OK;  // more pieces than kHostReadPieces: the plain path below
         } else {
             if (rc) return rc;
+            // the device output was not written this round: fa_copy_output must not hand out the last one
+            if (into_reply)
+                for (auto& rr : p->runs) rr.clear();
             reset_round(*p);
             return FA_OK;
         }
@@ -1441,6 +1413,14 @@ int tuning_from(const fa_tuning* t, CtxTuning* io) {
         if (t->rs_chunks < 1 || t->rs_chunks > 1024) return fail(FA_ERR_ARG, "rs_chunks must be 1..1024");
         nt.rs_chunks = t->rs_chunks;
     }
+    if (t->piece_span_kib) {
+        if (t->piece_span_kib < -1) return fail(FA_ERR_ARG, "piece_span_kib must be -1 (never cut) or > 0");
+        nt.piece_span = t->piece_span_kib < 0 ? 0 : (size_t)t->piece_span_kib << 10;
+    }
+    if (t->piece_split_kib) {
+        if (t->piece_split_kib < -1) return fail(FA_ERR_ARG, "piece_split_kib must be -1 (always cut) or > 0");
+        nt.piece_split = t->piece_split_kib < 0 ? 0 : (size_t)t->piece_split_kib << 10;
+    }
     *io = nt;
     return FA_OK;
 }
@@ -1454,6 +1434,8 @@ void tuning_to(const CtxTuning& c, fa_tuning* t) {
     t->slot_skew = c.slot_skew == kSkewAuto ? -2 : (int)c.slot_skew;
     t->walk = c.tu.walk + 1;
     t->rs_chunks = c.rs_chunks;
+    t->piece_span_kib = c.piece_span ? (int)(c.piece_span >> 10) : -1;
+    t->piece_split_kib = c.piece_split ? (int)(c.piece_split >> 10) : -1;
 }
 
 }  // namespace
@@ -1553,13 +1535,8 @@ int fa_create_ex(fa_ctx** out, const int* device_ids, int n_gpus, int flags) {
     // The exchange stream exists only where there is an exchange (the rs layout).  A high-priority stream
     // costs every launch on the device ~2% while its queue lives, even idle (the c4 workload 0.875 -> 0.858
     // of spec once one more high-priority stream had been created, and it stays so after the stream is
-    // destroyed -- the runtime keeps the queue; tools/order_effect.py, gpurun_out r05s27-s29).  FA_COMM_ALWAYS=1
-    // creates it for every context, as up to round 5 (experiments).
-    static const bool comm_always = [] {
-        const char* e = std::getenv("FA_COMM_ALWAYS");
-        return e && std::atoi(e) > 0;
-    }();
-    const bool need_comm = comm_always || (flags & FA_SHARD_CLIENT_RS);
+    // destroyed -- the runtime keeps the queue; tools/order_effect.py, gpurun_out r05s27-s29).
+    const bool need_comm = (flags & FA_SHARD_CLIENT_RS) != 0;
     for (int g = 0; g < n_gpus; ++g) {
         GpuRes& r = ctx->gpu[(size_t)g];
         r.dev = device_ids[g];
@@ -1699,7 +1676,7 @@ int fa_bucket_define(fa_ctx* ctx, int part_id, size_t n_elems, fa_dtype in, fa_d
             p.npiece[g] = 1;
             p.piece_len[g] = p.npad;
         } else {
-            p.piece_len[g] = piece_len_for(held, p.cnt[g], dsize(in));
+            p.piece_len[g] = piece_len_for(held, p.cnt[g], dsize(in), ctx->tuning);
             p.npiece[g] = p.cnt[g] ? (int)((p.cnt[g] + p.piece_len[g] - 1) / p.piece_len[g]) : 1;
         }
         p.stride[g] = slot_stride(p.piece_len[g] * dsize(in), ctx->tuning.slot_skew);
@@ -1712,7 +1689,7 @@ int fa_bucket_define(fa_ctx* ctx, int part_id, size_t n_elems, fa_dtype in, fa_d
         const size_t extra_off = out_off + (out_bytes + 4095) / 4096 * 4096 + shard16_bytes;
         const size_t extra_bytes = rs ? p.npad * 4 : eager ? p.cnt[g] * 4 : 0;
         const size_t bytes = std::max<size_t>(1, extra_off + extra_bytes);
-        if (pool_alloc((void**)&p.pool[g], bytes) != hipSuccess) {
+        if (hipMalloc((void**)&p.pool[g], bytes) != hipSuccess) {
             (void)hipGetLastError();
             free_part(ctx, p);
             return fail(FA_ERR_NOMEM, "device alloc of %zu B failed on GPU %zu", bytes, g);
@@ -1903,6 +1880,16 @@ int fa_bucket_progress(fa_ctx* ctx, int part_id, int* n_submitted, int* n_reduce
     if (rc) return rc;
     if (n_submitted) *n_submitted = p->n_submitted;
     if (n_reduced) *n_reduced = p->ready ? p->D : p->reduced;
+    return FA_OK;
+}
+
+int fa_bucket_host_read(fa_ctx* ctx, int part_id, int* kept) {
+    g_err.clear();
+    Part* p;
+    int rc = check_part(ctx, part_id, &p);
+    if (rc) return rc;
+    if (!kept) return fail(FA_ERR_ARG, "kept is null");
+    *kept = !p->ready && p->reduced == 0 && host_read_all(*p) ? 1 : 0;
     return FA_OK;
 }
 
@@ -2162,12 +2149,12 @@ extern "C" int fa_diag_rs_plan(size_t n, int n_gpus, int n_clients, int chunks, 
 }
 
 // Diagnostic, not part of the ABI in fa.h: how a range-layout GPU holding `held` slots of n elements of
-// `in` cuts them (piece_len_for, the current FA_PIECE_SPAN / FA_PIECE_SPLIT): *n_pieces pieces of
+// `in` cuts them (piece_len_for under the process default tuning, fa_set_tuning): *n_pieces pieces of
 // *piece_elems elements (the last one shorter).  Pure host arithmetic.
 extern "C" int fa_diag_pieces(size_t n, int held, int in, int* n_pieces, size_t* piece_elems) {
     g_err.clear();
     if (held < 0 || !dvalid(in)) return fail(FA_ERR_ARG, "bad piece arguments");
-    const size_t len = piece_len_for((size_t)held, n, dsize((fa_dtype)in));
+    const size_t len = piece_len_for((size_t)held, n, dsize((fa_dtype)in), defaults());
     if (n_pieces) *n_pieces = n ? (int)((n + len - 1) / len) : 1;
     if (piece_elems) *piece_elems = len;
     return FA_OK;

@@ -888,14 +888,8 @@ inline int phased_rl_last(int64_t rem, int64_t lanes, int RL, int RR) {
 // skew): RL / 10 in the f32 form -- 4 of its 40 (north star 1.259-1.261 against 1.271 ms, C4 5.25 against
 // 5.30, one rank's share at 2 GPUs 0.668-0.673 against 0.677-0.684; gpurun_out r02s25-s26); more loses
 // again.  None in the 512-thread bf16 form: with fp32 rows (10) no step was small enough (C3: 1 row
-// 0.425-0.427 ms against 0.424, 4 rows 0.444-0.449; r02s26-s27), and its bf16 rows (20) keep none either.  FA_PHASED_SKEW overrides it (below RL / 2).
-int phased_skew(int RL) {
-    static const int v = [] {
-        const char* e = std::getenv("FA_PHASED_SKEW");
-        return e ? std::max(0, std::atoi(e)) : -1;
-    }();
-    return std::min(v >= 0 ? v : RL >= 40 ? RL / 10 : 0, RL / 2 - 1);  // the bf16 form (20 rows): none
-}
+// 0.425-0.427 ms against 0.424, 4 rows 0.444-0.449; r02s26-s27), and its bf16 rows (20) keep none either.
+int phased_skew(int RL) { return RL >= 40 ? std::min(RL / 10, RL / 2 - 1) : 0; }
 
 // Enqueue one phased launch on stream s, on the stream's counter slot.
 template <typename Kern>
@@ -915,11 +909,7 @@ hipError_t phased_enqueue(PhasedDevice* d, Kern kern, int th, int RL, int RR, hi
     // The last phase writes without the meeting: each workgroup as soon as it has read its share, beside
     // the slower workgroups' last reads (one rank's share at 2 / 4 / 8 GPUs 0.664 / 0.344 / 0.173 ms
     // against 0.670 / 0.346 / 0.176 with the meeting, north star, C3 and C4 unchanged; gpurun_out r02s36).
-    // FA_PHASED_LAST_MEET=1 restores it.
-    static const int last_meet = [] {
-        const char* e = std::getenv("FA_PHASED_LAST_MEET");
-        return e ? std::atoi(e) : 0;
-    }();
+    constexpr int last_meet = 0;
     // FA_TIMELINE: a launch without meetings leaves their stamps alone, so clear the previous launch's
     if (d->tl) (void)hipMemsetAsync(d->tl, 0, sizeof(unsigned long long) * 8 * d->cus, s);
     hipLaunchKernelGGL(kern, dim3((unsigned)d->cus), dim3(th), 0, s, t, nc, init, out, head, nvec, n,
@@ -954,22 +944,7 @@ hipError_t launch_phased_r(PhasedDevice* d, const ClientTable& t, int nc, const 
 // Clients from which a bucket smaller than one phase takes a phase sized to it (plan_chain); fewer
 // clients make the output a larger share of the traffic, and its write burst after the meeting costs
 // more than the one-shot grid's interleaving (C2, D = 8: 0.085 vs 0.075 ms).
-int sized_min_clients() {
-    static const int v = [] {
-        const char* e = std::getenv("FA_SIZED_MIN_CLIENTS");
-        return e ? std::atoi(e) : 16;
-    }();
-    return v;
-}
-
-// experiment knob (tools/): FA_PHASED_MIN_VECS lowers the smallest bucket that takes a full phase
-int64_t phased_min_vecs_env() {
-    static const int64_t v = [] {
-        const char* e = std::getenv("FA_PHASED_MIN_VECS");
-        return e ? (int64_t)std::atoll(e) : (int64_t)-1;
-    }();
-    return v;
-}
+constexpr int kSizedMinClients = 16;
 
 template <typename T> constexpr fa_dtype dtype_of() { return std::is_same<T, float>::value ? FA_F32 : FA_BF16; }
 
@@ -1031,7 +1006,7 @@ hipError_t launch_chain_t(const ClientTable& t, int nc, const float* init, void*
 // Which kernel one FedAvg chain launch takes, decided on the host from the bucket's shape, the tuning and
 // the device's CU count alone (no device call), so that fa_diag_plan_chain can show the selection to the
 // CPU suite.  The phased kernel takes buckets of at least one full phase (walks 4-6), and with walk 5 (the
-// default) also buckets below one phase with >= sized_min_clients() clients, in one phase sized to them,
+// default) also buckets below one phase with >= kSizedMinClients clients, in one phase sized to them,
 // q vectors per lane spread evenly (phased_rl_last): up to RL of them go to LDS alone and the register stage
 // stays empty, so the smallest instantiation serves every q <= RL; above RL the register stage takes the
 // largest RR <= q of the instantiated set and LDS the rest (q - RR <= RL).  E.g. the strong-scaled north
@@ -1049,9 +1024,8 @@ ChainPlan plan_chain(fa_dtype in, fa_dtype out, int64_t nvec, int nc, bool vecto
     int regs = tu.walk == 3 ? 128 : (tu.walk == 5 || bf) ? 96 : 192;
     const int rl = 160 * 1024 / (th * V * (out == FA_BF16 ? 2 : 4));  // Phased<>::RL
     const int64_t lanes = (int64_t)cus * th;
-    const int64_t env = phased_min_vecs_env();
-    if (nvec < (env >= 0 ? env : lanes * (rl + regs / V))) {  // below one full phase
-        if (tu.walk != 4 || nc < sized_min_clients()) return p;
+    if (nvec < lanes * (rl + regs / V)) {  // below one full phase
+        if (tu.walk != 4 || nc < kSizedMinClients) return p;
         const int64_t q = (nvec + lanes - 1) / lanes;
         if (q < (bf ? 4 : 8)) return p;  // too few vectors per lane: the one-shot grid
         // register stages (bytes per lane) instantiated for the sized phase, largest first
@@ -1297,7 +1271,7 @@ __global__ __launch_bounds__(256) void read_probe_kernel(const ClientTable t, in
 
 hipError_t launch_read_probe(const ClientTable& t, int nc, int64_t nvec, float* sink, hipStream_t s) {
     // the phased kernel itself with no output (its reads, LDS and meetings, no writes) wherever an f32 chain of
-    // this shape takes it: from one phase up, and below one phase with >= sized_min_clients() clients in one
+    // this shape takes it: from one phase up, and below one phase with >= kSizedMinClients clients in one
     // phase sized to the buffers (the product's launch for such buckets; the simple probe below reads those
     // up to 14% slower than the product reduces them, r04s16)
     PhasedDevice* d = phased_device();

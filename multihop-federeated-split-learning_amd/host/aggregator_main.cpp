@@ -361,16 +361,14 @@ public:
     // copy each result into its reply.  With --eager the chains already ran as the receipts arrived.
     void reduce_all(const std::vector<int>& mps) {
         if (o_.eager || mps.size() < 2) return;
-        // small parts whose receipts the library reads in place (FA_HOST_READ_MAX_BYTES): each finalize then
-        // reduces straight into its reply, one round trip per part instead of a launch here and a copy there
-        static const size_t host_read_max = [] {  // FA_HOST_READ_MAX: the library's experiment knob
-            const char* e = std::getenv("FA_HOST_READ_MAX");
-            return e ? (size_t)std::strtoull(e, nullptr, 0) : (size_t)FA_HOST_READ_MAX_BYTES;
-        }();
-        if (o_.gpus == 1 && !o_.rs && o_.pinned &&
-            std::all_of(mps.begin(), mps.end(), [&](int mp) {
-                const Bucket& b = buckets_[mp];
-                return (size_t)o_.data_owners * b.numel * (size_t)b.elem <= host_read_max;
+        // parts whose receipts the library keeps to read in place (small pinned receipts, fa_bucket_host_read):
+        // each finalize then reduces straight into its reply, one round trip per part instead of a launch here
+        // and a copy there.  Asked of the library, which alone knows every condition (the environment, the
+        // frames' alignment and pinning); when some part is not kept, the batched launch covers them all.
+        if (std::all_of(mps.begin(), mps.end(), [&](int mp) {
+                int kept = 0;
+                FA_CHECK(fa_bucket_host_read(ctx_, mp, &kept));
+                return kept == 1;
             }))
             return;
         const auto t0 = std::chrono::steady_clock::now();

@@ -12,7 +12,8 @@
 //     clock that stepped back: an NTP step, a VM resume) -- logged, never dropped, since dropping a genuine
 //     receipt would leave the phase waiting forever for an owner that will not resend;
 //   * within a phase, a second receipt of (owner, bucket) replaces the one taken unless it was sent before
-//     it (the newest wins, whichever arrives last).
+//     it (the newest wins, whichever arrives last); the replaced receipt's key is remembered as if it had
+//     been reduced, so a late copy of it in a later round is stale too.
 // A genuine receipt is only ever mistaken for a copy if it carries the exact millisecond stamp, length and
 // sampled content of an earlier receipt of the same owner and bucket: a clock stepped back onto that very
 // millisecond with the sampled words unchanged.
@@ -69,7 +70,7 @@ public:
         auto c = consumed_.find({owner, model_part});
         if (c != consumed_.end() && std::find(c->second.begin(), c->second.end(), k) != c->second.end()) {
             v.stale = true;
-            v.why = "a byte copy of the receipt sent at " + std::to_string(k.t_start) + ", already reduced";
+            v.why = "a byte copy of the receipt sent at " + std::to_string(k.t_start) + ", already reduced or replaced";
             return v;
         }
         auto a = accepted_.find({owner, model_part});
@@ -93,17 +94,19 @@ public:
         return c != consumed_.end() && std::find(c->second.begin(), c->second.end(), k) != c->second.end();
     }
 
-    // The receipt was consumed into its slot (it replaces an earlier one of the same (owner, bucket)).
-    void accept(int owner, int model_part, const ReceiptKey& k) { accepted_[{owner, model_part}] = k; }
+    // The receipt was consumed into its slot.  When it replaces an earlier one of the same (owner, bucket)
+    // with different content, that one joins the reduced keys now: it was taken, so a late copy of it is
+    // never current again (it would otherwise count as its owner's receipt of a later phase).
+    void accept(int owner, int model_part, const ReceiptKey& k) {
+        auto it = accepted_.find({owner, model_part});
+        if (it != accepted_.end() && !(it->second == k)) remember({owner, model_part}, it->second);
+        accepted_[{owner, model_part}] = k;
+    }
 
     // The phase's buckets are reduced: their receipts join the reduced ones, and the newest stamp of each
     // owner becomes its floor (what a later phase's stamps are compared with, for the clock note).
     void end_phase() {
-        for (auto& kv : accepted_) {
-            auto& q = consumed_[kv.first];
-            q.push_back(kv.second);
-            if (q.size() > kKeep) q.pop_front();
-        }
+        for (auto& kv : accepted_) remember(kv.first, kv.second);
         std::map<int, long> fl;
         for (auto& kv : accepted_) {
             const int owner = kv.first.first;
@@ -115,6 +118,12 @@ public:
     }
 
 private:
+    void remember(const std::pair<int, int>& ob, const ReceiptKey& k) {
+        auto& q = consumed_[ob];
+        q.push_back(k);
+        if (q.size() > kKeep) q.pop_front();
+    }
+
     std::map<int, long> floor_;                                      // owner -> newest stamp of its last phase
     std::map<std::pair<int, int>, std::deque<ReceiptKey>> consumed_;  // (owner, bucket) -> reduced receipts
     std::map<std::pair<int, int>, ReceiptKey> accepted_;              // (owner, bucket) -> taken this phase

@@ -269,6 +269,7 @@ int cmd_bench_fedavg(int argc, char** argv) {
     auto acc = torch::zeros({n}, torch::kFloat32);
     torch::Tensor out;
     double best = 1e30, total = 0;
+    std::string rep_s;  // every timed rep, so the caller can report the spread
     for (int r = 0; r < reps + 1; ++r) {
         double t0 = now_s();
         acc.zero_();
@@ -278,12 +279,15 @@ int cmd_bench_fedavg(int argc, char** argv) {
         if (r == 0) continue;  // warm-up
         total += dt;
         if (dt < best) best = dt;
+        char b[32];
+        snprintf(b, sizeof b, "%s%.6f", rep_s.empty() ? "" : ",", dt);
+        rep_s += b;
     }
     double avg = total / reps, bytes = (double)D * n * (bf16 ? 2 : 4);
     printf("{\"mode\":\"fedavg\",\"dtype\":\"%s\",\"n\":%lld,\"D\":%d,\"threads\":%d,\"reps\":%d,\"avg_s\":%.6f,"
-           "\"best_s\":%.6f,\"gib_s\":%.4f,\"fill_s\":%.3f,\"checksum\":%.9g}\n",
+           "\"best_s\":%.6f,\"gib_s\":%.4f,\"fill_s\":%.3f,\"rep_s\":[%s],\"checksum\":%.9g}\n",
            bf16 ? "bf16" : "f32", (long long)n, D, threads, reps, avg, best, bytes / avg / (1ull << 30), fill_s,
-           acc.sum().item<double>());
+           rep_s.c_str(), acc.sum().item<double>());
     return 0;
 }
 

@@ -53,12 +53,12 @@ def test_library_is_gfx950_code(fa, tmp_path):
 
 def test_version_and_errors_without_gpu(fa):
     L = fa.lib()
-    assert L.fa_version() == 6
+    assert L.fa_version() == 7
     # argument errors are reported before any device work
     rc = L.fa_reduce_device(None, 0, None, None, 0, 16, 0, None, 0, 0, None, None)
     assert rc == fa.ERR_ARG and "null" in fa.last_error()
     assert L.fa_fill_uniform(None, 4, 7, 0, 0, 0, None) == fa.ERR_ARG
-    t = fa._Tuning(96, 0, 0, 0, 0, 0, 0, 0)
+    t = fa._Tuning(96, 0, 0, 0, 0, 0, 0, 0, 0, 0)
     assert L.fa_set_tuning(ctypes.byref(t)) == fa.ERR_ARG
     assert L.fa_bucket_define(None, 1, 10, 0, 0, 1, 0) == fa.ERR_ARG
     assert fa.last_error() == "ctx is null"
@@ -75,7 +75,7 @@ def test_tuning_roundtrip(fa):
     fa.set_tuning(block=128, unroll=16, load_policy=1, store_policy=4, rs_chunks=5)
     assert fa.get_tuning() == {"block": 128, "max_blocks": before["max_blocks"], "unroll": 16, "load_policy": 1,
                                "store_policy": 4, "slot_skew": before["slot_skew"], "walk": before["walk"],
-                               "rs_chunks": 5}
+                               "rs_chunks": 5, "piece_span_kib": 16 << 20, "piece_split_kib": 48 << 20}
     with pytest.raises(fa.FaError):
         fa.set_tuning(store_policy=5)
     assert fa.get_tuning()["store_policy"] == 4  # a rejected call changes nothing
@@ -84,7 +84,12 @@ def test_tuning_roundtrip(fa):
     assert fa.get_tuning()["slot_skew"] == 0
     fa.set_tuning(slot_skew=-2)
     assert fa.get_tuning()["slot_skew"] == -2
-    for bad in (dict(slot_skew=100), dict(slot_skew=-3), dict(walk=7), dict(rs_chunks=2000), dict(block=96)):
+    # range pieces (the former FA_PIECE_SPAN / FA_PIECE_SPLIT environment knobs): -1 = never / always cut
+    fa.set_tuning(piece_span_kib=-1, piece_split_kib=-1)
+    assert fa.get_tuning()["piece_span_kib"] == -1 and fa.get_tuning()["piece_split_kib"] == -1
+    fa.set_tuning(piece_span_kib=16 << 20, piece_split_kib=48 << 20)
+    for bad in (dict(slot_skew=100), dict(slot_skew=-3), dict(walk=7), dict(rs_chunks=2000), dict(block=96),
+                dict(piece_span_kib=-2), dict(piece_split_kib=-5)):
         with pytest.raises(fa.FaError):
             fa.set_tuning(**bad)
     fa.set_tuning(**{k: (v or -1) if k in ("max_blocks", "slot_skew") else v for k, v in before.items()})
@@ -98,6 +103,23 @@ def test_ctx_tuning_needs_a_ctx(fa):
     assert L.fa_ctx_get_tuning(None, ctypes.byref(t)) == fa.ERR_ARG
     assert L.fa_reduce_parts(None, 0, None, None, None) == fa.ERR_ARG
     assert L.fa_bucket_progress(None, 1, None, None) == fa.ERR_ARG
+    k = ctypes.c_int(7)
+    assert L.fa_bucket_host_read(None, 1, ctypes.byref(k)) == fa.ERR_ARG
+
+
+def test_no_experiment_knobs_in_the_product():
+    """The library and the drop-in process read only two environment variables:
+    FA_TIMELINE (a diagnostic) and FA_HOST_READ (fa.h); the closed experiments' knobs are gone."""
+    from conftest import PKG_DIR
+    names = set()
+    for sub in ("csrc", "host"):
+        d = os.path.join(PKG_DIR, sub)
+        for f in os.listdir(d):
+            if f.endswith((".hip", ".cpp", ".h")):
+                src = open(os.path.join(d, f)).read()
+                assert "getenv(name)" not in src and "getenv(k)" not in src, f  # no indirect lookups
+                names |= set(re.findall(r'getenv\("([A-Z_0-9]+)"\)', src))
+    assert names == {"FA_TIMELINE", "FA_HOST_READ"}, names
 
 
 @pytest.mark.parametrize("n,world,chunks", [(64, 1, 1), (1000, 2, 1), (10_000, 2, 4), (7_777, 3, 5),

@@ -1,6 +1,6 @@
 """GPU: bench.py's own legs on the one-GPU box, each ending with its parity object (verdict r03 #1).
 
-* A workload held in range pieces (forced small with FA_PIECE_SPLIT / FA_PIECE_SPAN, as C5's 128 x 1 GiB
+* A workload held in range pieces (forced small with --piece-split-kib / --piece-span-kib, as C5's 128 x 1 GiB
   is on one GPU) prints its line: read_stream_peak walks the pieces instead of asking fa_bucket_slot for a
   contiguous slot, and the client-sharded layout builds contiguous slots.
 * `--ctx-multi range|rs` (the in-process multi-GPU children the N = 1 run starts on a node with several
@@ -21,24 +21,36 @@ pytestmark = pytest.mark.gpu
 BENCH = os.path.join(ROOT, "bench.py")
 
 
-def run_bench(args, env=None, timeout=240):
-    r = subprocess.run([sys.executable, BENCH] + args, capture_output=True, text=True, timeout=timeout, cwd=ROOT,
-                       env=dict(os.environ, **(env or {})))
-    assert r.returncode == 0, r.stderr[-3000:]
-    return json.loads(r.stdout.strip().splitlines()[-1])
+def run_bench(args, env=None, timeout=240, tmp=None):
+    """The bench's own output: the full object (the side file its compact stdout line names) for a main line,
+    the printed object for a --ctx-multi child."""
+    import tempfile
+    with tempfile.TemporaryDirectory(prefix="fa_bench_") as d:
+        full = os.path.join(d, "full.json")
+        r = subprocess.run([sys.executable, BENCH] + args, capture_output=True, text=True, timeout=timeout, cwd=ROOT,
+                           env=dict(os.environ, FA_BENCH_FULL=full, **(env or {})))
+        assert r.returncode == 0, r.stderr[-3000:]
+        printed = r.stdout.strip().splitlines()
+        line = json.loads(printed[-1])
+        if "full_record" not in line:
+            return line
+        assert len(printed) == 1, printed[:-1]  # a main line: one line on stdout, nothing else
+        assert len(printed[-1]) <= 6000
+        with open(full) as f:
+            return json.load(f)
 
 
 def ok(p, samples=1024):
     assert p and p["ok"] and p["mismatches"] == 0 and p["samples"] >= samples, p
 
 
-PIECES = {"FA_PIECE_SPLIT": "0", "FA_PIECE_SPAN": str(256 << 20)}  # ns_w8's 1 GiB of slots -> 4 pieces
+PIECES = ["--piece-split-kib", "-1", "--piece-span-kib", str(256 << 10)]  # ns_w8's 1 GiB of slots -> 4 pieces
 
 
 @pytest.mark.parametrize("layout", ["range", "rs"])
 def test_pieced_workload_prints_its_line(fa, torch_gpu, layout):
     line = run_bench(["--workload", "ns_w8", "--layout", layout, "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
-                      "--no-secondary", "--no-live-pmc"], env=PIECES)
+                      "--no-secondary", "--no-live-pmc"] + PIECES)
     ok(line["parity"])
     assert line["value"] > 0 and line["roofline"]["phased_meeting_timeouts"] == 0
     if layout == "range":
@@ -66,11 +78,14 @@ def test_ctx_multi_child_carries_parity(fa, torch_gpu, layout):
 
 
 def test_ctx_multi_host_inclusive_parity(fa, torch_gpu):
-    """--h2d: every client submitted from pinned host memory (client k from buffer k % 8) and the result
-    finalized into host memory; checked against the oracle's chain with that client map."""
-    res = run_bench(["--ctx-multi", "range", "--workload", "ns_w8", "--h2d", "--steps", "2", "--warmup", "1"])
+    """--h2d: every client submitted from pinned host memory (its own buffer: 32 x 32 MiB fit the 16 GiB
+    bound) and the result finalized into a pinned host buffer; checked against the oracle's chain, with the
+    round's H2D / reduce / D2H split reported."""
+    res = run_bench(["--ctx-multi", "range", "--workload", "ns_w8", "--h2d", "--steps", "2", "--warmup", "1",
+                     "--ctx-gpus", "1"])
     ok(res["parity"])
-    assert res["host_inclusive"]
+    assert res["host_inclusive"] and res["distinct_host_buffers"] == 32
+    assert res["h2d_ms"] > 0 and res["reduce_ms"] > 0 and res["d2h_ms"] > 0 and res["pcie_GBs"] > 0
 
 
 def test_two_rank_rehearsal_parity_everywhere(fa, torch_gpu):

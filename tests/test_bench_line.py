@@ -1,0 +1,117 @@
+"""CPU: the bench's stdout line stays small enough for the driver to parse.
+
+BENCH_r05's line was 20.3 KB and the driver's parse returned null.  bench.compact_line keeps the required
+keys, roofline, cpu_baseline (with its spread), parity and one small object per secondary leg, and the full
+object goes to a side file.  Here the compaction runs on the round-5 final-tree line (profiles/r05s53_bench.json)
+and on the shapes of the lines a multi-GPU node produces (the N = 1 run with 8 in-process multi-GPU children,
+and the N = 8 main line with its layout secondaries).
+"""
+import copy
+import json
+import os
+import sys
+
+from conftest import ROOT
+
+sys.path.insert(0, ROOT)
+
+REQUIRED = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "parity")
+ROOFLINE = ("bound", "achieved", "peak", "unit", "frac", "traffic")
+CPU = ("value", "unit", "cores", "kind", "sample")
+
+
+def _r05():
+    with open(os.path.join(ROOT, "profiles", "r05s53_bench.json")) as f:
+        return json.load(f)
+
+
+def _check(line, bench):
+    s = json.dumps(bench.compact_line(line, "gpurun_out/bench_full.json"))
+    assert len(s.encode()) <= bench.LINE_MAX_BYTES, len(s)
+    got = json.loads(s)
+    for k in REQUIRED:
+        assert k in got, k
+    for k in ROOFLINE:
+        assert k in got["roofline"], k
+    if line.get("cpu_baseline"):
+        for k in CPU:
+            assert k in got["cpu_baseline"], k
+    assert got["value"] == line["value"] and got["roofline"]["frac"] == line["roofline"]["frac"]
+    assert "\n" not in s
+    return got
+
+
+def test_round5_line_compacts_under_the_bound():
+    import bench
+    line = _r05()
+    assert len(json.dumps(line)) > 20000  # the line the driver could not parse
+    got = _check(line, bench)
+    sec = got["secondary"]
+    assert set(sec) == set(line["secondary"])
+    assert sec["c4"]["frac"] == line["secondary"]["c4"]["frac"] and sec["c4"]["parity_ok"] is True
+    assert sec["c4"]["cpu_gib_s"] == line["secondary"]["c4"]["cpu_gib_s"]
+    assert sec["round_c2"]["ms"] == line["secondary"]["round_c2"]["round_ms_avg"]
+    assert sec["round_c1"]["e2e_literal_ms"] == line["secondary"]["round_c1"]["e2e_loopback_literal"]["round_ms_median"]
+    assert sec["round_c1"]["cpu_e2e_ms"] == line["secondary"]["round_c1"]["cpu_e2e_loopback"]["round_ms_median"]
+    assert sec["round_c1"]["e2e_parity_ok"] is True
+    rs = sec["ctx_rs_c4_8shard_rehearsal_on_one_gpu"]
+    assert rs["rehearsal"] and rs["err_over_bound"] == round(
+        line["secondary"]["ctx_rs_c4_8shard_rehearsal_on_one_gpu"]["parity"]["max_err_over_bound"], 3)
+    assert got["full_record"] == "gpurun_out/bench_full.json"
+
+
+def test_eight_gpu_node_n1_line_compacts():
+    """The N = 1 run on an 8-GPU node: every single-GPU leg plus eight in-process multi-GPU children, some of
+    them failed with long error text, and a host-inclusive leg with its split."""
+    import bench
+    line = _r05()
+    sec = line["secondary"]
+    child = sec.pop("ctx_rs_c4_8shard_rehearsal_on_one_gpu")
+    sec.pop("ctx_range_c5r_h2d_8shard_rehearsal_on_one_gpu")
+    for key in ("ctx_range_northstar_8gpu", "ctx_rs_northstar_8gpu", "ctx_rs_c4_4gpu", "ctx_rs_c4_8gpu",
+                "ctx_range_c5_h2d_8gpu", "ctx_rs_c4_4gpu_rschunks2", "ctx_rs_c4_4gpu_rschunks4"):
+        sec[key] = dict(copy.deepcopy(child), shared_device_rehearsal=False)
+    sec["ctx_rs_c4_4gpu_rschunks16"] = {"error": "rc 1: " + "x" * 300}
+    sec["ns_h2d"] = {"gib_s": 50.1, "ms_per_round": 166.0, "h2d_ms": 160.1, "reduce_ms": 1.3, "d2h_ms": 4.6,
+                     "pcie_GBs": 55.0, "parity": {"ok": True, "samples": 1026}, "description": "y" * 300}
+    got = _check(line, bench)
+    err = got["secondary"]["ctx_rs_c4_4gpu_rschunks16"]["error"]
+    assert err.startswith("rc 1: x") and len(err) <= 80
+    assert got["secondary"]["ns_h2d"]["h2d_ms"] == 160.1
+    assert "secondary_truncated" not in got
+
+
+def test_eight_gpu_main_line_compacts():
+    """The --gpus 8 main line: range over 8 ranks and the weak-range / rs / chain secondaries."""
+    import bench
+    line = _r05()
+    line["n_gpus"] = 8
+    line["roofline"]["kernel_ms_avg_max_over_ranks"] = 0.17
+    line["parity"] = dict(line["parity"], ranks=8)
+    line["cpu_baseline"] = None  # rank 0 at N = 1 only
+    desc = "client-sharded: each rank reduces its 4 whole clients into fp32 partials " * 3
+    line["secondary"] = {L: {"description": desc, "clients": 32, "steps": 20, "ms_per_step": 0.2, "gib_s": 40000.0,
+                             "phased_meeting_timeouts": 0,
+                             "parity": {"check": "c", "samples": 8000, "mismatches": 0, "max_abs_err": 1e-7,
+                                        "max_err_over_bound": 0.2, "ok": True, "ranks": 8}}
+                         for L in ("weak_range", "rs", "chain")}
+    line["secondary_error"] = "secondary layouts did not finish within 90 s"
+    got = _check(line, bench)
+    assert got["secondary"]["rs"] == {"gib_s": 40000.0, "ms": 0.2, "parity_ok": True, "err_over_bound": 0.2}
+    assert got["parity"]["ranks"] == 8
+
+
+def test_line_printer_writes_compact_line_and_full_record(tmp_path):
+    import io
+    import bench
+    out = io.StringIO()
+    full = tmp_path / "full.json"
+    p = bench.LinePrinter(0, out, full_path=str(full))
+    line = _r05()
+    p.emit(line)
+    p.emit(line)  # once only
+    printed = out.getvalue().splitlines()
+    assert len(printed) == 1 and len(printed[0]) <= bench.LINE_MAX_BYTES
+    assert json.loads(full.read_text()) == line
+    assert json.loads(printed[0])["value"] == line["value"]

@@ -233,8 +233,10 @@ def test_ctx_children_the_n1_run_starts(monkeypatch):
     import time
     res = bench.ctx_multi_secondaries(8, time.monotonic() + 1000)
     sweep = {"ctx_rs_c4_4gpu_rschunks%d" % c for c in bench.RS_CHUNK_SWEEP}
-    assert {"ctx_range_northstar_8gpu", "ctx_rs_northstar_8gpu", "ctx_rs_c4_4gpu", "ctx_rs_c4_8gpu",
+    assert {"ns_h2d", "ctx_range_northstar_8gpu", "ctx_rs_northstar_8gpu", "ctx_rs_c4_4gpu", "ctx_rs_c4_8gpu",
             "ctx_range_c5_h2d_8gpu"} | sweep == set(res)
+    # the north star host-inclusive on one GPU comes first, on every node
+    assert calls[0][calls[0].index("--ctx-gpus") + 1] == "1" and "--h2d" in calls[0] and "northstar" in calls[0]
     assert all(r["parity"]["ok"] for r in res.values())
     c4 = [c for c in calls if "c4" in c and c[c.index("--ctx-gpus") + 1] == "4"]
     assert c4 and c4[0][c4[0].index("--ctx-multi") + 1] == "rs" and "--rs-chunks" not in c4[0]
@@ -244,8 +246,9 @@ def test_ctx_children_the_n1_run_starts(monkeypatch):
     assert all("--rs-chunks" not in c for c in calls[:-len(bench.RS_CHUNK_SWEEP)])
     calls.clear()
     res = bench.ctx_multi_secondaries(1, time.monotonic() + 1000)
-    assert set(res) == {"ctx_rs_c4_8shard_rehearsal_on_one_gpu", "ctx_range_c5r_h2d_8shard_rehearsal_on_one_gpu"}
-    assert all("--ctx-shared" in c and c[c.index("--ctx-shared") + 1] == "8" for c in calls)
+    assert set(res) == {"ns_h2d", "ctx_rs_c4_8shard_rehearsal_on_one_gpu",
+                        "ctx_range_c5r_h2d_8shard_rehearsal_on_one_gpu"}
+    assert all("--ctx-shared" in c and c[c.index("--ctx-shared") + 1] == "8" for c in calls[1:])
     # no time left: skipped, never started
     calls.clear()
     res = bench.ctx_multi_secondaries(8, time.monotonic() + 10)

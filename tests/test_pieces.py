@@ -1,7 +1,7 @@
 """GPU: range-layout pieces (fa_api.hip piece_len_for; DESIGN.md 4, "the address span").  A GPU whose client
 slots would span more than 48 GiB holds them piece-major -- piece j of every slot, then piece j+1 -- and
 reduces one launch per piece, so that each launch's clients lie within 16 GiB.  The shapes that trigger it
-(C5: 128 GiB) are checked by tests/test_c5_shape.py; here FA_PIECE_SPLIT=0 / FA_PIECE_SPAN force pieces on
+(C5: 128 GiB) are checked by tests/test_c5_shape.py; here fa_tuning.piece_split_kib = -1 / piece_span_kib force pieces on
 small buckets so that every round shape runs over them against the oracle, bit-exact: host receipts (staged
 and pinned copies cut at piece boundaries), device-resident fills through fa_bucket_piece, accumulate on
 arrival, bf16, literal mode, the state sync, fa_reduce_parts with a pieced part, two range shards.  The
@@ -23,8 +23,12 @@ def assert_bits(got, ref):
 @pytest.fixture
 def pieces_env(monkeypatch):
     """Every range part defined inside the test is cut into pieces of <= 256 KiB of slots."""
-    monkeypatch.setenv("FA_PIECE_SPLIT", "0")
-    monkeypatch.setenv("FA_PIECE_SPAN", str(256 << 10))
+    from conftest import load_pkg
+    fa = load_pkg()
+    before = fa.get_tuning()
+    fa.set_tuning(piece_split_kib=-1, piece_span_kib=256)  # the process defaults new contexts start from
+    yield
+    fa.set_tuning(piece_split_kib=before["piece_split_kib"], piece_span_kib=before["piece_span_kib"])
 
 
 def ctx_for(fa, G, **kw):

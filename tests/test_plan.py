@@ -49,11 +49,11 @@ def test_plan_arguments_checked(fa):
         fa.rs_plan(100, 0, 2)
 
 
-def test_range_pieces(fa, monkeypatch):
+def test_range_pieces(fa):
     """Range layout pieces (fa_api.hip piece_len_for, DESIGN.md 4 "the address span"): a GPU whose held slots
     span more than 48 GiB cuts them into pieces of <= 16 GiB of slots (a multiple of 64 elements)."""
-    monkeypatch.delenv("FA_PIECE_SPAN", raising=False)
-    monkeypatch.delenv("FA_PIECE_SPLIT", raising=False)
+    before = fa.get_tuning()
+    assert before["piece_span_kib"] == 16 << 20 and before["piece_split_kib"] == 48 << 20
     assert fa.piece_plan(C5, 128) == (8, 1 << 25)            # C5 on one GPU: 128 GiB -> 8 x 16 GiB
     assert fa.piece_plan(C5 // 2, 128) == (4, 1 << 25)       # ... its range shard at 2 GPUs: 64 GiB
     assert fa.piece_plan(C5 // 4, 128) == (1, C5 // 4)       # ... at 4 GPUs: 32 GiB, one piece
@@ -62,9 +62,11 @@ def test_range_pieces(fa, monkeypatch):
     assert fa.piece_plan(0, 128) == (1, 1) and fa.piece_plan(C5, 0) == (1, C5)
     n, pl = fa.piece_plan(12 << 30, 5)                        # 240 GiB of slots in 5 slots: 15 pieces
     assert n == 15 and pl % 64 == 0 and (n - 1) * pl < 12 << 30 <= n * pl
-    monkeypatch.setenv("FA_PIECE_SPAN", "0")
-    assert fa.piece_plan(C5, 128) == (1, C5)
-    monkeypatch.setenv("FA_PIECE_SPAN", str(1 << 20))
-    monkeypatch.setenv("FA_PIECE_SPLIT", "0")
-    n, pl = fa.piece_plan(100_003, 5)                         # 2 MB of slots at 1 MiB per piece
-    assert (n, pl) == (2, 50_048)
+    try:
+        fa.set_tuning(piece_span_kib=-1)                      # never cut
+        assert fa.piece_plan(C5, 128) == (1, C5)
+        fa.set_tuning(piece_span_kib=1 << 10, piece_split_kib=-1)
+        n, pl = fa.piece_plan(100_003, 5)                     # 2 MB of slots at 1 MiB per piece
+        assert (n, pl) == (2, 50_048)
+    finally:
+        fa.set_tuning(piece_span_kib=before["piece_span_kib"], piece_split_kib=before["piece_split_kib"])

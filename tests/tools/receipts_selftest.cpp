@@ -112,6 +112,29 @@ int main() {
         // an owner never seen before
         expect(!l2.check(7, 1, ReceiptKey{1, 0, 0}).stale, "an unknown owner's first receipt is current");
     }
+    // a receipt replaced within its phase: a late copy of it in the next round is stale, so it
+    // can neither stand in for its owner's receipt of that round nor replace the real one
+    {
+        ReceiptLedger l4;
+        const ReceiptKey first = key_of(0, 5, 1, 100), second = key_of(1, 5, 1, 101);
+        expect(!l4.check(5, 1, first).stale, "first receipt of the phase");
+        l4.accept(5, 1, first);
+        expect(!l4.check(5, 1, second).stale, "a newer receipt with other content replaces it");
+        l4.accept(5, 1, second);
+        expect(l4.is_reduced_copy(5, 1, first), "the replaced receipt is remembered at once");
+        l4.end_phase();  // phase 1 reduced with `second`
+        l4.accept(5, 2, key_of(0, 5, 2, 102));
+        l4.end_phase();
+        const auto late = l4.check(5, 1, first);
+        expect(late.stale, "a late copy of the replaced receipt in the next round is stale");
+        expect(l4.check(5, 1, second).stale, "a late copy of the reduced receipt is stale");
+        expect(!l4.check(5, 1, key_of(2, 5, 1, 103)).stale, "the next round's own receipt is current");
+        // a retransmission (the same key) does not push its own key: it stays current within its phase
+        ReceiptLedger l5;
+        l5.accept(6, 1, first);
+        l5.accept(6, 1, first);
+        expect(!l5.is_reduced_copy(6, 1, first), "a retransmission is not remembered as replaced");
+    }
     // the memory is bounded: kKeep phases of a bucket
     {
         ReceiptLedger l3;

@@ -37,8 +37,8 @@ for s in $STEPS; do
         timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
         rc=$?; tail -3 "$OUT/smoke.log"; ok_or_fail $rc smoke ;;
     bench)
-        timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
-        rc=$?; cat "$OUT/bench.json"; tail -3 "$OUT/bench.err"; ok_or_fail $rc bench ;;
+        FA_BENCH_FULL="$OUT/bench_full.json" timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
+        rc=$?; cat "$OUT/bench.json"; wc -c "$OUT/bench.json"; tail -3 "$OUT/bench.err"; ok_or_fail $rc bench ;;
     prof)
         timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
             python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-secondary --no-live-pmc > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
@@ -72,9 +72,7 @@ for s in $STEPS; do
         done ;;
     slices)  # one rank's share of the strong-scaled north star at W = 1, 2, 4, 8 (tools/strong_slices.py)
         timeout -k 10 300 python tools/strong_slices.py 20 > "$OUT/slices.jsonl" 2> "$OUT/slices.err"
-        rc=$?; cat "$OUT/slices.jsonl"; tail -2 "$OUT/slices.err"; ok_or_fail $rc slices
-        FA_PHASED_MIN_VECS=0 timeout -k 10 300 python tools/strong_slices.py 20 > "$OUT/slices_phased.jsonl" 2>> "$OUT/slices.err"
-        rc=$?; cat "$OUT/slices_phased.jsonl"; ok_or_fail $rc slices_phased ;;
+        rc=$?; cat "$OUT/slices.jsonl"; tail -2 "$OUT/slices.err"; ok_or_fail $rc slices ;;
     rounds)  # one aggregator round on its own buckets, batched vs per part (tools/rounds.py) + kernel trace
         timeout -k 10 300 python tools/rounds.py 20 round_c2,round_c3,round_c4 > "$OUT/rounds.jsonl" 2> "$OUT/rounds.err"
         rc=$?; cat "$OUT/rounds.jsonl"; tail -2 "$OUT/rounds.err"; ok_or_fail $rc rounds
