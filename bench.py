@@ -95,22 +95,34 @@ def cpu_threads():
     return max(1, min(n, cap) if cap > 0 else n)
 
 
+def _cpu_topology(c, what):
+    try:
+        with open("/sys/devices/system/cpu/cpu%d/%s" % (c, what)) as f:
+            return f.read().strip()
+    except OSError:
+        return str(c)
+
+
 def pick_cores(n):
-    """`n` CPUs of this process's affinity mask, one per physical core where the topology says so (an SMT
-    sibling of a chosen CPU is taken only when the mask has no other core left)."""
+    """`n` CPUs of this process's affinity mask: one per physical core (an SMT sibling only when the mask has
+    no other core left), dealt round-robin over the L3 domains (CCDs), as a 16-core allocation of this CPU
+    would spread.  Pinning 16 threads to one end of the mask instead puts them on two CCDs, whose links to
+    memory then bound the reference's stream-like loop (r06s01: 73 GiB/s against 258 unpinned)."""
     mask = sorted(os.sched_getaffinity(0))
-    chosen, seen, spare = [], set(), []
+    groups, seen, spare = collections.OrderedDict(), set(), []
     for c in mask:
-        try:
-            with open("/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list" % c) as f:
-                core = f.read().strip()
-        except OSError:
-            core = str(c)
+        core = _cpu_topology(c, "topology/thread_siblings_list")
         if core in seen:
             spare.append(c)
             continue
         seen.add(core)
-        chosen.append(c)
+        groups.setdefault(_cpu_topology(c, "cache/index3/shared_cpu_list"), []).append(c)
+    chosen, lists = [], [list(v) for v in groups.values()]
+    while lists and len(chosen) < n:
+        for g in lists:
+            if g and len(chosen) < n:
+                chosen.append(g.pop(0))
+        lists = [g for g in lists if g]
     return (chosen + spare)[:max(1, n)]
 
 

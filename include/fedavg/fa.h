@@ -133,6 +133,16 @@ int fa_submit_gather(fa_ctx* ctx, int part_id, int client_slot, int n_segments, 
 int fa_submit_gather_pinned(fa_ctx* ctx, int part_id, int client_slot, int n_segments, const void* const* srcs,
                             const size_t* bytes, float weight);
 
+/* Streaming ingest: a receipt handed over while its frame is still arriving (network_layer.cpp:48-65 reads
+ * the whole frame first; aggregator.cpp:63-64 then decodes it).  fa_submit_piece_pinned enqueues the H2D
+ * DMA of bytes [byte_offset, byte_offset + bytes) of the bucket (e.g. one parameter record, as soon as its
+ * bytes are in) from pinned memory the caller keeps unchanged until fa_finalize* returns.  The slot counts
+ * as the client's receipt only after fa_submit_commit (weight as for fa_submit); pieces never committed are
+ * overwritten by the slot's next submit.  A piece overlapping one already sent replaces those bytes. */
+int fa_submit_piece_pinned(fa_ctx* ctx, int part_id, int client_slot, size_t byte_offset, const void* host_src,
+                           size_t bytes);
+int fa_submit_commit(fa_ctx* ctx, int part_id, int client_slot, float weight);
+
 /* Replaces the end of a phase: the reduced module handed to new_message()
  * (aggregator.cpp:96-106 / :153-166).  Waits for the submits, reduces on every
  * GPU, copies the result (out dtype) to host_dst and resets the round. */

@@ -1020,6 +1020,22 @@ int advance_prefix(fa_ctx* ctx, Part& p) {
     return FA_OK;
 }
 
+// The bookkeeping of one receipt in slot `slot`: it counts for the round (a second one replaces it), with its
+// weight; on arrival the chain advances over the in-order prefix.
+int mark_submitted(fa_ctx* ctx, Part& p, int slot, float weight) {
+    p.ready = false;  // a new receipt invalidates a finished reduction (fa_reduce_parts, a full prefix)
+    if (!p.submitted[(size_t)slot]) {
+        p.submitted[(size_t)slot] = 1;
+        ++p.n_submitted;
+    } else if (slot < p.reduced) {  // a receipt already chained was replaced: restart the chain
+        p.reduced = 0;
+        p.ready = false;
+    }
+    p.w[(size_t)slot] = weight;
+    p.last_slot = slot;
+    return advance_prefix(ctx, p);
+}
+
 int submit_impl(fa_ctx* ctx, int part_id, int slot, const Gather& src, float weight, bool pinned) {
     Trace tr("fa_submit part %d slot %d", part_id, slot);
     Part* p;
@@ -1078,17 +1094,42 @@ int submit_impl(fa_ctx* ctx, int part_id, int slot, const Gather& src, float wei
         return FA_OK;
     });
     if (rc) return rc;
-    p->ready = false;  // a new receipt invalidates a finished reduction (fa_reduce_parts, a full prefix)
-    if (!p->submitted[(size_t)slot]) {
-        p->submitted[(size_t)slot] = 1;
-        ++p->n_submitted;
-    } else if (slot < p->reduced) {  // a receipt already chained was replaced: restart the chain
-        p->reduced = 0;
-        p->ready = false;
+    return mark_submitted(ctx, *p, slot, weight);
+}
+
+// Streaming ingest (fa_submit_piece_pinned): bytes [at, at + len) of a receipt -- one parameter record of an
+// archive that is still arriving -- DMA'd from pinned memory into the slot's bytes on every GPU that holds
+// them.  Only the copies: the slot counts as a receipt once fa_submit_commit names it.
+int piece_impl(fa_ctx* ctx, int part_id, int slot, size_t at, const void* src, size_t len) {
+    Trace tr("fa_submit_piece part %d slot %d", part_id, slot);
+    Part* p;
+    int rc = check_part(ctx, part_id, &p);
+    if (rc) return rc;
+    if (slot < 0 || slot >= p->D) return fail(FA_ERR_ARG, "client slot %d out of range [0,%d)", slot, p->D);
+    const size_t si = dsize(p->in);
+    if (at > p->n * si || len > p->n * si - at)
+        return fail(FA_ERR_ARG, "piece [%zu, %zu) outside part %d's %zu bytes", at, at + len, part_id, p->n * si);
+    if (len && !src) return fail(FA_ERR_ARG, "piece source is null");
+    if (len == 0) return FA_OK;
+    if ((rc = host_flush(ctx, *p))) return rc;  // kept receipts first: the plain path from here on
+    for (int g = 0; g < ctx->G; ++g) {
+        if (!holds(*p, g, slot)) continue;
+        const size_t base = p->off[(size_t)g] * si, end = base + p->cnt[(size_t)g] * si;
+        const size_t a = std::max(at, base), b = std::min(at + len, end);
+        if (a >= b) continue;
+        GpuRes& r = ctx->gpu[(size_t)g];
+        DeviceGuard dg(r.dev);
+        const size_t piece_bytes = p->piece_len[(size_t)g] * si;
+        for (size_t x = a - base; x < b - base;) {  // GPU-local bytes, one copy per range piece
+            const int j = (int)(x / piece_bytes);
+            const size_t in = x - (size_t)j * piece_bytes, take = std::min(b - base - x, piece_bytes - in);
+            FA_HIP(hipMemcpyAsync(piece_ptr(*p, g, slot, j) + in, static_cast<const char*>(src) + (base + x - at), take,
+                                  hipMemcpyHostToDevice, r.copy));
+            x += take;
+        }
+        ++r.copy_gen;
     }
-    p->w[(size_t)slot] = weight;
-    p->last_slot = slot;
-    return advance_prefix(ctx, *p);
+    return FA_OK;
 }
 
 // D2H of the part's output (the result leaves for new_message()) into `dst`, following the runs of its
@@ -1752,6 +1793,27 @@ int fa_submit_gather(fa_ctx* ctx, int part_id, int client_slot, int n_segments, 
                      const size_t* bytes, float weight) {
     g_err.clear();
     return submit_impl(ctx, part_id, client_slot, Gather{n_segments, srcs, bytes}, weight, false);
+}
+
+int fa_submit_piece_pinned(fa_ctx* ctx, int part_id, int client_slot, size_t byte_offset, const void* host_src,
+                           size_t bytes) {
+    g_err.clear();
+    return piece_impl(ctx, part_id, client_slot, byte_offset, host_src, bytes);
+}
+
+int fa_submit_commit(fa_ctx* ctx, int part_id, int client_slot, float weight) {
+    g_err.clear();
+    Trace tr("fa_submit_commit part %d slot %d", part_id, client_slot);
+    Part* p;
+    int rc = check_part(ctx, part_id, &p);
+    if (rc) return rc;
+    if (client_slot < 0 || client_slot >= p->D)
+        return fail(FA_ERR_ARG, "client slot %d out of range [0,%d)", client_slot, p->D);
+    if (p->host_src[(size_t)client_slot].size()) {  // an earlier receipt kept in place would shadow the pieces
+        p->host_src[(size_t)client_slot].clear();
+        --p->n_host;
+    }
+    return mark_submitted(ctx, *p, client_slot, weight);
 }
 
 int fa_submit_gather_pinned(fa_ctx* ctx, int part_id, int client_slot, int n_segments, const void* const* srcs,

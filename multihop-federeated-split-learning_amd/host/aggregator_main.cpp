@@ -65,6 +65,9 @@ struct Options {
     // 16 at a time 2.15-2.31 s -- the phase end drops from 0.48-0.51 s to 0.04-0.17 s
     int rx_concurrency = 8;
     int senders = 8;  // fan-out sender threads (each destination keeps to one, in order)
+    // streaming ingest: receipt frames of at least this many bytes go to their slot record by record while
+    // they arrive (NetLayer::set_streaming; pinned frames only); 0 = off
+    size_t stream_min = 1u << 20;
     std::map<int, double> samples;  // client id -> n_k
 };
 
@@ -73,7 +76,7 @@ void usage() {
                  "       [--rounds R] [--port-base P] [--discover] [--link-mbps M] [--samples id:n,...]\n"
                  "       [--divisor K] [--last-layers L] [--no-pinned] [--layout range|rs] [--rs-chunks C]\n"
                  "       [--eager] [--stall-report S] [--receipt-timeout S] [--rx-concurrency K]\n"
-                 "       [--senders S] [--test-shared-device]\n";
+                 "       [--senders S] [--stream-min-bytes N] [--test-shared-device]\n";
 }
 
 bool parse_args(int argc, char** argv, Options* o) {
@@ -103,6 +106,7 @@ bool parse_args(int argc, char** argv, Options* o) {
         else if (a == "--receipt-timeout") o->receipt_timeout_s = std::atof(val("--receipt-timeout"));
         else if (a == "--rx-concurrency") o->rx_concurrency = std::atoi(val("--rx-concurrency"));
         else if (a == "--senders") o->senders = std::atoi(val("--senders"));
+        else if (a == "--stream-min-bytes") o->stream_min = (size_t)std::strtoull(val("--stream-min-bytes"), nullptr, 0);
         else if (a == "--layout") {
             std::string l = val("--layout");
             if (l == "rs") o->rs = true;
@@ -190,7 +194,49 @@ public:
 
     // Stale receipts across rounds (host/receipts.h): a byte copy of a receipt its owner already had reduced
     // (a late copy of an earlier round's) is dropped -- never counted, never in a slot.
-    void end_phase() { ledger_.end_phase(); }
+    void end_phase() {
+        ledger_.end_phase();
+        // frames that ended without a receipt for this phase (a malformed frame, one still queued for the
+        // next phase) need no stream any more: their receipts, if any, take the plain path
+        streams_.erase(std::remove_if(streams_.begin(), streams_.end(),
+                                      [](const Stream& s) { return s.in->ended.load(std::memory_order_acquire); }),
+                       streams_.end());
+    }
+
+    // ---------------------------------------------------------------- streaming ingest
+    //
+    // The reference reads a whole frame before anything else happens (network_layer.cpp:48-65) and only then
+    // decodes it (aggregator.cpp:63-64); so did this process until round 6, and a phase ended with the H2D
+    // copies of the receipts that landed last.  The archive's parameter records (data/<key>) come first in
+    // the zip, stored and 64-byte aligned, and every receipt of a bucket is the same module saved again: so
+    // the records' places in a frame of a given length are those of the bucket's previous receipt.  A large
+    // frame is announced while it arrives (NetLayer::set_streaming); once its owner and bucket are known and
+    // the bucket has a layout for its length, each record is DMA'd to the slot as soon as its bytes are in
+    // (fa_submit_piece_pinned).  When the frame is complete the archive is parsed as before; if its records
+    // are where they were predicted, the slot is committed (fa_submit_commit), else the receipt is submitted
+    // the plain way over the streamed bytes.  Only a slot whose owner has no receipt of the bucket yet this
+    // phase is streamed into, by one frame at a time, and a receipt that lands whole stops any other frame
+    // streaming into its slot -- so a stale copy can never overwrite a receipt taken (the ledger still judges
+    // every frame once it is complete; a stream it drops was never committed).
+    void set_phase(const std::vector<int>& mps) { phase_mps_ = std::set<int>(mps.begin(), mps.end()); }
+
+    void pump() {
+        intake();
+        for (auto it = streams_.begin(); it != streams_.end();) {
+            Stream& s = *it;
+            if (s.in->failed.load(std::memory_order_acquire)) {  // the connection broke: nothing comes of it
+                it = streams_.erase(it);
+                continue;
+            }
+            if (s.slot < 0 && !s.cancelled) claim(s);
+            if (s.slot >= 0) feed(s, s.in->have.load(std::memory_order_acquire));
+            ++it;
+        }
+    }
+
+    unsigned long long streamed() const { return streamed_; }
+    unsigned long long stream_fallbacks() const { return stream_fallbacks_; }
+    unsigned long long streamed_bytes() const { return streamed_bytes_; }
 
     static ReceiptKey key_of(const Receipt& r) {
         return ReceiptKey{r.t_start, r.blob_len, archive_fingerprint(r.blob(), r.blob_len)};
@@ -199,6 +245,7 @@ public:
     // A receipt of the other phase is never taken (see main): counted as a stale copy when it is a byte copy
     // of one already reduced, else as ignored (a retransmission of this round's).
     void other_phase(const Receipt& r, int phase) {
+        take_stream(r);
         if (ledger_.is_reduced_copy(r.client_id, r.model_part, key_of(r))) {
             std::cerr << "[aggregator] stale part " << r.model_part << " from owner " << r.client_id
                       << " during phase " << phase << " (a byte copy of a receipt already reduced): dropped\n";
@@ -215,6 +262,7 @@ public:
     // as a second torch::load would) but is not another receipt -- the phase waits for D distinct owners.
     // A stale receipt (above) is dropped: returns false without touching the slot.
     bool absorb(const Receipt& r) {
+        const Stream st = take_stream(r);  // the frame's own stream, if it was streamed into a slot
         const ReceiptKey key = key_of(r);
         const ReceiptLedger::Verdict v = ledger_.check(r.client_id, r.model_part, key);
         if (v.stale) {
@@ -251,10 +299,19 @@ public:
             std::exit(1);
         }
         const int slot = slot_of(r.client_id);
+        cancel_streams(r.client_id, r.model_part);  // nothing else writes this slot from here on
         std::vector<const void*> ptrs;
         std::vector<size_t> bytes;
         if (ar.param_segments(&ptrs, &bytes)) {
-            if (r.frame->pinned) {  // DMA from the frame itself; it is held until the bucket is finalized
+            auto recs = records_of(r, ptrs, bytes);
+            if (st.slot == slot && st.recs && *st.recs == *recs) {
+                // streamed: the layout held; the records not sent yet go now, then the slot counts
+                Stream done = st;
+                feed(done, r.frame->size());
+                FA_CHECK(fa_submit_commit(ctx_, r.model_part, slot, weight_of(r.client_id)));
+                ++streamed_;
+            } else if (r.frame->pinned) {  // DMA from the frame itself; it is held until the bucket is finalized
+                if (st.slot >= 0) ++stream_fallbacks_;  // the layout changed: the plain submit overwrites
                 FA_CHECK(fa_submit_gather_pinned(ctx_, r.model_part, slot, (int)ptrs.size(), ptrs.data(),
                                                  bytes.data(), weight_of(r.client_id)));
                 b.held.push_back(r.frame);
@@ -269,6 +326,10 @@ public:
                 std::exit(1);
             }
             FA_CHECK(fa_submit(ctx_, r.model_part, slot, flat.data(), weight_of(r.client_id)));
+        }
+        if (r.frame->pinned && !ptrs.empty()) {  // the layout later frames of this length are streamed with
+            b.recs = records_of(r, ptrs, bytes);
+            b.recs_len = r.blob_len;
         }
         b.bytes_in += r.blob_len;
         ledger_.accept(r.client_id, r.model_part, key);
@@ -388,10 +449,87 @@ public:
     }
 
 private:
+    struct Rec {  // one parameter record: where it lies in the archive, its bytes, where they go in the bucket
+        size_t off = 0, bytes = 0, at = 0;
+        bool operator==(const Rec& o) const { return off == o.off && bytes == o.bytes && at == o.at; }
+    };
+    using Recs = std::shared_ptr<const std::vector<Rec>>;
+    struct Stream {
+        std::shared_ptr<Inflight> in;
+        int slot = -1;           // the slot it streams into (-1: none yet)
+        bool cancelled = false;  // a receipt of its (owner, bucket) landed whole: never streamed again
+        Recs recs;               // the layout it streams by (the bucket's at the time it was claimed)
+        size_t next = 0;         // records sent so far
+    };
+
+    static Recs records_of(const Receipt& r, const std::vector<const void*>& ptrs, const std::vector<size_t>& bytes) {
+        auto v = std::make_shared<std::vector<Rec>>();
+        size_t at = 0;
+        for (size_t i = 0; i < ptrs.size(); ++i) {
+            v->push_back(Rec{(size_t)((const uint8_t*)ptrs[i] - r.blob()), bytes[i], at});
+            at += bytes[i];
+        }
+        return v;
+    }
+
+    void intake() {
+        for (auto& in : net_->take_new_streams()) streams_.push_back(Stream{in});
+    }
+
+    Stream take_stream(const Receipt& r) {
+        intake();
+        for (auto it = streams_.begin(); it != streams_.end(); ++it)
+            if (it->in->buf.get() == r.frame.get()) {
+                Stream s = *it;
+                streams_.erase(it);
+                return s;
+            }
+        return Stream{};
+    }
+
+    void cancel_streams(int owner, int mp) {
+        for (auto& s : streams_)
+            if (s.in->client_id == owner && s.in->model_part == mp) {
+                s.slot = -1;
+                s.cancelled = true;
+            }
+    }
+
+    void claim(Stream& s) {
+        const Inflight& in = *s.in;
+        if (!phase_mps_.count(in.model_part) || !in.buf->pinned) return;
+        auto bi = buckets_.find(in.model_part);
+        if (bi == buckets_.end() || !bi->second.defined) return;
+        Bucket& b = bi->second;
+        if (!b.recs || b.recs->empty() || b.recs_len != in.blob_len || b.arrived.count(in.client_id)) return;
+        auto si = slots_.find(in.client_id);
+        if (si == slots_.end()) return;  // an owner not seen yet takes its slot when its receipt lands
+        for (auto& o : streams_)
+            if (&o != &s && o.slot >= 0 && o.in->client_id == in.client_id && o.in->model_part == in.model_part) return;
+        s.slot = si->second;
+        s.recs = b.recs;
+        s.next = 0;
+        b.held.push_back(in.buf);  // DMA'd from until the bucket is finalized, whatever becomes of the frame
+    }
+
+    void feed(Stream& s, size_t have) {
+        const Inflight& in = *s.in;
+        while (s.next < s.recs->size()) {
+            const Rec& rc = (*s.recs)[s.next];
+            if (in.blob_off + rc.off + rc.bytes > have) break;
+            FA_CHECK(fa_submit_piece_pinned(ctx_, in.model_part, s.slot, rc.at, in.buf->data() + in.blob_off + rc.off,
+                                            rc.bytes));
+            streamed_bytes_ += rc.bytes;
+            ++s.next;
+        }
+    }
+
     struct Bucket {
         bool defined = false;
         size_t numel = 0, bytes_in = 0;
         int elem = 4;  // bytes per parameter element: 4 fp32, 2 bf16
+        Recs recs;            // the parameter records of the last pinned receipt (the streaming layout)
+        size_t recs_len = 0;  // ... for archives of this length
         Receipt last;
         std::vector<std::shared_ptr<const Bytes>> held;  // pinned frames DMA'd from, until finalize
         std::set<int> arrived;  // client ids received this round
@@ -432,22 +570,39 @@ private:
     ReceiptLedger ledger_;
     // cumulative receipt accounting, printed with every round
     unsigned long long stale_dropped_ = 0, ignored_ = 0, replaced_ = 0, clock_back_ = 0;
+    std::vector<Stream> streams_;
+    std::set<int> phase_mps_;
+    unsigned long long streamed_ = 0, stream_fallbacks_ = 0, streamed_bytes_ = 0;
 };
 
 // The next receipt, with the failure detection the reference lacks (its receive loop blocks forever on a
 // data owner that died, network_layer.cpp:654-665): every stall_report_s of silence names the owners still
-// missing in this phase; after receipt_timeout_s of silence (if set) the aggregator exits with code 3.
+// missing in this phase; after receipt_timeout_s of silence (if set) the aggregator exits with code 3.  Bytes
+// of a streamed frame arriving count as activity.  While it waits, the frames still arriving are streamed to
+// their slots (Aggregator::pump).
 Receipt wait_receipt(NetLayer& net, const Options& o, Aggregator& agg, const std::vector<int>& mps, int round,
                      int phase) {
+    static uint64_t gen = 0;  // the network layer's progress counter, as last seen (one consumer)
     Receipt r;
-    double silent = 0;
+    auto last = std::chrono::steady_clock::now();
+    int reports = 0;
     for (;;) {
-        double step = o.stall_report_s;
-        if (o.receipt_timeout_s > 0) step = std::min(step, o.receipt_timeout_s - silent);
-        if (net.try_next_receipt(&r, std::max(1, (int)(step * 1000)))) return r;
-        silent += step;
-        const bool give_up = o.receipt_timeout_s > 0 && silent >= o.receipt_timeout_s - 1e-9;
-        std::cerr << "[aggregator] round " << round << " phase " << phase << ": no receipt for " << silent
+        agg.pump();
+        const double silent = secs_since(last);
+        double wait = (reports + 1) * o.stall_report_s - silent;
+        if (o.receipt_timeout_s > 0) wait = std::min(wait, o.receipt_timeout_s - silent);
+        const int ev = net.wait_event(&r, &gen, std::max(1, (int)(wait * 1000)));
+        if (ev == 1) return r;
+        if (ev == 2) {  // progress: a frame is arriving
+            last = std::chrono::steady_clock::now();
+            reports = 0;
+            continue;
+        }
+        const double now_silent = secs_since(last);
+        const bool give_up = o.receipt_timeout_s > 0 && now_silent >= o.receipt_timeout_s - 1e-3;
+        if (!give_up && now_silent < (reports + 1) * o.stall_report_s - 1e-3) continue;
+        ++reports;
+        std::cerr << "[aggregator] round " << round << " phase " << phase << ": no receipt for " << now_silent
                   << " s; missing " << agg.missing(mps) << (give_up ? "; giving up (--receipt-timeout)" : "")
                   << "\n";
         if (give_up) {
@@ -481,6 +636,7 @@ int main(int argc, char** argv) {
     NetLayer net(o.id, RoutingTable(o.port_base), o.senders);
     net.set_link_mbps(o.link_mbps);
     net.set_rx_concurrency(o.rx_concurrency);
+    if (o.pinned) net.set_streaming(o.stream_min);  // the records are DMA'd from the pinned frame as it fills
     std::string err;
     if (o.discover && !net.find_init(600, &err)) {
         std::cerr << "[aggregator] discovery failed: " << err << "\n";
@@ -513,6 +669,7 @@ int main(int argc, char** argv) {
         // counts, cumulatively: stale_dropped (byte copies, either phase), ignored (other-phase receipts that
         // are not copies), replaced (retransmissions within a phase), clock_back (owner clocks that went back).
         auto t0 = std::chrono::steady_clock::now();
+        agg.set_phase({1});
         int received = 0;
         while (received < o.data_owners) {
             Receipt r = wait_receipt(net, o, agg, {1}, round, 1);
@@ -537,6 +694,7 @@ int main(int argc, char** argv) {
         const int want = o.data_owners * L;
         std::vector<int> mps;
         for (int mp = 2; mp <= L + 1; ++mp) mps.push_back(mp);
+        agg.set_phase(mps);
         while (got < want) {
             Receipt r = wait_receipt(net, o, agg, mps, round, 2);
             if (r.model_part == 1) {  // a retransmission of this round's part 1 (above), or a late copy
@@ -568,10 +726,10 @@ int main(int argc, char** argv) {
                "\"phase2\":{\"receive_s\":%.6f,\"reduce_s\":%.6f,\"bytes_in\":%zu,\"layers\":%d,"
                "\"absorb_s\":%.6f,\"finalize_s\":%.6f,\"frame_s\":%.6f,\"send_s\":%.6f},"
                "\"send_failures\":%llu,\"stale_dropped\":%llu,\"ignored\":%llu,\"replaced\":%llu,"
-               "\"clock_back\":%llu}\n",
+               "\"clock_back\":%llu,\"streamed\":%llu,\"stream_fallbacks\":%llu,\"streamed_bytes\":%llu}\n",
                round, recv1, red1, in1, s1.absorb_s, s1.finalize_s, s1.frame_s, recv2, red2, in2, L, s2.absorb_s,
                s2.finalize_s, s2.frame_s, send2, (unsigned long long)net.send_failures(), agg.stale_dropped(), agg.ignored(),
-               agg.replaced(), agg.clock_back());
+               agg.replaced(), agg.clock_back(), agg.streamed(), agg.stream_fallbacks(), agg.streamed_bytes());
         fflush(stdout);
     }
     net.stop();

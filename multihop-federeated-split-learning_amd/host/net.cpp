@@ -342,8 +342,67 @@ void NetLayer::gate_leave() {
     cv_gate_.notify_all();
 }
 
+// A large OPERATION frame whose head is in: announced to the consumer as Inflight (set_streaming).
+std::shared_ptr<Inflight> NetLayer::announce(const std::shared_ptr<Bytes>& b, size_t have, size_t len) {
+    Message m;
+    size_t off = 0, blen = 0;
+    if (!split_receipt_head(b->data(), have, len, &m, &off, &blen, nullptr) || m.type != OPERATION || off == 0)
+        return nullptr;
+    auto in = std::make_shared<Inflight>();
+    in->client_id = m.client_id;
+    in->model_part = m.model_part;
+    in->t_start = m.t_start;
+    in->buf = b;
+    in->blob_off = off;
+    in->blob_len = blen;
+    in->have.store(have, std::memory_order_release);
+    {
+        std::lock_guard<std::mutex> lk(m_rx_);
+        new_streams_.push_back(in);
+        ++progress_gen_;
+    }
+    cv_rx_.notify_all();
+    return in;
+}
+
+void NetLayer::progress(Inflight* in, size_t have, bool end, bool failed) {
+    in->have.store(have, std::memory_order_release);
+    if (end) {
+        in->failed.store(failed, std::memory_order_release);
+        in->ended.store(true, std::memory_order_release);
+    }
+    {
+        std::lock_guard<std::mutex> lk(m_rx_);
+        ++progress_gen_;
+    }
+    cv_rx_.notify_all();
+}
+
+std::vector<std::shared_ptr<Inflight>> NetLayer::take_new_streams() {
+    std::lock_guard<std::mutex> lk(m_rx_);
+    std::vector<std::shared_ptr<Inflight>> out;
+    out.swap(new_streams_);
+    return out;
+}
+
+int NetLayer::wait_event(Receipt* r, uint64_t* gen, int timeout_ms) {
+    // on the system clock, as try_next_receipt (libstdc++'s steady-clock wait_for is invisible to TSan)
+    const auto until = std::chrono::system_clock::now() + std::chrono::milliseconds(timeout_ms);
+    std::unique_lock<std::mutex> lk(m_rx_);
+    cv_rx_.wait_until(lk, until, [&] { return !receipts_.empty() || progress_gen_ != *gen; });
+    const bool moved = progress_gen_ != *gen;
+    *gen = progress_gen_;
+    if (!receipts_.empty()) {
+        *r = std::move(receipts_.front());
+        receipts_.pop_front();
+        return 1;
+    }
+    return moved ? 2 : 0;
+}
+
 // recv_frame with the receive gate (set_rx_concurrency): the length first, then -- for a large frame,
-// once its turn has come -- the body.  A turn is given up when the sender stalls.
+// once its turn has come -- the body.  A turn is given up when the sender stalls.  A frame of at least
+// stream_min_ bytes is announced to the consumer while it arrives (set_streaming).
 std::shared_ptr<Bytes> NetLayer::recv_frame_gated(int fd, uint64_t seq) {
     int32_t len = 0;
     if (!recv_all(fd, &len, 4) || len <= 0) return nullptr;
@@ -354,6 +413,9 @@ std::shared_ptr<Bytes> NetLayer::recv_frame_gated(int fd, uint64_t seq) {
     bool gated = gate_limit_ > 0 && (size_t)len >= kGateBytes;
     if (gated && !gate_enter(seq)) return nullptr;
     auto b = frame_buffer_for(head, have, (size_t)len);
+    std::shared_ptr<Inflight> in;
+    if (stream_min_ > 0 && (size_t)len >= stream_min_ && have < (size_t)len) in = announce(b, have, (size_t)len);
+    size_t told = have;  // bytes reported to the consumer so far
     char* c = reinterpret_cast<char*>(b->data()) + have;
     size_t n = (size_t)len - have;
     auto last = std::chrono::steady_clock::now();
@@ -374,8 +436,13 @@ std::shared_ptr<Bytes> NetLayer::recv_frame_gated(int fd, uint64_t seq) {
         c += k;
         n -= (size_t)k;
         last = std::chrono::steady_clock::now();
+        if (in && n > 0 && (size_t)len - n - told >= kStreamStep) {
+            told = (size_t)len - n;
+            progress(in.get(), told, false, false);
+        }
     }
     if (gated) gate_leave();
+    if (in) progress(in.get(), (size_t)len - n, true, n != 0);
     return n == 0 ? b : nullptr;
 }
 
@@ -385,7 +452,7 @@ void NetLayer::reader_loop(Conn* c) {
     const int fd = c->fd;
     uint64_t seq = c->seq0;
     for (;;) {
-        auto text = gate_limit_ > 0 ? recv_frame_gated(fd, seq) : recv_frame(fd);
+        auto text = gate_limit_ > 0 || stream_min_ > 0 ? recv_frame_gated(fd, seq) : recv_frame(fd);
         if (!text) {
             publish(seq, Item{});  // release the FIFO position
             break;

@@ -65,6 +65,19 @@ struct Receipt {  // Task.h:30-51, the fields the aggregation path uses
     const uint8_t* blob() const { return (const uint8_t*)frame->data() + blob_off; }
 };
 
+// A large OPERATION frame while it is still arriving (NetLayer::set_streaming): its header fields, the buffer
+// it is being received into and how much of the frame text is in.  The reader stores `have` (release) after
+// the bytes below it have landed, and sets `ended` (with `failed` when the connection broke) last.  The
+// complete frame is then published as a Receipt whose `frame` is this same buffer.
+struct Inflight {
+    int client_id = -1, model_part = 0;
+    long t_start = 0;
+    std::shared_ptr<Bytes> buf;
+    size_t blob_off = 0, blob_len = 0;
+    std::atomic<size_t> have{0};
+    std::atomic<bool> ended{false}, failed{false};
+};
+
 class NetLayer {
 public:
     NetLayer(int my_id, RoutingTable routes, int senders = 8)
@@ -90,6 +103,16 @@ public:
     void set_rx_concurrency(int k) { gate_limit_ = k; }
     static constexpr size_t kGateBytes = 8u << 20;
     static constexpr int kGateStallMs = 2000;
+
+    // Streaming ingest: frames of at least min_bytes (0 = off) are announced as Inflight while they arrive, so
+    // the consumer can start on the parts already in (the reference reads a whole frame first,
+    // network_layer.cpp:48-65).  Readers report progress every kStreamStep bytes and at the end.
+    void set_streaming(size_t min_bytes) { stream_min_ = min_bytes; }
+    static constexpr size_t kStreamStep = 256u << 10;
+    // Inflight frames announced since the last call.
+    std::vector<std::shared_ptr<Inflight>> take_new_streams();
+    // Waits up to timeout_ms for a receipt (1, *r set) or for stream progress since *gen (2); 0 on timeout.
+    int wait_event(Receipt* r, uint64_t* gen, int timeout_ms);
 
     Receipt next_receipt();      // blocking FIFO pop (check_new_task for a data owner, :392-409)
     Message next_refactor();     // blocking (check_new_refactor_task, :481-493)
@@ -136,6 +159,8 @@ private:
     void sender_loop(int i);
     Item parse_frame(std::shared_ptr<Bytes> text, bool* keep);
     std::shared_ptr<Bytes> recv_frame_gated(int fd, uint64_t seq);
+    std::shared_ptr<Inflight> announce(const std::shared_ptr<Bytes>& b, size_t have, size_t len);
+    void progress(Inflight* in, size_t have, bool end, bool failed);
     bool gate_enter(uint64_t seq);
     void gate_leave();
 
@@ -168,6 +193,9 @@ private:
     std::condition_variable cv_rx_;
     std::deque<Receipt> receipts_;
     std::deque<Message> refactors_;
+    size_t stream_min_ = 0;
+    uint64_t progress_gen_ = 0;                         // under m_rx_
+    std::vector<std::shared_ptr<Inflight>> new_streams_;  // under m_rx_
     uint64_t next_seq_ = 0, next_pub_ = 0;  // under m_rx_
     std::map<uint64_t, Item> pending_;       // finished frames waiting for an earlier one
     std::mutex m_tx_;

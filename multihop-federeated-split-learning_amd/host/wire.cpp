@@ -225,9 +225,14 @@ bool decode(const std::string& text, Message* m, std::string* err) {
 }
 
 bool split_receipt(const char* base, size_t size, Message* m, size_t* blob_off, size_t* blob_len, std::string* err) {
+    return split_receipt_head(base, size, size, m, blob_off, blob_len, err);
+}
+
+bool split_receipt_head(const char* base, size_t have, size_t size, Message* m, size_t* blob_off, size_t* blob_len,
+                        std::string* err) {
     // The header is the text before "values : " (at a line start, within the first 4 KiB); the archive
     // runs from there to the closing ",\n}" (Message.h:514-518), parsed without touching its bytes.
-    const size_t scan = std::min<size_t>(size, 4096);
+    const size_t scan = std::min<size_t>(std::min(have, size), 4096);
     const char* v = nullptr;
     for (size_t i = 0; i + 9 <= scan; ++i)
         if (std::memcmp(base + i, "values : ", 9) == 0 && (i == 0 || base[i - 1] == '\n')) {

@@ -115,6 +115,10 @@ bool decode(const std::string& text, Message* m, std::string* err);
 // A received OPERATION frame's text (no length prefix): the header fields decoded into *m, and where
 // the torch::save archive (`values`) lies inside it; false for a malformed header.
 bool split_receipt(const char* base, size_t size, Message* m, size_t* blob_off, size_t* blob_len, std::string* err);
+// The same from the first `have` bytes of a frame text of `size` bytes (a frame still arriving): the header
+// must lie within them.
+bool split_receipt_head(const char* base, size_t have, size_t size, Message* m, size_t* blob_off, size_t* blob_len,
+                        std::string* err);
 // Length-prefixed frame as it goes on the socket (one copy of m.values).
 std::string frame(const Message& m);
 std::shared_ptr<Bytes> frame_bytes(const Message& m);

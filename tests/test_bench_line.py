@@ -115,3 +115,26 @@ def test_line_printer_writes_compact_line_and_full_record(tmp_path):
     assert len(printed) == 1 and len(printed[0]) <= bench.LINE_MAX_BYTES
     assert json.loads(full.read_text()) == line
     assert json.loads(printed[0])["value"] == line["value"]
+
+
+def test_cpu_baseline_cores_spread_over_ccds(monkeypatch):
+    """The CPU legs run pinned on one CPU per physical core, dealt over the L3 domains:
+    a 64-core, 8-CCD, SMT-2 mask gives 16 cores as 2 per CCD and never an SMT sibling."""
+    import bench
+    cpus = list(range(128))  # cpu c and c + 64 are SMT siblings; CCD = (c % 64) // 8
+    monkeypatch.setattr(bench.os, "sched_getaffinity", lambda pid: set(cpus))
+
+    def topo(c, what):
+        core = c % 64
+        if what.startswith("topology"):
+            return "%d,%d" % (core, core + 64)
+        return "ccd%d" % (core // 8)
+    monkeypatch.setattr(bench, "_cpu_topology", topo)
+    got = bench.pick_cores(16)
+    assert len(set(got)) == 16 and all(c < 64 for c in got)
+    assert sorted((c // 8) for c in got) == sorted(list(range(8)) * 2)
+    assert bench.pick_cores(1) == [0]
+    assert len(bench.pick_cores(100)) == 100  # SMT siblings once every core is taken
+    assert bench.compact_cpus([0, 1, 2, 3, 8, 16, 17]) == "0-3,8,16-17"
+    s = bench.spread([0.5, 0.25, 1.0], 2**30)
+    assert s == {"min": 1.0, "median": 2.0, "max": 4.0, "reps": 3}

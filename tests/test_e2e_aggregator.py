@@ -316,3 +316,83 @@ def test_bf16_parts_over_tcp(torch_gpu, tmp_path, extra):
     finally:
         if agg.poll() is None:
             agg.kill()
+
+
+def _stream_run(blobs, parts_spec, D, rounds, agg_extra, owner_extra, timeout=300):
+    """fa_aggregator with streaming ingest against fake owners whose frames go out in random pieces
+    (fake_owners --chunked); returns (owners' result, the aggregator's round lines, its stderr)."""
+    base = pick_base()
+    agg = subprocess.Popen([AGG, "-i", "-1", "-d", str(D), "-c", "1", "--rounds", str(rounds), "--port-base",
+                            str(base), "--stall-report", "20", "--receipt-timeout", "120"] + agg_extra,
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        time.sleep(0.5)
+        r = subprocess.run([OWNERS, "--blobs", blobs, "--parts", "1,2,3", "-d", str(D), "-c", "1", "--rounds",
+                            str(rounds), "--port-base", str(base), "--reply-timeout", "120"] + parts_spec + owner_extra,
+                           capture_output=True, text=True, timeout=timeout)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res = json.loads(r.stdout.strip().splitlines()[-1])
+        out, err = agg.communicate(timeout=60)
+        assert agg.returncode == 0, err[-2000:]
+        lines = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+        assert len(lines) == rounds
+        return res, lines, err
+    finally:
+        if agg.poll() is None:
+            agg.kill()
+
+
+LENET = ["--model-name", "2", "--start", "6", "--end", "1"]
+LARGE = ["--model-name", "1", "--start", "9", "--end", "3"]
+
+
+@pytest.mark.parametrize("chunks,extra", [
+    ("1,64,7", []),                               # 1..64-byte pieces: every record boundary splits somewhere
+    ("1,65536,8", []),                            # 1 B .. 64 KiB
+    ("1,65536,9", ["--eager"]),                   # the chain advances on commits
+    ("1,65536,10", ["--mode", "literal"]),        # literal: owners in turn, the last committed receipt
+    ("1,4096,11", ["--gpus", "2", "--test-shared-device"]),  # range shards: each piece split over the GPUs
+])
+def test_streaming_ingest_lenet_random_pieces(torch_gpu, chunks, extra):
+    """Streaming ingest: every frame (--stream-min-bytes 1) is DMA'd to its slot record by
+    record while it arrives, the owners writing their frames in random pieces of 1 byte to 64 KiB with random
+    pauses, all owners at once, so the frames land interleaved in random order.  From round 1 on (the layout
+    comes from round 0's receipts) receipts are committed from their streams; every reply bit-exact."""
+    D, rounds = 3, 3
+    owner = ["--chunked", chunks] + (["--mode", "literal"] if "literal" in extra else [])
+    res, lines, err = _stream_run(os.path.join(GOLDEN, "lenet5_c1"), LENET, D, rounds,
+                                  ["--stream-min-bytes", "1"] + extra, owner)
+    assert res["ok"] and res["checked_elems"] == rounds * D * (50_536 + 10_164 + 850)
+    assert lines[0]["streamed"] == 0  # round 0: no layout yet
+    assert lines[-1]["streamed"] >= (rounds - 1) * D * 3 - 2, lines[-1]  # nearly every later receipt
+    assert lines[-1]["stream_fallbacks"] == 0 and lines[-1]["streamed_bytes"] > 0
+
+
+@pytest.mark.parametrize("extra", [[], ["--eager"], ["--layout", "rs", "--rs-chunks", "3"],
+                                   ["--gpus", "3", "--test-shared-device"]])
+def test_streaming_ingest_multi_mb_parts(torch_gpu, tmp_path, extra):
+    """Multi-MB parts at the default threshold (frames of >= 1 MiB stream) in random 4..64 KiB pieces: parts
+    2 and 3 are streamed from round 1 on, part 1 (150 KB) is not; every reply bit-exact (rs: the bound)."""
+    sizes = _large_parts(str(tmp_path))
+    D, rounds = 6, 3
+    tol = ["--rel-tol", "1e-6"] if "rs" in extra else []
+    res, lines, err = _stream_run(str(tmp_path), LARGE, D, rounds, extra, ["--chunked", "4096,65536,3"] + tol)
+    assert res["ok"] and res["checked_elems"] == rounds * D * sum(sizes.values())
+    assert lines[-1]["streamed"] >= (rounds - 1) * D * 2 - 2, lines[-1]
+    assert lines[-1]["stream_fallbacks"] == 0
+
+
+@pytest.mark.parametrize("extra", [[], ["--eager"]])
+def test_streaming_with_late_copies_and_retransmissions(torch_gpu, extra):
+    """Streamed frames that must NOT end up in a slot: owner 2 re-sends its previous round's receipts before
+    and after the current ones (late byte copies, stale), all of it in random pieces, streamed.  A stale copy may stream into the empty slot but is never committed, and a
+    receipt that lands whole stops any other frame streaming into its slot: every reply bit-exact and the
+    stale counts exact, as without streaming."""
+    D, rounds = 4, 3
+    res, lines, err = _stream_run(os.path.join(GOLDEN, "lenet5_c1"), LENET, D, rounds,
+                                  ["--stream-min-bytes", "1"] + extra,
+                                  ["--chunked", "1,65536,5", "--retransmit-late", "2"])
+    assert res["ok"] and res["rounds"] == rounds
+    for r, l in enumerate(lines[1:], start=1):
+        assert 2 * 3 * r - 1 <= l["stale_dropped"] <= 2 * 3 * r, (r, l)
+    assert lines[-1]["streamed"] > 0

@@ -174,6 +174,45 @@ def test_kept_receipts_into_output_then_copy(fa, O, torch_gpu):
             assert np.array_equal(got.view(np.uint32), O.fedavg(xs[mp], w).view(np.uint32)), mp
 
 
+def test_host_read_query_and_no_stale_copy_output(fa, O, torch_gpu):
+    """fa_bucket_host_read says whether a part's round is kept to be read in place (the drop-in's phase 2 asks
+    it before batching); and once a round was reduced straight into a pinned reply, the part's
+    device output was not written, so fa_copy_output refuses (FA_ERR_STATE) rather than return the previous
+    round's result."""
+    n, D = 10_164, 2
+    w = O.weights(D)
+    with fa.Aggregator(1) as agg:
+        agg.define(2, n, fa.F32, fa.F32, D, fa.FEDAVG)
+        # round 0 the plain way (pageable receipts): a device output exists afterwards
+        xs0 = [O.gen(0x10, k, n) for k in range(D)]
+        for k in range(D):
+            agg.submit(2, k, xs0[k], w[k])
+        assert not agg.host_read_kept(2)
+        agg.finalize(2)
+        assert np.array_equal(agg.copy_output(2).view(np.uint32), O.fedavg(xs0, w).view(np.uint32))
+        # round 1: pinned receipts kept in place, reduced straight into the pinned reply
+        xs1 = [O.gen(0x11, k, n) for k in range(D)]
+        keep = []
+        for k in range(D):
+            assert not agg.host_read_kept(2)  # not every receipt yet
+            buf, views = place(fa, xs1[k], [(0, n)], n * 4)
+            keep.append(buf)
+            agg.submit_gather(2, k, views, w[k], pinned=True)
+        assert agg.host_read_kept(2)
+        dbuf, dviews = dst_views(fa, n, 4, [(0, n)], n * 4)
+        agg.finalize_gather(2, dviews, pinned=True)
+        assert agg.host_reads() == 1
+        assert np.array_equal(gathered(dviews, np.float32).view(np.uint32), O.fedavg(xs1, w).view(np.uint32))
+        with pytest.raises(fa.FaError) as e:
+            agg.copy_output(2)
+        assert e.value.code == fa.ERR_STATE
+        # a device reduction afterwards gives it an output again
+        for k in range(D):
+            agg.submit(2, k, xs1[k], w[k])
+        agg.reduce(2)
+        assert np.array_equal(agg.copy_output(2).view(np.uint32), O.fedavg(xs1, w).view(np.uint32))
+
+
 @pytest.mark.parametrize("case", ["pageable_mix", "misaligned", "over_limit", "sync", "slot_read", "replaced"])
 def test_paths_that_copy_kept_receipts_in(fa, O, torch_gpu, case):
     """Where the in-place read must not (or cannot) run, the kept receipts go to their slots first and the

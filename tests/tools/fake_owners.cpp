@@ -12,6 +12,9 @@
 //                  [--clock-skew K,S] [--reply-timeout S] [--rel-tol X] [--routing-table]
 //                  [--sequential]   (owners send at once, one connection each, unless --sequential
 //                                    or --mode literal, whose result depends on the arrival order)
+//                  [--chunked MIN,MAX[,SEED]]  (every frame written in random pieces of MIN..MAX bytes with
+//                                    random pauses; owners sending at once then arrive interleaved in random
+//                                    order: the aggregator's streaming ingest)
 // Every frame is stamped (t_start, network_layer.cpp:761) when it first goes out, on its owner's clock;
 // --clock-skew K,S sets owner K's clock back S ms more every round (an NTP step, a VM resume).
 // --routing-table: the refactor message carries the owners' addresses (read_table 1, as the init node's
@@ -32,6 +35,7 @@
 #include <fstream>
 #include <iostream>
 #include <map>
+#include <random>
 #include <set>
 #include <sstream>
 #include <string>
@@ -151,6 +155,8 @@ int main(int argc, char** argv) {
     double rel_tol = 0;                   // > 0: fp32 replies within rel_tol * sum_k |w_k x_k| (the rs layout)
     bool routing_table = false;           // --routing-table: the refactor message carries the owners' addresses
     long reply_timeout_ms = 600000;
+    size_t chunk_min = 0, chunk_max = 0;  // --chunked: frames written in random pieces
+    uint64_t chunk_seed = 1;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
         const char* v = i + 1 < argc ? argv[i + 1] : "";
@@ -183,6 +189,15 @@ int main(int argc, char** argv) {
             skew_owner = std::atoi(v), skew_ms = std::atol(c + 1), ++i;
         }
         else if (a == "--reply-timeout") reply_timeout_ms = (long)(std::atof(v) * 1000), ++i;
+        else if (a == "--chunked") {
+            unsigned long long lo = 0, hi = 0, sd = 1;
+            const int got = std::sscanf(v, "%llu,%llu,%llu", &lo, &hi, &sd);
+            if (got < 2 || lo < 1 || hi < lo) {
+                std::cerr << "--chunked MIN,MAX[,SEED] with 1 <= MIN <= MAX\n";
+                return 2;
+            }
+            chunk_min = lo, chunk_max = hi, chunk_seed = sd, ++i;
+        }
         else {
             std::cerr << "unknown argument " << a << "\n";
             return 2;
@@ -286,6 +301,20 @@ int main(int argc, char** argv) {
     };
     const int threads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     OwnerThreads owners(concurrent ? D : 0);
+    std::vector<std::mt19937_64> chunk_rng;
+    for (int k = 0; k < D; ++k) chunk_rng.emplace_back(chunk_seed * 1000003ull + (uint64_t)k);
+    // a frame in random pieces with random pauses (--chunked), else in one write
+    auto send_frame = [&](int fd, const Bytes& f, int k) -> bool {
+        if (chunk_max == 0) return send_all(fd, f.data(), f.size());
+        std::mt19937_64& rng = chunk_rng[(size_t)k];
+        for (size_t o = 0; o < f.size();) {
+            const size_t c = std::min<size_t>(f.size() - o, chunk_min + rng() % (chunk_max - chunk_min + 1));
+            if (!send_all(fd, f.data() + o, c)) return false;
+            o += c;
+            if (rng() % 32 == 0) std::this_thread::sleep_for(std::chrono::microseconds(rng() % 300));
+        }
+        return true;
+    };
     auto fill = [&](uint64_t sd, uint32_t k, size_t n, int es, uint8_t* x) {  // the oracle's generator, in chunks
         std::vector<std::thread> th;
         const size_t per = (n + threads - 1) / threads;
@@ -357,10 +386,18 @@ int main(int argc, char** argv) {
                     for (auto& f : by_owner[k]) {
                         const int fd = connect_to(routes.host_for(-1), routes.port_for(-1), 100, 200);
                         stamp(k, f);
-                        if (fd < 0 || !send_all(fd, f.first->data(), f.first->size())) send_ok = false;
+                        if (fd < 0 || !send_frame(fd, *f.first, k)) send_ok = false;
                         if (fd >= 0) close(fd);
                     }
                 });
+            } else if (chunk_max > 0) {  // in owner order, each frame in random pieces (--chunked)
+                for (int k = 0; k < D && send_ok; ++k)
+                    for (auto& f : by_owner[k]) {
+                        const int fd = connect_to(routes.host_for(-1), routes.port_for(-1), 100, 200);
+                        stamp(k, f);
+                        if (fd < 0 || !send_frame(fd, *f.first, k)) send_ok = false;
+                        if (fd >= 0) close(fd);
+                    }
             } else {  // one after another, in owner order (literal mode: the last receipt is owner D-1's)
                 for (int k = 0; k < D; ++k)
                     for (auto& f : by_owner[k]) {

@@ -6,6 +6,8 @@
 //    recycling 3 rounds would allocate 3x that), and receipts carry the pool's `pinned` tag;
 //  * a frame queued for several destinations reaches each of them (serialize-once fan-out), in
 //    order per destination;
+//  * streaming (set_streaming): frames written in random pieces are announced while they arrive, their
+//    progress is monotonic and true, a complete one is published as the same buffer, a broken one fails;
 //  * TorchArchive::layout_into + seal_params == with_params_into on a real archive (optional arg).
 // Prints one JSON line {"ok": ..., ...}; exit 0 iff ok.
 #include <unistd.h>
@@ -17,6 +19,7 @@
 #include <cstring>
 #include <fstream>
 #include <iostream>
+#include <map>
 #include <memory>
 #include <sstream>
 #include <thread>
@@ -214,6 +217,102 @@ int main(int argc, char** argv) {
         }
     }
 
+    // streaming: 4 owners write 3 MiB frames in random pieces (1 B .. 64 KiB) at once; every frame is announced
+    // while it arrives with its header fields, its `have` only grows and the bytes below it are the sender's,
+    // it ends complete, and the receipt published for it is the same buffer.  One owner hangs up mid-frame:
+    // its stream ends failed and no receipt comes of it.
+    size_t streamed_checks = 0;
+    {
+        RoutingTable sroutes(base + 200);
+        // on the heap: a NetLayer on the stack where the gate test's stood would reuse its (trivially
+        // destroyed) mutexes' addresses, which ThreadSanitizer then takes for the same mutexes
+        auto sagg_p = std::make_unique<NetLayer>(-1, sroutes);
+        NetLayer& sagg = *sagg_p;
+        sagg.set_streaming(1u << 20);
+        if (!sagg.start()) {
+            std::cerr << "stream: bind failed\n";
+            ok = false;
+        } else {
+            const int S = 5;  // owners 0..3 whole, owner 4 hangs up halfway
+            std::vector<std::shared_ptr<Bytes>> sf;
+            for (int k = 0; k < S; ++k) sf.push_back(make_frame(300 + k, 2 + (k % 2), payload, (uint8_t)(11 + k)));
+            std::vector<std::thread> th;
+            for (int k = 0; k < S; ++k)
+                th.emplace_back([&, k] {
+                    const int fd = connect_to("127.0.0.1", sroutes.port_for(-1), 50, 100);
+                    uint64_t x = 0x9E3779B97F4A7C15ull * (uint64_t)(k + 1);
+                    const size_t end = k == S - 1 ? sf[k]->size() / 2 : sf[k]->size();
+                    for (size_t o = 0; fd >= 0 && o < end;) {
+                        x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+                        const size_t c = std::min<size_t>(end - o, 1 + x % 65536);
+                        if (!send_all(fd, sf[k]->data() + o, c)) break;
+                        o += c;
+                        if (x % 16 == 0) std::this_thread::sleep_for(std::chrono::microseconds(x % 200));
+                    }
+                    if (fd >= 0) close(fd);
+                });
+            std::map<const Bytes*, std::shared_ptr<Inflight>> streams;
+            std::map<const Bytes*, size_t> last_have;
+            int receipts = 0;
+            uint64_t gen = 0;
+            const auto t_end = std::chrono::steady_clock::now() + std::chrono::seconds(30);
+            auto check_progress = [&] {
+                for (auto& in : sagg.take_new_streams()) {
+                    const int k = in->client_id - 300;
+                    if (k < 0 || k >= S || in->model_part != 2 + (k % 2) || in->blob_len != payload) {
+                        std::cerr << "stream: bad header fields\n";
+                        ok = false;
+                        continue;
+                    }
+                    streams[in->buf.get()] = in;
+                }
+                for (auto& kv : streams) {
+                    Inflight& in = *kv.second;
+                    const bool ended = in.ended.load(std::memory_order_acquire);
+                    const size_t have = in.have.load(std::memory_order_acquire);
+                    if (have < last_have[kv.first]) ok = false;  // never shrinks
+                    last_have[kv.first] = have;
+                    const int k = in.client_id - 300;
+                    // the bytes below `have` are the sender's (the frame text = the sent bytes after the length)
+                    for (size_t j = 0; j < have; j += 9973) {
+                        ++streamed_checks;
+                        if (in.buf->data()[j] != sf[(size_t)k]->data()[4 + j]) {
+                            std::cerr << "stream: byte " << j << " of owner " << k << " below have is wrong\n";
+                            ok = false;
+                            break;
+                        }
+                    }
+                    if (ended && in.failed.load() != (k == S - 1)) {
+                        std::cerr << "stream: owner " << k << " ended with the wrong status\n";
+                        ok = false;
+                    }
+                }
+            };
+            while (receipts < S - 1 && std::chrono::steady_clock::now() < t_end) {
+                Receipt rc;
+                const int ev = sagg.wait_event(&rc, &gen, 200);
+                check_progress();
+                if (ev != 1) continue;
+                ++receipts;
+                auto it = streams.find(rc.frame.get());
+                if (it == streams.end() || !it->second->ended.load() || it->second->failed.load() ||
+                    it->second->have.load() != rc.frame->size() || rc.client_id == 300 + S - 1) {
+                    std::cerr << "stream: receipt of client " << rc.client_id << " does not match its stream\n";
+                    ok = false;
+                }
+            }
+            for (auto& t : th) t.join();
+            std::this_thread::sleep_for(std::chrono::milliseconds(200));
+            check_progress();
+            Receipt extra;
+            if (receipts != S - 1 || (int)streams.size() != S || sagg.try_next_receipt(&extra, 100)) {
+                std::cerr << "stream: " << receipts << " receipts, " << streams.size() << " streams\n";
+                ok = false;
+            }
+            sagg.stop();
+        }
+    }
+
     // archive split copy: layout_into + values + seal_params == with_params_into
     size_t checked_archive = 0;
     if (argc > 1) {
@@ -253,8 +352,8 @@ int main(int argc, char** argv) {
         checked_archive = ar.size();
     }
     printf("{\"ok\": %s, \"rounds\": %d, \"senders\": %d, \"pool_allocations\": %zu, \"live_after\": %zu, "
-           "\"archive_bytes\": %zu, \"send_failures\": %llu}\n",
+           "\"archive_bytes\": %zu, \"send_failures\": %llu, \"streamed_checks\": %zu}\n",
            ok ? "true" : "false", rounds, D, allocs, (size_t)live_allocs, checked_archive,
-           (unsigned long long)send_failures);
+           (unsigned long long)send_failures, streamed_checks);
     return ok ? 0 : 1;
 }

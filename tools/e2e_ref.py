@@ -83,6 +83,8 @@ def leg(name, spec, D, agg_cmd, mode, port_base, rounds, blobs, startup_s, extra
         view = {k: med(lambda p, k=k: p[k.split(".")[0]][k.split(".")[1]])
                 for k in ("phase1.receive_s", "phase1.absorb_s", "phase1.reduce_s", "phase2.receive_s",
                           "phase2.absorb_s", "phase2.reduce_s", "phase2.send_s")}
+    if lines:  # streaming ingest (fa_aggregator, round 6): receipts committed from their streams, cumulative
+        view = dict(view or {}, streamed=lines[-1].get("streamed"), stream_fallbacks=lines[-1].get("stream_fallbacks"))
     return {"leg": name, "mode": mode, "ok": res["ok"], "rounds_timed": len(ms), "aggregator_view_ms": view,
             "round_ms_median": round(statistics.median(ms), 3), "round_ms_min": min(ms),
             "round0_ms": res["round_ms"][0], "checked_elems": res["checked_elems"]}
@@ -120,7 +122,8 @@ def main():
                                                                  "1", "--mode", mode, "--rounds", str(rounds + 1),
                                                                  "--port-base", str(base)] +
                                       os.environ.get("E2E_AGG_ARGS", "").split(),
-                                      mode, base, rounds + 1, blobs, 0.5), config=cfg)), flush=True)
+                                      mode, base, rounds + 1, blobs, 0.5), config=cfg,
+                                  agg_args=os.environ.get("E2E_AGG_ARGS", ""))), flush=True)
 
 
 if __name__ == "__main__":

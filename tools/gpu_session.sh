@@ -104,6 +104,15 @@ for s in $STEPS; do
             ok_or_fail $rc "e2e_ref $C"
         done
         kill $HB ;;
+    stream_ab)  # streaming ingest on / off, alternating, C2 and C3 through the drop-in (tools/e2e_ref.py)
+        for C in ${STREAM_CFGS:-c2 c3}; do
+            for i in 1 2; do
+                for A in "--stream-min-bytes 0" ""; do
+                    E2E_ONLY_FA=1 E2E_AGG_ARGS="$A" timeout -k 10 600 python -u tools/e2e_ref.py $C 0 10 >> "$OUT/stream_ab.jsonl" 2>> "$OUT/stream_ab.err"
+                    rc=$?; tail -c 400 "$OUT/stream_ab.jsonl"; echo; ok_or_fail $rc "stream_ab $C"
+                done
+            done
+        done ;;
     probe)
         hipcc --offload-arch=gfx950 -O3 tools/hbm_probe.hip -o "$OUT/hbm_probe" > "$OUT/probe_build.log" 2>&1 &&
         timeout -k 10 300 "$OUT/hbm_probe" > "$OUT/hbm_probe.json" 2> "$OUT/probe.err"
