@@ -103,19 +103,38 @@ def _cpu_topology(c, what):
         return str(c)
 
 
+def _numa_node(c):
+    try:
+        for e in os.listdir("/sys/devices/system/cpu/cpu%d" % c):
+            if e.startswith("node") and e[4:].isdigit():
+                return int(e[4:])
+    except OSError:
+        pass
+    return 0
+
+
 def pick_cores(n):
     """`n` CPUs of this process's affinity mask: one per physical core (an SMT sibling only when the mask has
-    no other core left), dealt round-robin over the L3 domains (CCDs), as a 16-core allocation of this CPU
-    would spread.  Pinning 16 threads to one end of the mask instead puts them on two CCDs, whose links to
-    memory then bound the reference's stream-like loop (r06s01: 73 GiB/s against 258 unpinned)."""
+    no other core left), on one NUMA node when it holds enough cores (its memory then local to every thread;
+    the inputs are first-touched by the same cores), dealt round-robin over that node's L3 domains (CCDs), as
+    a 16-core allocation of this CPU would spread.  Pinning 16 threads to one end of the mask instead puts
+    them on two CCDs, whose links to memory then bound the reference's stream-like loop (r06s01: 73 GiB/s)."""
     mask = sorted(os.sched_getaffinity(0))
-    groups, seen, spare = collections.OrderedDict(), set(), []
+    cores, seen, spare = [], set(), []
     for c in mask:
         core = _cpu_topology(c, "topology/thread_siblings_list")
         if core in seen:
             spare.append(c)
             continue
         seen.add(core)
+        cores.append(c)
+    by_node = collections.OrderedDict()
+    for c in cores:
+        by_node.setdefault(_numa_node(c), []).append(c)
+    home = [v for v in by_node.values() if len(v) >= n]
+    pool = home[0] if home else cores
+    groups = collections.OrderedDict()
+    for c in pool:
         groups.setdefault(_cpu_topology(c, "cache/index3/shared_cpu_list"), []).append(c)
     chosen, lists = [], [list(v) for v in groups.values()]
     while lists and len(chosen) < n:
@@ -123,7 +142,8 @@ def pick_cores(n):
             if g and len(chosen) < n:
                 chosen.append(g.pop(0))
         lists = [g for g in lists if g]
-    return (chosen + spare)[:max(1, n)]
+    rest = [c for c in cores if c not in chosen]
+    return (chosen + rest + spare)[:max(1, n)]
 
 
 def compact_cpus(cpus):
@@ -337,10 +357,10 @@ def cpu_baseline(D, n, reps, dt="f32", skip=None):
                           n * s / 2**20, D * n * s / 2**30, reps)
     bf = ["bf16"] if dt == "bf16" else []
 
-    def run(args, timeout=120, ncores=None):
+    def run(args, timeout=120, ncores=None, pin=True):
         use = cores if ncores is None else cores[:ncores]
         out = subprocess.run([harness] + [str(a) for a in args], capture_output=True, text=True, timeout=timeout,
-                             check=True, **pinned_child(use)).stdout
+                             check=True, **(pinned_child(use) if pin else {})).stdout
         return json.loads(out.strip().splitlines()[-1])
 
     def leg_timeout(cap=90):
@@ -362,6 +382,13 @@ def cpu_baseline(D, n, reps, dt="f32", skip=None):
             res = None
         if res is not None:
             per = {}
+            try:  # the same leg with the threads left to the scheduler, for comparison (not the baseline)
+                ru = run(["bench-fedavg", n, D, len(cores), 5] + bf, timeout=leg_timeout(120), pin=False)
+                res["unpinned"] = {"value": round(ru["gib_s"], 3), "spread": spread(ru.get("rep_s", []), D * n * s),
+                                   "note": "%d threads, no affinity set: the scheduler may spread them over more "
+                                           "cores / sockets than the pinned run's" % len(cores)}
+            except Exception as e:  # noqa: BLE001 -- optional figure
+                print("cpu baseline: unpinned leg not timed (%s)" % e, file=sys.stderr)
             try:
                 r1 = run(["bench-fedavg", n, D, 1, 2] + bf, timeout=leg_timeout(120), ncores=1)
                 res["fedavg_1_core"] = {"value": round(r1["gib_s"], 3), "unit": "GiB/s", "cores": 1,
@@ -1085,6 +1112,8 @@ def compact_line(line, full_record=None):
         out["cpu_baseline"] = {k: cpu[k] for k in CPU_KEYS if k in cpu}
         if isinstance(cpu.get("fedavg_1_core"), dict):
             out["cpu_baseline"]["value_1_core"] = cpu["fedavg_1_core"].get("value")
+        if isinstance(cpu.get("unpinned"), dict):
+            out["cpu_baseline"]["value_unpinned"] = cpu["unpinned"].get("value")
     else:
         out["cpu_baseline"] = cpu
     par = line.get("parity")

@@ -813,22 +813,6 @@ void parallel_ranges(size_t n, size_t grain, const std::function<void(size_t, si
     for (auto& t : th) t.join();
 }
 
-// CRC-32 of a large buffer: per-chunk CRCs in parallel, joined with zlib's crc32_combine.
-uint32_t crc32_parallel(const uint8_t* p, size_t n) {
-    const size_t grain = 8u << 20;
-    if (n < 2 * grain) return crc32(p, n);
-    const size_t chunks = (n + grain - 1) / grain;
-    std::vector<uint32_t> part(chunks);
-    parallel_ranges(chunks, 1, [&](size_t lo, size_t hi) {
-        for (size_t c = lo; c < hi; ++c) {
-            const size_t a = c * grain, len = std::min(grain, n - a);
-            part[c] = crc32(p + a, len);
-        }
-    });
-    uint32_t c = part[0];
-    for (size_t k = 1; k < chunks; ++k) c = (uint32_t)crc32_combine(c, part[k], (z_off_t)std::min(grain, n - k * grain));
-    return c;
-}
 }  // namespace
 
 bool TorchArchive::with_params_into(const float* src, uint8_t* o, std::string* err) const {
@@ -890,12 +874,39 @@ bool TorchArchive::layout_into(uint8_t* o, std::vector<void*>* dsts, std::vector
 }
 
 void TorchArchive::seal_params(uint8_t* o) const {
+    // Every parameter record's CRC-32, all records' chunks in one parallel pass: a reply's records are
+    // mostly a few MB each (ResNet-18's part 2: 37.7 MB in 2.4-9.4 MB records), so sealing them one after
+    // another, each below the parallel threshold, put ~2.6 ms of one core on the end of every C2 phase.
+    constexpr size_t kGrain = 1u << 20;
+    struct Task {
+        int rec;
+        size_t lo, len;
+    };
     std::vector<char> touched(entries_.size(), 0);
     for (auto& t : params_) touched[t.record] = 1;
+    std::vector<Task> tasks;
+    size_t total = 0;
     for (size_t k = 0; k < entries_.size(); ++k) {
         if (!touched[k]) continue;
-        const ZipEntry& z = entries_[k];
-        const uint32_t c = crc32_parallel(o + z.data_offset, z.size);
+        const uint64_t n = entries_[k].size;
+        total += n;
+        for (uint64_t lo = 0; lo < n || (n == 0 && lo == 0); lo += kGrain) {
+            tasks.push_back(Task{(int)k, (size_t)lo, (size_t)std::min<uint64_t>(kGrain, n - lo)});
+            if (n == 0) break;
+        }
+    }
+    std::vector<uint32_t> part(tasks.size());
+    auto run = [&](size_t a, size_t b) {
+        for (size_t i = a; i < b; ++i) part[i] = crc32(o + entries_[tasks[i].rec].data_offset + tasks[i].lo, tasks[i].len);
+    };
+    if (total < 4 * kGrain) run(0, tasks.size());  // a small model: no threads
+    else parallel_ranges(tasks.size(), 1, run);
+    for (size_t i = 0; i < tasks.size();) {  // join each record's chunks in order
+        const int k = tasks[i].rec;
+        uint32_t c = part[i];
+        for (++i; i < tasks.size() && tasks[i].rec == k; ++i)
+            c = (uint32_t)crc32_combine(c, part[i], (z_off_t)tasks[i].len);
+        const ZipEntry& z = entries_[(size_t)k];
         wr32(o + z.cd_offset + 16, c);
         if (z.desc_offset) wr32(o + z.desc_offset, c);   // flag bit 3: CRC lives in the data descriptor
         else wr32(o + z.local_offset + 14, c);           // otherwise in the local header

@@ -118,8 +118,8 @@ def test_line_printer_writes_compact_line_and_full_record(tmp_path):
 
 
 def test_cpu_baseline_cores_spread_over_ccds(monkeypatch):
-    """The CPU legs run pinned on one CPU per physical core, dealt over the L3 domains:
-    a 64-core, 8-CCD, SMT-2 mask gives 16 cores as 2 per CCD and never an SMT sibling."""
+    """The CPU legs run pinned on one CPU per physical core of one NUMA node, dealt over
+    its L3 domains: a 64-core, 8-CCD, SMT-2 mask gives 16 cores as 2 per CCD and never an SMT sibling."""
     import bench
     cpus = list(range(128))  # cpu c and c + 64 are SMT siblings; CCD = (c % 64) // 8
     monkeypatch.setattr(bench.os, "sched_getaffinity", lambda pid: set(cpus))
@@ -130,11 +130,17 @@ def test_cpu_baseline_cores_spread_over_ccds(monkeypatch):
             return "%d,%d" % (core, core + 64)
         return "ccd%d" % (core // 8)
     monkeypatch.setattr(bench, "_cpu_topology", topo)
+    monkeypatch.setattr(bench, "_numa_node", lambda c: 0)
     got = bench.pick_cores(16)
     assert len(set(got)) == 16 and all(c < 64 for c in got)
     assert sorted((c // 8) for c in got) == sorted(list(range(8)) * 2)
     assert bench.pick_cores(1) == [0]
     assert len(bench.pick_cores(100)) == 100  # SMT siblings once every core is taken
+    # two sockets (node = core // 32): 16 cores fit one node, so they all come from node 0's 4 CCDs
+    monkeypatch.setattr(bench, "_numa_node", lambda c: (c % 64) // 32)
+    got = bench.pick_cores(16)
+    assert all((c % 64) < 32 for c in got) and sorted(c // 8 for c in got) == sorted(list(range(4)) * 4)
+    assert len(set(bench.pick_cores(40))) == 40  # more than a node holds: the rest from the other
     assert bench.compact_cpus([0, 1, 2, 3, 8, 16, 17]) == "0-3,8,16-17"
     s = bench.spread([0.5, 0.25, 1.0], 2**30)
     assert s == {"min": 1.0, "median": 2.0, "max": 4.0, "reps": 3}

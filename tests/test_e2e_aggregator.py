@@ -356,14 +356,15 @@ LARGE = ["--model-name", "1", "--start", "9", "--end", "3"]
 def test_streaming_ingest_lenet_random_pieces(torch_gpu, chunks, extra):
     """Streaming ingest: every frame (--stream-min-bytes 1) is DMA'd to its slot record by
     record while it arrives, the owners writing their frames in random pieces of 1 byte to 64 KiB with random
-    pauses, all owners at once, so the frames land interleaved in random order.  From round 1 on (the layout
-    comes from round 0's receipts) receipts are committed from their streams; every reply bit-exact."""
+    pauses, all owners at once, so the frames land interleaved in random order.  Once a bucket's first receipt
+    has given its layout, receipts are committed from their streams; every reply bit-exact."""
     D, rounds = 3, 3
     owner = ["--chunked", chunks] + (["--mode", "literal"] if "literal" in extra else [])
     res, lines, err = _stream_run(os.path.join(GOLDEN, "lenet5_c1"), LENET, D, rounds,
                                   ["--stream-min-bytes", "1"] + extra, owner)
     assert res["ok"] and res["checked_elems"] == rounds * D * (50_536 + 10_164 + 850)
-    assert lines[0]["streamed"] == 0  # round 0: no layout yet
+    # the layout of a bucket comes from its first receipt: later frames of the same round stream already
+    assert lines[0]["streamed"] <= D * 3 - 3
     assert lines[-1]["streamed"] >= (rounds - 1) * D * 3 - 2, lines[-1]  # nearly every later receipt
     assert lines[-1]["stream_fallbacks"] == 0 and lines[-1]["streamed_bytes"] > 0
 

@@ -78,6 +78,27 @@ def test_patched_archive_loads_in_libtorch(cfg, mp, tmp_path):
         assert na == nb and torch.equal(a, b)
 
 
+def test_patched_multi_mb_archive_crcs(tmp_path):
+    """The reply seal on a multi-MB archive (seal_params: every record's CRC-32 in 1 MiB chunks over threads,
+    joined with crc32_combine): records of 0.5-9.4 MB and one empty one, checked by zipfile against zlib."""
+    import torch
+    import torch.nn as nn
+    torch.manual_seed(3)
+    m = nn.Sequential(nn.Linear(1024, 2304), nn.Linear(2304, 1000), nn.Linear(1000, 123), nn.Linear(7, 0))
+    src = str(tmp_path / "big.pt")
+    torch.jit.save(torch.jit.script(m), src)
+    n = json.loads(tool("dump", src))["param_numel"]
+    vals = np.random.default_rng(5).standard_normal(n).astype(np.float32)
+    vals.tofile(tmp_path / "v.f32")
+    tool("patch", src, tmp_path / "v.f32", tmp_path / "out.pt")
+    data = (tmp_path / "out.pt").read_bytes()
+    assert len(data) > 4 << 20
+    assert zipfile.ZipFile(io.BytesIO(data)).testzip() is None
+    got = torch.jit.load(io.BytesIO(data))
+    flat = torch.cat([p.detach().reshape(-1) for _, p in got.named_parameters()])
+    assert np.array_equal(flat.numpy().view(np.uint32), vals.view(np.uint32))
+
+
 def test_frame_round_trip_and_grammar(tmp_path):
     """[int32 len] + Message.h text; `values` is the archive, binary-safe, followed by ',\\n}'."""
     src = os.path.join(GOLDEN, "lenet5_c1", "mp2_client0.pt")
