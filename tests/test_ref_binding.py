@@ -66,3 +66,26 @@ def test_reference_process_with_the_binding_runs_a_lenet_round(torch_gpu, tmp_pa
         log_out.close()
         log_err.close()
     assert "refactor done" in err(), err()
+
+
+REF_CN = os.path.join(ROOT, "oracle", "_ref", "ref_compute_node")
+
+
+@pytest.mark.skipif(not os.access(REF_CN, os.X_OK), reason="oracle/_ref/ref_compute_node not built (needs the "
+                    "reference tree in the build container: make -f oracle/Makefile.ref)")
+@pytest.mark.parametrize("D,spec", [(8, ("1", "1", "4", "8")),    # C2: ResNet-18 split 3,8 -> layers 4..8
+                                    (3, ("2", "0", "2", "5"))])   # LeNet-5's middle layers
+def test_compute_node_binding_on_the_reference_states(torch_gpu, tmp_path, D, spec):
+    """INTEGRATION.md section 5 run for real: the reference's own compute node state --
+    systemAPI(false, id) + refactor() -> init_state_vector (systemAPI.cpp:3-15), one State per data owner
+    with the layers the reference's builders make for the node's part -- aggregated through libfa.so by the
+    binding block extracted verbatim (oracle/_ref/compute_node_fa.cpp).  Every client's every layer must equal
+    the oracle's ordered FedAvg chain over the same values with the binding's weights (n_k differ), bit for
+    bit.  The reference never aggregates a compute node's states (compute_node.cpp:16-84)."""
+    if not ports_free([8080, 8081, 8082, 8083]):
+        pytest.skip("the reference's fixed ports 8080-8083 are in use")
+    r = subprocess.run([REF_CN, str(D)] + list(spec), capture_output=True, text=True, timeout=240, cwd=str(tmp_path))
+    assert r.returncode == 0, (r.stdout[-1000:], r.stderr[-2000:])
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["ok"] and res["mismatches"] == 0 and res["clients"] == D and res["layers"] >= 1
+    assert res["checked_elems"] >= D * res["layer0_elems"] > 0
