@@ -82,7 +82,8 @@ def leg(name, spec, D, agg_cmd, mode, port_base, rounds, blobs, startup_s, extra
         med = lambda f: round(statistics.median(f(p) for p in lines[1:]) * 1e3, 3)  # noqa: E731
         view = {k: med(lambda p, k=k: p[k.split(".")[0]][k.split(".")[1]])
                 for k in ("phase1.receive_s", "phase1.absorb_s", "phase1.reduce_s", "phase2.receive_s",
-                          "phase2.absorb_s", "phase2.reduce_s", "phase2.send_s")}
+                          "phase2.absorb_s", "phase2.reduce_s", "phase2.finalize_s", "phase2.frame_s",
+                          "phase2.send_s")}
     if lines:  # streaming ingest (fa_aggregator, round 6): receipts committed from their streams, cumulative
         view = dict(view or {}, streamed=lines[-1].get("streamed"), stream_fallbacks=lines[-1].get("stream_fallbacks"))
     return {"leg": name, "mode": mode, "ok": res["ok"], "rounds_timed": len(ms), "aggregator_view_ms": view,
