@@ -104,6 +104,11 @@ for s in $STEPS; do
             ok_or_fail $rc "e2e_ref $C"
         done
         kill $HB ;;
+    e2e_c4s)  # C4 at D = 64 through the drop-in, streaming ingest off / on (tools/e2e_bench.py)
+        for A in "--stream-min-bytes 0" ""; do
+            E2E_NO_REF=1 timeout -k 10 600 python tools/e2e_bench.py 64 3 $A >> "$OUT/e2e_c4s.jsonl" 2>> "$OUT/e2e_c4s.err"
+            rc=$?; tail -c 600 "$OUT/e2e_c4s.jsonl"; echo; ok_or_fail $rc "e2e_c4s $A"
+        done ;;
     stream_ab)  # streaming ingest on / off, alternating, C2 and C3 through the drop-in (tools/e2e_ref.py)
         for C in ${STREAM_CFGS:-c2 c3}; do
             for i in 1 2; do
