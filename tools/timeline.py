@@ -4,8 +4,7 @@
   FA_TIMELINE=1 python tools/timeline.py [workloads, default northstar,ns_w2,ns_w4,ns_w8] [launches=8]
 
 The kernel's thread 0 of every workgroup stamps the 100 MHz wall clock at its start, at its arrival at /
-departure from the first and the last meeting (the last phase has none by default: FA_PHASED_LAST_MEET=1
-for a timeline that shows it), and once its stores have completed (fedavg_phased_kernel,
+departure from the first and the last meeting (the last phase has none), and once its stores have completed (fedavg_phased_kernel,
 FA_TIMELINE); fa_diag_phased_timeline copies them out after each launch.  Per workload this prints the
 median over launches of: the start spread (dispatch ramp), the read time to the first meeting (min /
 median / max over workgroups and per XCD = blockIdx % 8), the meeting wait, the last meeting's arrival
@@ -114,7 +113,6 @@ def main():
         if out["meetings"]:
             out["read0_median_per_xcd_us"] = {x: med(["read0_median_per_xcd_us", x]) for x in range(8)}
             out["lds0_median_per_xcd_us"] = {x: med(["lds0_median_per_xcd_us", x]) for x in range(8)}
-        out["skew"] = os.environ.get("FA_PHASED_SKEW", "default")
         if raws:
             out["workgroup_us_per_launch"] = raws
         print(json.dumps(out), flush=True)
