@@ -33,8 +33,7 @@ def main():
         wall, ka, km = bench.timed_loop(torch, s, steps, 5, stream, None, lambda: None)
         print(json.dumps({"W": W, "elems": n // W, "sets": s.nsets, "kernel_ms_avg": round(ka, 4),
                           "kernel_ms_min_per_launch_events": round(min(km), 4), "wall_ms": round(wall / steps * 1e3, 4),
-                          "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / bench.HBM_PEAK_GBS, 4),
-                          "phased_env": os.environ.get("FA_PHASED_MIN_VECS")}), flush=True)
+                          "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / bench.HBM_PEAK_GBS, 4)}), flush=True)
         s.close()
 
 
