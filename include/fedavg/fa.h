@@ -203,6 +203,14 @@ int fa_reduce_parts(fa_ctx* ctx, int n_parts, const int* part_ids, const float* 
  * part has no device output: never reduced, or its last round was read in place straight into a pinned
  * reply (fa_submit_pinned). */
 int fa_copy_output(fa_ctx* ctx, int part_id, void* host_dst);
+/* CRC-32 (zlib's: IEEE 802.3, reflected, initial and final inversion) of consecutive byte segments of the
+ * part's current device output: segment k = bytes [sum_{j<k} bytes[j], + bytes[k]) of the reduced bucket in
+ * its out dtype; the segments cover it exactly.  Computed on the GPU(s) holding the output, from HBM: for the
+ * zip records of a reply built around the reduced parameters (aggregator.cpp:96-101 hands the module to
+ * torch::save, which writes a CRC-32 per record), so the host need not read the reply back.  Waits for the
+ * reduction and returns with the CRCs.  FA_ERR_STATE when the part has no device output (never reduced, or
+ * its last round was read in place straight into a pinned reply). */
+int fa_output_crc32(fa_ctx* ctx, int part_id, int n_segments, const size_t* bytes, uint32_t* crcs);
 /* Wait for all copy and compute work of the ctx. */
 int fa_sync(fa_ctx* ctx);
 

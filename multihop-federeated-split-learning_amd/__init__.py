@@ -84,6 +84,7 @@ def lib():
         "fa_sync_part": (I, [P, I, P, P]),
         "fa_bucket_progress": (I, [P, I, ctypes.POINTER(I), ctypes.POINTER(I)]),
         "fa_bucket_host_read": (I, [P, I, ctypes.POINTER(I)]),
+        "fa_output_crc32": (I, [P, I, I, ctypes.POINTER(S), ctypes.POINTER(U32)]),
         "fa_reduce_parts": (I, [P, I, ctypes.POINTER(I), P, P]),
         "fa_ctx_set_tuning": (I, [P, ctypes.POINTER(_Tuning)]),
         "fa_ctx_get_tuning": (I, [P, ctypes.POINTER(_Tuning)]),
@@ -513,6 +514,14 @@ class Aggregator:
             out = np.empty(n, np.float32 if out_dtype == F32 else np.uint16)
         check(lib().fa_copy_output(self.handle, part_id, out.ctypes.data))
         return out
+
+    def output_crc32(self, part_id, seg_bytes):
+        """fa_output_crc32: zlib CRC-32 of consecutive byte segments of the part's device output (GPU-side)."""
+        n = len(seg_bytes)
+        b = (ctypes.c_size_t * max(1, n))(*seg_bytes)
+        out = (ctypes.c_uint32 * max(1, n))()
+        check(lib().fa_output_crc32(self.handle, part_id, n, b, out))
+        return [out[i] for i in range(n)]
 
     def sync(self):
         check(lib().fa_sync(self.handle))

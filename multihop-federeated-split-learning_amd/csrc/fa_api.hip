@@ -241,6 +241,10 @@ struct GpuRes {
     std::map<hipStream_t, uint64_t> waited;  // per stream: the copy batch it last waited for
     hipEvent_t step_ev = nullptr;  // orders the rs exchange of a piece after its reduction
     void* scratch = nullptr;       // fp32 chain accumulator for bf16-out, D > kMaxClients
+    // fa_output_crc32: the piece table (pinned staging + device copy) and the per-piece results, grown on use
+    char* crc_host = nullptr;
+    char* crc_dev = nullptr;
+    size_t crc_bytes = 0;
     size_t scratch_bytes = 0;
     // Device segment tables of batched launches (fa_reduce_parts beyond the kernel-argument table): a ring,
     // so a changed table is uploaded into a slot whose last launch is long done; each slot remembers the
@@ -1635,6 +1639,8 @@ void fa_destroy(fa_ctx* ctx) {
         for (hipEvent_t e : {r.copy_ev, r.step_ev})
             if (e) (void)hipEventDestroy(e);
         if (r.scratch) (void)hipFree(r.scratch);
+        if (r.crc_host) (void)hipHostFree(r.crc_host);
+        if (r.crc_dev) (void)hipFree(r.crc_dev);
         for (hipStream_t s : {r.compute, r.copy, r.comm})
             if (s) {
                 fa::phased_release_stream(r.dev, s);  // its phased counter slot goes to the next new stream
@@ -1962,6 +1968,105 @@ int fa_reduce_part(fa_ctx* ctx, int part_id, const float* h_weights, void* hip_s
     if (rc) return rc;
     if (hip_stream && ctx->G != 1) return fail(FA_ERR_ARG, "an explicit stream needs a single-GPU ctx");
     return reduce_part(ctx, *p, h_weights ? h_weights : p->w.data(), static_cast<hipStream_t>(hip_stream));
+}
+
+int fa_output_crc32(fa_ctx* ctx, int part_id, int n_segments, const size_t* bytes, uint32_t* crcs) {
+    g_err.clear();
+    Trace tr("fa_output_crc32 part %d n %d", part_id, n_segments);
+    Part* p;
+    int rc = check_part(ctx, part_id, &p);
+    if (rc) return rc;
+    if (n_segments < 0 || (n_segments > 0 && (!bytes || !crcs))) return fail(FA_ERR_ARG, "bad segment list");
+    const size_t so = dsize(p->out);
+    size_t total = 0;
+    for (int k = 0; k < n_segments; ++k) total += bytes[k];
+    if (total != p->n * so)
+        return fail(FA_ERR_ARG, "segments hold %zu bytes, part %d's output %zu", total, part_id, p->n * so);
+    bool any = false;
+    for (auto& rr : p->runs) any = any || !rr.empty();
+    if (!any && p->n) return fail(FA_ERR_STATE, "part %d has no device output", part_id);
+    // segment k = output bytes [seg_lo[k], seg_lo[k] + bytes[k]); each GPU's runs map bucket bytes to its
+    // output buffer: the pieces are their intersections, in segment order on every GPU
+    std::vector<size_t> seg_lo((size_t)n_segments + 1, 0);
+    for (int k = 0; k < n_segments; ++k) seg_lo[(size_t)k + 1] = seg_lo[(size_t)k] + bytes[k];
+    struct Piece {
+        size_t dev_off, len;  // bytes of the GPU's output buffer
+        int seg;
+        size_t end;           // the piece's end, relative to its segment's start
+    };
+    std::vector<std::vector<Piece>> pieces((size_t)ctx->G);
+    for (int g = 0; g < ctx->G; ++g)
+        for (const Run& run : p->runs[(size_t)g]) {
+            const size_t a = run.dst * so, b = (run.dst + run.cnt) * so;  // bucket bytes of this run
+            int k = (int)(std::upper_bound(seg_lo.begin(), seg_lo.end(), a) - seg_lo.begin()) - 1;
+            for (size_t x = a; x < b && k < n_segments; ++k) {
+                const size_t e = std::min(b, seg_lo[(size_t)k + 1]);
+                if (e > x) pieces[(size_t)g].push_back(Piece{run.src * so + (x - a), e - x, k, e - seg_lo[(size_t)k]});
+                x = std::max(x, e);
+            }
+        }
+    std::vector<uint32_t> raw;  // R(piece, 0) per piece, all GPUs in order
+    for (int g = 0; g < ctx->G; ++g) {
+        auto& pc = pieces[(size_t)g];
+        if (pc.empty()) continue;
+        GpuRes& r = ctx->gpu[(size_t)g];
+        DeviceGuard dg(r.dev);
+        const size_t np = pc.size();
+        const size_t need = np * 16 + (np + 1) * 8 + np * 4 + 64;
+        if (r.crc_bytes < need) {
+            if (r.crc_host) (void)hipHostFree(r.crc_host);
+            if (r.crc_dev) (void)hipFree(r.crc_dev);
+            r.crc_host = r.crc_dev = nullptr;
+            r.crc_bytes = 0;
+            const size_t cap = std::max<size_t>(need, 64u << 10);
+            if (hipHostMalloc((void**)&r.crc_host, cap, hipHostMallocDefault) != hipSuccess ||
+                hipMalloc((void**)&r.crc_dev, cap) != hipSuccess) {
+                (void)hipGetLastError();
+                if (r.crc_host) (void)hipHostFree(r.crc_host);
+                r.crc_host = nullptr;
+                return fail(FA_ERR_NOMEM, "crc table allocation failed");
+            }
+            r.crc_bytes = cap;
+        }
+        uint64_t* h_off = reinterpret_cast<uint64_t*>(r.crc_host);
+        uint64_t* h_len = h_off + np;
+        uint64_t* h_chunk0 = h_len + np;
+        uint32_t* h_out = reinterpret_cast<uint32_t*>(h_chunk0 + np + 1);
+        uint64_t chunks = 0;
+        for (size_t i = 0; i < np; ++i) {
+            h_off[i] = pc[i].dev_off;
+            h_len[i] = pc[i].len;
+            h_chunk0[i] = chunks;
+            chunks += (pc[i].len + fa::kCrcChunkBytes - 1) / fa::kCrcChunkBytes;
+        }
+        h_chunk0[np] = chunks;
+        const size_t table = (np * 2 + np + 1) * 8;
+        uint64_t* d_off = reinterpret_cast<uint64_t*>(r.crc_dev);
+        uint32_t* d_out = reinterpret_cast<uint32_t*>(d_off + np * 3 + 1);
+        // after the reduction that wrote the output (on whatever stream it ran)
+        hipStream_t ds = p->done_stream[(size_t)g];
+        if (ds && ds != r.compute) {
+            FA_HIP(hipEventRecord(p->done[(size_t)g], ds));
+            FA_HIP(hipStreamWaitEvent(r.compute, p->done[(size_t)g], 0));
+        }
+        FA_HIP(hipMemcpyAsync(d_off, h_off, table, hipMemcpyHostToDevice, r.compute));
+        FA_HIP(hipMemsetAsync(d_out, 0, np * 4, r.compute));
+        FA_HIP(fa::launch_crc32_pieces(p->run_src[(size_t)g], d_off, d_off + np, d_off + 2 * np, (int)np, chunks, d_out,
+                                       r.compute));
+        FA_HIP(hipMemcpyAsync(h_out, d_out, np * 4, hipMemcpyDeviceToHost, r.compute));
+        FA_HIP(hipStreamSynchronize(r.compute));
+        raw.insert(raw.end(), h_out, h_out + np);
+    }
+    // join a segment's pieces: R(seg, ~0) = shift(~0, L) ^ XOR_i shift(R(piece_i, 0), L - end_i); CRC = ~R
+    for (int k = 0; k < n_segments; ++k) crcs[k] = fa::crc32_mulmod(fa::crc32_x8n(bytes[k]), 0xFFFFFFFFu);
+    size_t i = 0;
+    for (int g = 0; g < ctx->G; ++g)
+        for (const Piece& pc : pieces[(size_t)g]) {
+            const size_t L = bytes[pc.seg];
+            crcs[pc.seg] ^= fa::crc32_mulmod(fa::crc32_x8n(L - pc.end), raw[i++]);
+        }
+    for (int k = 0; k < n_segments; ++k) crcs[k] = ~crcs[k];
+    return FA_OK;
 }
 
 int fa_copy_output(fa_ctx* ctx, int part_id, void* host_dst) {

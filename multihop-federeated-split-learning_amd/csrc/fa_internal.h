@@ -50,6 +50,16 @@ struct Tuning {
                       // for buckets smaller than one phase), 4 phased with the larger register stage
 };
 
+// CRC-32 of byte ranges of device memory (the reply's zip records): piece i = [base + off[i], + len[i]),
+// chunk0 the prefix count of its 256-byte chunks (np + 1 entries, chunks = chunk0[np]); out[i] (zeroed by the
+// caller) gets R(piece i, 0), the CRC register over the piece from 0, without the inversions.  Device arrays.
+hipError_t launch_crc32_pieces(const void* base, const uint64_t* d_off, const uint64_t* d_len, const uint64_t* d_chunk0,
+                               int np, uint64_t chunks, uint32_t* d_out, hipStream_t s);
+constexpr uint64_t kCrcChunkBytes = 256;
+// Host side of the same algebra: a * b mod P (reflected) and x^(8 n) mod P.
+uint32_t crc32_mulmod(uint32_t a, uint32_t b);
+uint32_t crc32_x8n(uint64_t n);
+
 hipError_t launch_chain(const ClientTable& t, int nc, fa_dtype in, fa_dtype out, const float* init, void* dst,
                         int64_t head, int64_t nvec, int64_t n, bool vector_ok, const Tuning& tu, hipStream_t s);
 // Meetings of the phased kernel on device `dev` that gave up waiting (the grid was not co-resident).

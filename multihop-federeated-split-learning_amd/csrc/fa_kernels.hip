@@ -1332,4 +1332,114 @@ hipError_t launch_fill(void* dst, int64_t n, fa_dtype dt, uint64_t seed, uint32_
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ CRC-32 of output byte ranges
+//
+// The reply of a phase is the last receipt's zip archive around the reduced parameters, and every parameter
+// record carries the CRC-32 of its bytes (torch::save's zip, which torch::load on the data owner checks,
+// data_owner.cpp:232-253).  Those bytes are the part's device output, so their CRCs are computed here, from
+// HBM, instead of by the host reading the reply back after its D2H (C2: 37.7 MB, ~0.7 ms of host time per
+// phase; C4's FC reply 478 MB).  zlib's CRC-32 (reflected IEEE 802.3 polynomial) is linear: with R(M, r) the
+// register after message M from register r, R(A || B, r) = R(B, 0) ^ shift(R(A, r), |B|), where shift(c, n)
+// = c * x^(8n) mod P.  So every lane takes one 256-byte chunk of a piece, computes R(chunk, 0) with a byte
+// table in LDS and shifts it by the bytes after the chunk in its piece; the XOR of a piece's lanes is
+// R(piece, 0) (one wave reduction and one atomic XOR per wave when its lanes share a piece, which they do
+// but at piece edges).  The host joins the pieces of a segment and applies the initial and final inversion.
+namespace {
+
+constexpr uint32_t kCrcPoly = 0xEDB88320u;
+constexpr int kCrcChunk = 256;
+
+// a(x) * b(x) mod P in the reflected representation (bit 31 = x^0), 32 fixed steps
+__host__ __device__ constexpr uint32_t crc_mulmod(uint32_t a, uint32_t b) {
+    uint32_t p = 0;
+    for (int i = 0; i < 32; ++i) {
+        if (a & (0x80000000u >> i)) p ^= b;
+        b = (b & 1u) ? (b >> 1) ^ kCrcPoly : b >> 1;
+    }
+    return p;
+}
+
+struct CrcX2n {  // t[k] = x^(2^k) mod P
+    uint32_t t[64];
+    constexpr CrcX2n() : t() {
+        uint32_t p = 1u << 30;  // x^1
+        t[0] = p;
+        for (int k = 1; k < 64; ++k) t[k] = p = crc_mulmod(p, p);
+    }
+};
+__constant__ CrcX2n kCrcX2n;
+
+// x^(8 n) mod P: the multiplier that moves a CRC register over n zero bytes
+__device__ inline uint32_t crc_x8n(uint64_t n) {
+    uint32_t p = 0x80000000u;  // x^0
+    for (int k = 3; n; n >>= 1, ++k)
+        if (n & 1) p = crc_mulmod(kCrcX2n.t[k], p);
+    return p;
+}
+
+__global__ __launch_bounds__(256) void crc32_pieces_kernel(const uint8_t* __restrict__ base,
+                                                           const uint64_t* __restrict__ off,
+                                                           const uint64_t* __restrict__ len,
+                                                           const uint64_t* __restrict__ chunk0, int np,
+                                                           uint32_t* __restrict__ out) {
+    __shared__ uint32_t tab[256];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+        uint32_t c = (uint32_t)i;
+        for (int k = 0; k < 8; ++k) c = (c & 1u) ? (c >> 1) ^ kCrcPoly : c >> 1;
+        tab[i] = c;
+    }
+    __syncthreads();
+    const uint64_t total = chunk0[np];
+    const int lane = threadIdx.x & 63;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    // wave-uniform trip count: every lane of a wave runs every iteration (the shuffles need all 64)
+    for (uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); g0 < total; g0 += stride) {
+        const uint64_t g = g0 + lane;
+        int p = -1;
+        uint32_t r = 0;
+        if (g < total) {
+            int lo = 0, hi = np - 1;  // the piece whose chunks hold chunk g
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (chunk0[mid] <= g) lo = mid;
+                else hi = mid - 1;
+            }
+            p = lo;
+            const uint64_t a = (g - chunk0[p]) * kCrcChunk, L = len[p];
+            const uint64_t e = a + kCrcChunk < L ? a + kCrcChunk : L;
+            const uint8_t* q = base + off[p] + a;
+            for (uint64_t i = 0; i < e - a; ++i) r = tab[(r ^ q[i]) & 0xFFu] ^ (r >> 8);
+            r = crc_mulmod(crc_x8n(L - e), r);
+        }
+        const int p0 = __shfl(p, 0);
+        if (__all(p == p0)) {
+            for (int o = 32; o > 0; o >>= 1) r ^= __shfl_xor(r, o);
+            if (lane == 0 && p0 >= 0) atomicXor(out + p0, r);
+        } else if (p >= 0) {
+            atomicXor(out + p, r);
+        }
+    }
+}
+
+}  // namespace
+
+uint32_t crc32_mulmod(uint32_t a, uint32_t b) { return crc_mulmod(a, b); }
+
+uint32_t crc32_x8n(uint64_t n) {
+    static constexpr CrcX2n x2n;
+    uint32_t p = 0x80000000u;
+    for (int k = 3; n; n >>= 1, ++k)
+        if (n & 1) p = crc_mulmod(x2n.t[k], p);
+    return p;
+}
+
+hipError_t launch_crc32_pieces(const void* base, const uint64_t* d_off, const uint64_t* d_len, const uint64_t* d_chunk0,
+                               int np, uint64_t chunks, uint32_t* d_out, hipStream_t s) {
+    if (np <= 0 || chunks == 0) return hipSuccess;
+    const uint64_t blocks = std::min<uint64_t>((chunks + 255) / 256, 4096);
+    hipLaunchKernelGGL(crc32_pieces_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
+                       static_cast<const uint8_t*>(base), d_off, d_len, d_chunk0, np, d_out);
+    return hipGetLastError();
+}
+
 }  // namespace fa

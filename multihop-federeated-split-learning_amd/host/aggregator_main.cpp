@@ -164,6 +164,10 @@ double secs_since(std::chrono::steady_clock::time_point t) {
         }                                                                                    \
     } while (0)
 
+// Replies of at least this many parameter bytes get their records' CRC-32s from the GPU (fa_output_crc32);
+// smaller ones are sealed on the host, which takes less than the call's round trip.
+constexpr size_t kGpuCrcMinBytes = 1u << 20;
+
 class Aggregator {
 public:
     Aggregator(const Options& o, NetLayer* net, const std::vector<int>& owners) : o_(o), net_(net) {
@@ -371,8 +375,13 @@ public:
             const auto t1 = std::chrono::steady_clock::now();
             FA_CHECK(fa_finalize_gather(ctx_, mp, (int)dsts.size(), dsts.data(), bytes.data(),
                                         f->pinned ? FA_HOST_PINNED : 0));
+            // the records' CRC-32s from the reduced bucket on the GPU (a few us; the host would read the
+            // whole reply back); a part read in place into its reply has no device output: the host seals it
+            std::vector<uint32_t> crcs(dsts.size());
+            const bool gpu_crc = !bytes.empty() && b.numel * (size_t)b.elem >= kGpuCrcMinBytes &&
+                                 fa_output_crc32(ctx_, mp, (int)bytes.size(), bytes.data(), crcs.data()) == FA_OK;
             t_fin = secs_since(t1);
-            ar.seal_params((uint8_t*)values);
+            if (!gpu_crc || !ar.seal_params_with((uint8_t*)values, crcs.data())) ar.seal_params((uint8_t*)values);
         } else {  // strided parameters: through a flat copy
             const auto t1 = std::chrono::steady_clock::now();
             std::vector<uint8_t> out(b.numel * (size_t)b.elem);

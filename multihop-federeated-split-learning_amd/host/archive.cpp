@@ -927,6 +927,25 @@ bool TorchArchive::layout_into(uint8_t* o, std::vector<void*>* dsts, std::vector
     return true;
 }
 
+bool TorchArchive::seal_params_with(uint8_t* o, const uint32_t* crcs) const {
+    const int es = param_elem_size();
+    if (!es) return false;
+    std::vector<char> seen(entries_.size(), 0);
+    for (auto& t : params_) {  // one parameter per record, covering all of it
+        if (t.record < 0 || seen[t.record]) return false;
+        seen[t.record] = 1;
+        const ZipEntry& z = entries_[(size_t)t.record];
+        if (t.data != base_ + z.data_offset || (uint64_t)t.numel * (uint64_t)es != z.size) return false;
+    }
+    for (size_t i = 0; i < params_.size(); ++i) {
+        const ZipEntry& z = entries_[(size_t)params_[i].record];
+        wr32(o + z.cd_offset + 16, crcs[i]);
+        if (z.desc_offset) wr32(o + z.desc_offset, crcs[i]);
+        else wr32(o + z.local_offset + 14, crcs[i]);
+    }
+    return true;
+}
+
 void TorchArchive::seal_params(uint8_t* o) const {
     // Every parameter record's CRC-32, all records' chunks in one parallel pass: a reply's records are
     // mostly a few MB each (ResNet-18's part 2: 37.7 MB in 2.4-9.4 MB records), so sealing them one after

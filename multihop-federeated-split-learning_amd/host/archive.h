@@ -80,6 +80,10 @@ public:
     bool layout_into(uint8_t* dst, std::vector<void*>* param_dsts, std::vector<size_t>* param_bytes,
                      std::string* err) const;
     void seal_params(uint8_t* dst) const;
+    // The same with the CRC-32s given, one per parameter in named_parameters order (e.g. computed on the GPU
+    // from the reduced bucket, fa_output_crc32); false -- nothing written -- unless every parameter fills
+    // its record exactly (the record's bytes are the parameter's, so the given CRC is the record's).
+    bool seal_params_with(uint8_t* dst, const uint32_t* crcs) const;
     size_t size() const { return size_; }
     // Parses that took their tensor views from the layout cache (an archive with the same structure, pickle
     // and code records as one parsed before: every receipt of a bucket), process-wide.

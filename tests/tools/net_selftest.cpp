@@ -25,6 +25,8 @@
 #include <thread>
 #include <vector>
 
+#include <zlib.h>
+
 #include "archive.h"
 #include "net.h"
 
@@ -348,6 +350,23 @@ int main(int argc, char** argv) {
         if (one != two) {
             std::cerr << "layout_into + seal_params differs from with_params_into\n";
             ok = false;
+        }
+        // the same seal from CRC-32s computed elsewhere (fa_output_crc32 on the GPU; here zlib's, per parameter)
+        std::vector<uint8_t> three(ar.size(), 0xCD);
+        std::vector<void*> d3;
+        std::vector<size_t> b3;
+        if (ar.layout_into(three.data(), &d3, &b3, &err)) {
+            std::vector<uint32_t> crcs;
+            const float* v = vals.data();
+            for (size_t k = 0; k < d3.size(); ++k) {
+                std::memcpy(d3[k], v, b3[k]);
+                crcs.push_back((uint32_t)::crc32(0, (const Bytef*)v, (uInt)b3[k]));
+                v += b3[k] / 4;
+            }
+            if (!ar.seal_params_with(three.data(), crcs.data()) || three != one) {
+                std::cerr << "seal_params_with differs from with_params_into\n";
+                ok = false;
+            }
         }
         checked_archive = ar.size();
     }
