@@ -42,6 +42,8 @@
 #include <thread>
 #include <vector>
 
+#include <zlib.h>
+
 #include "archive.h"
 #include "fa_oracle.h"
 #include "net.h"
@@ -497,6 +499,27 @@ int main(int argc, char** argv) {
             checked += p->n;
             // buffers are the last receipt's (template buffers are identical for every client here)
             if (ar.buffers().size() != p->ar.buffers().size()) ok = false;
+            // every parameter record's CRC-32 as torch::load checks it: the central directory's and the local
+            // header's (or data descriptor's) against zlib over the record's bytes (the aggregator seals them,
+            // from the GPU for large replies: fa_output_crc32)
+            for (auto& t : ar.params()) {
+                const ZipEntry& z = ar.entries()[(size_t)t.record];
+                const uint8_t* rb = r.blob();
+                uLong c = ::crc32(0L, Z_NULL, 0);
+                for (uint64_t o = 0; o < z.size;) {  // zlib takes uInt lengths
+                    const uInt take = (uInt)std::min<uint64_t>(z.size - o, 1u << 30);
+                    c = ::crc32(c, rb + z.data_offset + o, take);
+                    o += take;
+                }
+                uint32_t local = 0;
+                std::memcpy(&local, rb + (z.desc_offset ? z.desc_offset : z.local_offset + 14), 4);
+                if ((uint32_t)c != z.crc || local != z.crc) {
+                    std::cerr << "reply for part " << p->mp << ": record " << z.name << " CRC-32 "
+                              << std::hex << z.crc << "/" << local << " but its bytes give " << (uint32_t)c << std::dec
+                              << "\n";
+                    ok = false;
+                }
+            }
         }
     }
     printf("{\"ok\": %s, \"rounds\": %d, \"data_owners\": %d, \"checked_elems\": %zu, \"round_ms\": [", ok ? "true" : "false",
