@@ -215,6 +215,7 @@ CPU_RECEIVE_LOOPS = [
 # process -- the reference's own CPU path (oracle/_ref/ref_cpu_aggregator: its systemAPI / network_layer with
 # aggregator.cpp:55-167 on CPU libtorch) or the drop-in fa_aggregator.  Owner view: first send to last reply.
 C1_E2E_ROUNDS = 40
+C2_E2E_ROUNDS = 8
 FAKE_OWNERS = os.path.join(ROOT, "tests", "tools", "bin", "fa_fake_owners")
 FA_AGGREGATOR = os.path.join(PKG_DIR, "bin", "fa_aggregator")
 REF_CPU_AGGREGATOR = os.path.join(ROOT, "oracle", "_ref", "ref_cpu_aggregator")
@@ -243,20 +244,33 @@ def free_port_base():
     raise RuntimeError("no free port range")
 
 
+# The model arguments the fake owners send in the refactor message: (--model-name, --model-type, --start, --end)
+C1_MODEL = ("2", "0", "6", "1")   # LeNet-5 split 6,1
+C2_MODEL = ("1", "1", "9", "3")   # ResNet-18 split 3,8 (the ref_harness golden spec of tools/e2e_ref.py)
+
+
 def e2e_c1(agg_cmd, mode, port_base, rounds=C1_E2E_ROUNDS, startup_s=0.5, timeout=120, owner_flags=()):
     """Rounds of BASELINE C1 (LeNet-5, D = 2, fp32) through one aggregator process over loopback; returns the
     owners' round times (round 0, which allocates, reported apart) and their bit-exact check of every reply."""
-    golden = os.path.join(ROOT, "tests", "golden", "lenet5_c1")
-    with tempfile.TemporaryDirectory(prefix="fa_c1_") as tmp:  # the reference process writes its logs in cwd
+    return e2e_run(agg_cmd, mode, port_base, os.path.join(ROOT, "tests", "golden", "lenet5_c1"), 2, C1_MODEL,
+                   rounds, startup_s, timeout, owner_flags)
+
+
+def e2e_run(agg_cmd, mode, port_base, blobs, D, model, rounds, startup_s=0.5, timeout=120, owner_flags=()):
+    """Rounds of one config (templates mp1..3_client0.pt in `blobs`, D owners) through one aggregator process
+    over loopback against the fake owners, who check every element and every record CRC of every reply."""
+    golden = blobs
+    with tempfile.TemporaryDirectory(prefix="fa_e2e_") as tmp:  # the reference process writes its logs in cwd
         agg_out = open(os.path.join(tmp, "agg.out"), "w+")
         agg = subprocess.Popen(agg_cmd, stdout=agg_out, stderr=subprocess.DEVNULL, cwd=tmp, start_new_session=True)
         try:
             time.sleep(startup_s)
             if agg.poll() is not None:
                 raise RuntimeError("aggregator exited early (rc %s)" % agg.returncode)
-            r = subprocess.run([FAKE_OWNERS, "--blobs", golden, "--parts", "1,2,3", "-d", "2", "-c", "1",
-                                "--rounds", str(rounds), "--port-base", str(port_base), "--model-name", "2",
-                                "--start", "6", "--end", "1", "--mode", mode, "--reply-timeout", "30"] + list(owner_flags),
+            r = subprocess.run([FAKE_OWNERS, "--blobs", golden, "--parts", "1,2,3", "-d", str(D), "-c", "1",
+                                "--rounds", str(rounds), "--port-base", str(port_base), "--model-name", model[0],
+                                "--model-type", model[1], "--start", model[2], "--end", model[3], "--mode", mode,
+                                "--reply-timeout", "30"] + list(owner_flags),
                                capture_output=True, text=True, timeout=timeout, cwd=tmp)
         finally:
             if agg.poll() is None:
@@ -283,6 +297,7 @@ def e2e_c1(agg_cmd, mode, port_base, rounds=C1_E2E_ROUNDS, startup_s=0.5, timeou
         med = lambda f: round(statistics.median(f(p) for p in phases[1:]) * 1e3, 4)  # noqa: E731
         server = {"phase1_reduce_ms": med(lambda p: p["phase1"]["reduce_s"]),
                   "phase2_reduce_ms": med(lambda p: p["phase2"]["reduce_s"]),
+                  "streamed": phases[-1].get("streamed"),
                   "phase2_send_ms": med(lambda p: p["phase2"]["send_s"]),
                   "absorb_ms": med(lambda p: p["phase1"]["absorb_s"] + p["phase2"]["absorb_s"]),
                   "note": "medians over rounds 1.. of the aggregator's own round lines: reduce = the batched GPU "
@@ -1049,6 +1064,7 @@ LEG_KEYS = (("gib_s", "gib_s"), ("frac", "frac"), ("kernel_ms_avg", "ms"), ("rou
             ("cpu_gib_s", "cpu_gib_s"), ("gpus", "gpus"), ("h2d_ms", "h2d_ms"), ("reduce_ms", "reduce_ms"),
             ("d2h_ms", "d2h_ms"), ("pcie_GBs", "pcie_GBs"))
 E2E_KEYS = (("e2e_loopback_literal", "e2e_literal_ms"), ("e2e_loopback_fedavg", "e2e_fedavg_ms"),
+            ("e2e_loopback_fedavg_no_streaming", "e2e_fedavg_nostream_ms"),
             ("e2e_loopback_reference_process_with_binding", "e2e_ref_binding_ms"), ("cpu_e2e_loopback", "cpu_e2e_ms"))
 
 
@@ -1094,6 +1110,11 @@ def compact_leg(v):
                 out[dst] = e.get("round_ms_median")
                 p = e.get("parity")
                 out["e2e_parity_ok"] = out.get("e2e_parity_ok", True) and bool(p and p.get("ok"))
+                view = e.get("aggregator_view") or {}
+                if "fedavg" in src and view.get("phase2_reduce_ms") is not None:  # the phase-2 tail
+                    out[dst.replace("_ms", "_tail_ms")] = view["phase2_reduce_ms"]
+    if v.get("e2e_error"):
+        out["e2e_error"] = True
     return out
 
 
@@ -1752,6 +1773,27 @@ def single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier):
                          "libfa.so (oracle/_ref/ref_aggregator)")
             except Exception as e:  # noqa: BLE001
                 c1["e2e_loopback_reference_process_with_binding"] = {"error": repr(e)[:300]}
+
+    # BASELINE C2 end to end through the drop-in (FedAvg, 8 owners at once, ResNet-18 receipts made by the
+    # reference's builders): the owner-view round and the phase-2 tail (last receipt -> replies framed), with
+    # streaming ingest (the default) and without it (--stream-min-bytes 0)
+    harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if os.access(FA_AGGREGATOR, os.X_OK) and os.access(FAKE_OWNERS, os.X_OK) and os.access(harness, os.X_OK) \
+            and budget_left() > 90:
+        c2 = sec.setdefault("round_c2", {})
+        try:
+            with tempfile.TemporaryDirectory(prefix="fa_c2_blobs_") as blobs:
+                for mp in ("-1", "2"):  # the reference's ResNet-18 parts saved by torch::save (client 0's)
+                    subprocess.run([harness, "golden", "1", "1", "9", "3", "10", "1", "24301", "7", blobs, mp],
+                                   check=True, capture_output=True, timeout=120)
+                for stream in (True, False):
+                    base = free_port_base()
+                    c2["e2e_loopback_fedavg" + ("" if stream else "_no_streaming")] = e2e_run(
+                        [FA_AGGREGATOR, "-i", "-1", "-d", "8", "-c", "1", "--rounds", str(C2_E2E_ROUNDS),
+                         "--port-base", str(base)] + ([] if stream else ["--stream-min-bytes", "0"]),
+                        "fedavg", base, blobs, 8, C2_MODEL, C2_E2E_ROUNDS, timeout=180, owner_flags=["--routing-table"])
+        except Exception as e:  # noqa: BLE001
+            c2["e2e_error"] = repr(e)[:300]
 
     def one(key, s, desc):
         torch.cuda.synchronize()

@@ -75,7 +75,16 @@ def test_eight_gpu_node_n1_line_compacts():
     sec["ctx_rs_c4_4gpu_rschunks16"] = {"error": "rc 1: " + "x" * 300}
     sec["ns_h2d"] = {"gib_s": 50.1, "ms_per_round": 166.0, "h2d_ms": 160.1, "reduce_ms": 1.3, "d2h_ms": 4.6,
                      "pcie_GBs": 55.0, "parity": {"ok": True, "samples": 1026}, "description": "y" * 300}
+    e2e = {"aggregator_view": {"phase1_reduce_ms": 0.4, "phase2_reduce_ms": 1.3, "streamed": 63, "note": "z" * 200},
+           "rounds_timed": 7, "round_ms_median": 25.1, "parity": {"ok": True, "samples": 10}}
+    sec["round_c2"]["e2e_loopback_fedavg"] = e2e
+    sec["round_c2"]["e2e_loopback_fedavg_no_streaming"] = dict(e2e, round_ms_median=27.0,
+                                                                aggregator_view=dict(e2e["aggregator_view"],
+                                                                                     phase2_reduce_ms=7.2))
     got = _check(line, bench)
+    c2 = got["secondary"]["round_c2"]
+    assert c2["e2e_fedavg_ms"] == 25.1 and c2["e2e_fedavg_tail_ms"] == 1.3
+    assert c2["e2e_fedavg_nostream_ms"] == 27.0 and c2["e2e_fedavg_nostream_tail_ms"] == 7.2 and c2["e2e_parity_ok"]
     err = got["secondary"]["ctx_rs_c4_4gpu_rschunks16"]["error"]
     assert err.startswith("rc 1: x") and len(err) <= 80
     assert got["secondary"]["ns_h2d"]["h2d_ms"] == 160.1
