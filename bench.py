@@ -76,6 +76,11 @@ def budget_left():
     return T_START + BUDGET_S - time.monotonic()
 
 
+def progress(msg):
+    """A progress line on stderr (the run's legs, with the time since start): stdout carries the one line."""
+    print("bench [%6.1f s] %s" % (time.monotonic() - T_START, msg), file=sys.stderr, flush=True)
+
+
 def load_pkg():
     if "mhfsl_amd" in sys.modules:
         return sys.modules["mhfsl_amd"]
@@ -961,6 +966,8 @@ def timed_loop(torch, setup, steps, warmup, stream, dist, barrier, per_launch=10
     between steps (an event pair per step added 7-12 us of wall time per step, gpurun_out r02s71).
     kern_ms: per-launch event pairs from a separate loop of `per_launch` steps after the timed region
     (kernel_ms_min / _median)."""
+    if not hasattr(stream, "cuda_stream"):  # Event.record on a non-stream crashes inside the HIP runtime
+        raise TypeError("timed_loop needs a torch.cuda.Stream, got %r" % (stream,))
     for i in range(warmup):
         setup.launch(i, stream)
     torch.cuda.synchronize()
@@ -1706,10 +1713,12 @@ def ctx_multi_secondaries(n_dev, deadline, timeout=120):
 def single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier):
     """The other BASELINE configs' single-GPU shapes, compute-node sync and literal mode (rank 0, N = 1)."""
     sec = {}
+    skip = set(os.environ.get("FA_BENCH_SKIP", "").split(","))  # diagnostics: legs left out of this run
     for name in sorted(WORKLOADS):
-        if name == args.workload:
+        if name == args.workload or "workloads" in skip:
             continue
         sD, sn, si, so, sdesc = WORKLOADS[name]
+        progress("workload " + name)
         s = Setup(fa, torch, sD, sn, si, so, 0, device)
         torch.cuda.synchronize()
         w2, ka, _ = timed_loop(torch, s, max(10, args.steps), 3, stream, dist, barrier)
@@ -1733,8 +1742,9 @@ def single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier):
 
     # the buckets of one aggregator round as it forms them: per-round device time and roofline fraction,
     # phase 2 batched (fa_reduce_parts) and, for comparison, one launch per part
-    for name in sorted(ROUNDS):
+    for name in sorted(ROUNDS) if "rounds" not in skip else []:
         for batched in (True, False):
+            progress("round %s%s" % (name, "" if batched else " unbatched"))
             s = RoundSetup(fa, torch, name, device, batched=batched)
             torch.cuda.synchronize()
             w2, ka, _ = timed_loop(torch, s, max(10, args.steps), 3, stream, dist, barrier)
@@ -1751,8 +1761,9 @@ def single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier):
     # BASELINE C1 end to end: the drop-in process fa_aggregator on this GPU against the fake owners over
     # loopback, FedAvg (owners at once) and the reference-literal mode (owners in turn, as the CPU reference
     # leg runs); both checked reply by reply against the oracle
-    if os.access(FA_AGGREGATOR, os.X_OK) and os.access(FAKE_OWNERS, os.X_OK):
+    if os.access(FA_AGGREGATOR, os.X_OK) and os.access(FAKE_OWNERS, os.X_OK) and "c1e2e" not in skip:
         c1 = sec.setdefault("round_c1", {})
+        progress("C1 end to end")
         for mode in ("fedavg", "literal"):
             try:
                 base = free_port_base()
@@ -1779,23 +1790,26 @@ def single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier):
     # streaming ingest (the default) and without it (--stream-min-bytes 0)
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
     if os.access(FA_AGGREGATOR, os.X_OK) and os.access(FAKE_OWNERS, os.X_OK) and os.access(harness, os.X_OK) \
-            and budget_left() > 90:
+            and budget_left() > 90 and "c2e2e" not in skip:
         c2 = sec.setdefault("round_c2", {})
+        progress("C2 end to end")
         try:
             with tempfile.TemporaryDirectory(prefix="fa_c2_blobs_") as blobs:
                 for mp in ("-1", "2"):  # the reference's ResNet-18 parts saved by torch::save (client 0's)
                     subprocess.run([harness, "golden", "1", "1", "9", "3", "10", "1", "24301", "7", blobs, mp],
                                    check=True, capture_output=True, timeout=120)
-                for stream in (True, False):
+                for streamed in (True, False):
                     base = free_port_base()
-                    c2["e2e_loopback_fedavg" + ("" if stream else "_no_streaming")] = e2e_run(
+                    c2["e2e_loopback_fedavg" + ("" if streamed else "_no_streaming")] = e2e_run(
                         [FA_AGGREGATOR, "-i", "-1", "-d", "8", "-c", "1", "--rounds", str(C2_E2E_ROUNDS),
-                         "--port-base", str(base)] + ([] if stream else ["--stream-min-bytes", "0"]),
+                         "--port-base", str(base)] + ([] if streamed else ["--stream-min-bytes", "0"]) +
+                        os.environ.get("FA_BENCH_C2_AGG_ARGS", "").split(),
                         "fedavg", base, blobs, 8, C2_MODEL, C2_E2E_ROUNDS, timeout=180, owner_flags=["--routing-table"])
         except Exception as e:  # noqa: BLE001
             c2["e2e_error"] = repr(e)[:300]
 
     def one(key, s, desc):
+        progress(key)
         torch.cuda.synchronize()
         _, ka, _ = timed_loop(torch, s, max(10, args.steps), 3, stream, dist, barrier)
         sec[key] = {"description": desc, "kernel_ms_avg": round(ka, 4),

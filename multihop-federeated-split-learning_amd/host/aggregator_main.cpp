@@ -68,6 +68,7 @@ struct Options {
     // streaming ingest: receipt frames of at least this many bytes go to their slot record by record while
     // they arrive (NetLayer::set_streaming; pinned frames only); 0 = off
     size_t stream_min = 1u << 20;
+    bool gpu_crc = true;  // --crc gpu|host: the reply records' CRC-32s from the GPU (fa_output_crc32) or the host
     std::map<int, double> samples;  // client id -> n_k
 };
 
@@ -76,7 +77,7 @@ void usage() {
                  "       [--rounds R] [--port-base P] [--discover] [--link-mbps M] [--samples id:n,...]\n"
                  "       [--divisor K] [--last-layers L] [--no-pinned] [--layout range|rs] [--rs-chunks C]\n"
                  "       [--eager] [--stall-report S] [--receipt-timeout S] [--rx-concurrency K]\n"
-                 "       [--senders S] [--stream-min-bytes N] [--test-shared-device]\n";
+                 "       [--senders S] [--stream-min-bytes N] [--crc gpu|host] [--test-shared-device]\n";
 }
 
 bool parse_args(int argc, char** argv, Options* o) {
@@ -107,6 +108,11 @@ bool parse_args(int argc, char** argv, Options* o) {
         else if (a == "--rx-concurrency") o->rx_concurrency = std::atoi(val("--rx-concurrency"));
         else if (a == "--senders") o->senders = std::atoi(val("--senders"));
         else if (a == "--stream-min-bytes") o->stream_min = (size_t)std::strtoull(val("--stream-min-bytes"), nullptr, 0);
+        else if (a == "--crc") {
+            std::string c = val("--crc");
+            if (c == "host") o->gpu_crc = false;
+            else if (c != "gpu") return false;
+        }
         else if (a == "--layout") {
             std::string l = val("--layout");
             if (l == "rs") o->rs = true;
@@ -378,7 +384,7 @@ public:
             // the records' CRC-32s from the reduced bucket on the GPU (a few us; the host would read the
             // whole reply back); a part read in place into its reply has no device output: the host seals it
             std::vector<uint32_t> crcs(dsts.size());
-            const bool gpu_crc = !bytes.empty() && b.numel * (size_t)b.elem >= kGpuCrcMinBytes &&
+            const bool gpu_crc = o_.gpu_crc && !bytes.empty() && b.numel * (size_t)b.elem >= kGpuCrcMinBytes &&
                                  fa_output_crc32(ctx_, mp, (int)bytes.size(), bytes.data(), crcs.data()) == FA_OK;
             t_fin = secs_since(t1);
             if (!gpu_crc || !ar.seal_params_with((uint8_t*)values, crcs.data())) ar.seal_params((uint8_t*)values);
