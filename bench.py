@@ -901,7 +901,7 @@ def device_to_host(ptr, count, dtype):
     return out
 
 
-def _read_rate(torch, setup, stream, launch, reps):
+def _read_rate(torch, setup, stream, launch, reps, passes=1):
     """GB/s of one read-only launch form over the setup's client slots: one launch per range piece (a bucket
     set held in pieces, e.g. C5 on one GPU, is reduced one launch per piece too), bytes of all pieces / the
     sum of their median HIP-event times on the launch stream.  The reps rotate over the input sets as the
@@ -922,7 +922,7 @@ def _read_rate(torch, setup, stream, launch, reps):
             b.synchronize()
             if i >= 2:
                 ms.append(a.elapsed_time(b))
-        nbytes += setup.D * n * 4
+        nbytes += passes * setup.D * n * 4
         t_ms += statistics.median(ms)
     return round(nbytes / (t_ms * 1e-3) / 1e9, 1)
 
@@ -949,6 +949,25 @@ def read_plain_peak(fa, torch, setup, stream, reps=5):
     best = max(rates, key=rates.get)
     return {"GBs": rates[best], "form": best, "forms": rates,
             "kernel": "plain grid-stride read, 256 lanes per workgroup, nt 16-byte loads, slot after slot"}
+
+
+RW_PLAIN_FORMS = [(g, u, nt) for g in (2048, 4096, 8192, 16384) for u in (8, 16) for nt in (False, True)]
+
+
+def rw_plain_peak(fa, torch, setup, stream, reps=3):
+    """The independent in-place read+write ceiling on the sync legs' own slots (their traffic: every slot read
+    and written back where it lies): the best of plain grid-stride launches (fa_diag_rw_plain; grids x loads in
+    flight x plain/nt stores of RW_PLAIN_FORMS), slot after slot, none of the sync kernel's element-major walk.
+    GB/s counts the bytes read and the bytes written, as the sync legs' algorithmic bytes do."""
+    rates = {}
+    for g, u, nt in RW_PLAIN_FORMS:
+        rates["grid%d_u%d_%s" % (g, u, "nt" if nt else "plain")] = _read_rate(
+            torch, setup, stream,
+            lambda ptrs, n: fa.diag_rw_plain(ptrs, n, grid=g, unroll=u, nt=nt, stream=stream), reps, passes=2)
+    best = max(rates, key=rates.get)
+    return {"GBs": rates[best], "form": best, "forms": rates,
+            "kernel": "plain grid-stride in-place read+write, 256 lanes per workgroup, nt 16-byte loads, "
+                      "slot after slot"}
 
 
 def settle(freed_bytes):
@@ -1068,6 +1087,7 @@ CONFIG_KEYS = ("workload", "description", "clients", "elems_per_client", "in_dty
 # a leg's figure -> its key in the compact line
 LEG_KEYS = (("gib_s", "gib_s"), ("frac", "frac"), ("kernel_ms_avg", "ms"), ("round_ms_avg", "ms"),
             ("ms_per_round", "ms"), ("ms_per_step", "ms"), ("frac_of_read_stream_independent", "frac_ind"),
+            ("frac_of_copy_independent", "frac_copy_ind"),
             ("cpu_gib_s", "cpu_gib_s"), ("gpus", "gpus"), ("h2d_ms", "h2d_ms"), ("reduce_ms", "reduce_ms"),
             ("d2h_ms", "d2h_ms"), ("pcie_GBs", "pcie_GBs"))
 E2E_KEYS = (("e2e_loopback_literal", "e2e_literal_ms"), ("e2e_loopback_fedavg", "e2e_fedavg_ms"),
@@ -1815,7 +1835,12 @@ def single_gpu_secondaries(fa, torch, args, device, stream, dist, barrier):
         sec[key] = {"description": desc, "kernel_ms_avg": round(ka, 4),
                     "achieved_GBs": round(s.algo_bytes() / (ka * 1e-3) / 1e9, 1),
                     "frac": round(s.algo_bytes() / (ka * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                    "input_sets_rotated": s.nsets, "parity": parity_guarded(lambda: s.parity(0))}
+                    "input_sets_rotated": s.nsets}
+        if isinstance(s, SyncSetup) and s.in_dt == fa.F32 and not under_profiler():
+            cp = rw_plain_peak(fa, torch, s, stream)  # before the parity check, which refills a set
+            sec[key]["copy_ceiling_independent"] = cp
+            sec[key]["frac_of_copy_independent"] = round(sec[key]["achieved_GBs"] / cp["GBs"], 4)
+        sec[key]["parity"] = parity_guarded(lambda: s.parity(0))
         s.close()
         settle(s.nsets * s.input_bytes())
     # compute-node aggregation on the C2 shape: 8 client copies synced in place

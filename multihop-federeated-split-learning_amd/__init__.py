@@ -95,6 +95,7 @@ def lib():
         "fa_fill_uniform": (I, [P, S, I, U64, U32, U64, P]),
         "fa_diag_read_stream": (I, [P, I, S, P]),  # diagnostics (outside fa.h)
         "fa_diag_read_plain": (I, [P, I, S, I, I, P]),
+        "fa_diag_rw_plain": (I, [P, I, S, I, I, I, P]),
         "fa_diag_plan_chain": (I, [I, I, S, I, I, I, ctypes.POINTER(I), ctypes.POINTER(ctypes.c_longlong)]),
         "fa_diag_rs_plan": (I, [S, I, I, I, I, I, I, ctypes.POINTER(I), ctypes.POINTER(I),
                                 ctypes.POINTER(ctypes.c_longlong)]),
@@ -238,6 +239,14 @@ def diag_read_plain(buffers, n, grid=8192, unroll=16, stream=None):
     buffers (n elements each) one after another, on `stream`."""
     arr = (ctypes.c_void_p * len(buffers))(*[_addr(b) for b in buffers])
     check(lib().fa_diag_read_plain(arr, len(buffers), n, grid, unroll, _stream(stream)))
+
+
+def diag_rw_plain(buffers, n, grid=8192, unroll=16, nt=False, stream=None):
+    """fa_diag_rw_plain (diagnostic, outside fa.h): the independent in-place read+write ceiling -- one plain
+    grid-stride launch reading every fp32 device buffer (n elements each) and writing it back where it lies
+    (values unchanged), buffer after buffer, nt loads and plain (or nt) stores, on `stream`."""
+    arr = (ctypes.c_void_p * len(buffers))(*[_addr(b) for b in buffers])
+    check(lib().fa_diag_rw_plain(arr, len(buffers), n, grid, unroll, 1 if nt else 0, _stream(stream)))
 
 
 PLAN_ONE_SHOT, PLAN_SCALAR, PLAN_PHASED = 0, 1, 2

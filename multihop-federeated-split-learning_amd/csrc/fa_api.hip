@@ -2223,6 +2223,21 @@ extern "C" int fa_diag_read_plain(const void* const* d_bufs, int nc, size_t n, i
     return FA_OK;
 }
 
+// Diagnostic, not part of the ABI in fa.h: the independent in-place read+write ceiling -- every buffer read
+// and written back where it lies (x * 1), a plain grid-stride walk buffer after buffer (grid workgroups of 256
+// lanes, `unroll` 8 or 16 non-temporal 16-byte loads in flight per lane, plain or non-temporal stores); bench.py
+// times it on the sync legs' own slots (copy_ceiling_independent).  The values are left as they were.
+extern "C" int fa_diag_rw_plain(const void* const* d_bufs, int nc, size_t n, int grid, int unroll, int nt,
+                                void* hip_stream) {
+    g_err.clear();
+    if (grid < 1 || grid > (1 << 20) || (unroll != 8 && unroll != 16)) return fail(FA_ERR_ARG, "bad grid or unroll");
+    fa::ClientTable t{};
+    int rc;
+    if ((rc = read_table(d_bufs, nc, n, &t))) return rc;
+    FA_HIP(fa::launch_rw_plain(t, nc, (int64_t)(n / 4), grid, unroll, nt != 0, static_cast<hipStream_t>(hip_stream)));
+    return FA_OK;
+}
+
 // Diagnostic, not part of the ABI in fa.h: how many reductions of this context read their receipts in place
 // (small pinned receipts, host_reduce); -1 for a null context.
 extern "C" long long fa_diag_host_reads(fa_ctx* ctx) { return ctx ? (long long)ctx->host_reads : -1; }

@@ -103,5 +103,6 @@ hipError_t launch_fill(void* dst, int64_t n, fa_dtype dt, uint64_t seed, uint32_
 hipError_t launch_read_probe(const ClientTable& t, int nc, int64_t nvec, float* sink, hipStream_t s);
 hipError_t launch_read_plain(const ClientTable& t, int nc, int64_t nvec, int grid, int unroll, float* sink,
                              hipStream_t s);
+hipError_t launch_rw_plain(const ClientTable& t, int nc, int64_t nvec, int grid, int unroll, bool nt, hipStream_t s);
 
 }  // namespace fa

@@ -1321,6 +1321,44 @@ hipError_t launch_read_plain(const ClientTable& t, int nc, int64_t nvec, int gri
     return hipGetLastError();
 }
 
+// Independent in-place read+write ceiling (the compute-node sync legs' copy_ceiling_independent): every
+// slot read and written back where it lies, a plain grid-stride walk slot after slot with U non-temporal
+// 16-byte loads in flight per lane, stored plain or non-temporal -- the sync's traffic (D reads + D writes of
+// the same addresses) with none of its element-major structure.  x * scale with scale = 1 leaves every
+// finite value as it was and keeps the store from being folded away.
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void rw_plain_kernel(const ClientTable t, int nc, int64_t nvec, float scale) {
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int k = 0; k < nc; ++k) {
+        f32x4* p = static_cast<f32x4*>(const_cast<void*>(t.src[k]));
+        int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+        for (; v + (U - 1) * stride < nvec; v += U * stride) {
+            f32x4 x[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) x[u] = __builtin_nontemporal_load(p + v + u * stride);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if constexpr (NT) __builtin_nontemporal_store(x[u] * scale, p + v + u * stride);
+                else p[v + u * stride] = x[u] * scale;
+            }
+        }
+        for (; v < nvec; v += stride) {
+            const f32x4 x = __builtin_nontemporal_load(p + v) * scale;
+            if constexpr (NT) __builtin_nontemporal_store(x, p + v);
+            else p[v] = x;
+        }
+    }
+}
+
+hipError_t launch_rw_plain(const ClientTable& t, int nc, int64_t nvec, int grid, int unroll, bool nt, hipStream_t s) {
+    const dim3 g((unsigned)grid), b(256);
+    if (unroll == 8 && nt) hipLaunchKernelGGL((rw_plain_kernel<8, true>), g, b, 0, s, t, nc, nvec, 1.0f);
+    else if (unroll == 8) hipLaunchKernelGGL((rw_plain_kernel<8, false>), g, b, 0, s, t, nc, nvec, 1.0f);
+    else if (nt) hipLaunchKernelGGL((rw_plain_kernel<16, true>), g, b, 0, s, t, nc, nvec, 1.0f);
+    else hipLaunchKernelGGL((rw_plain_kernel<16, false>), g, b, 0, s, t, nc, nvec, 1.0f);
+    return hipGetLastError();
+}
+
 hipError_t launch_fill(void* dst, int64_t n, fa_dtype dt, uint64_t seed, uint32_t client, uint64_t idx0,
                        hipStream_t s) {
     Tuning tu{256, 8192, 8, 0, 0};

@@ -1023,6 +1023,25 @@ def test_read_stream_probe_reads_only(fa, O, torch_gpu, n, D):
         fa.diag_read_stream(clients, n + 1, stream=s)  # not a multiple of 4
 
 
+@pytest.mark.parametrize("n,D,grid,unroll,nt", [(1_000_000, 8, 2048, 8, False), (4_000_004, 3, 8192, 16, True),
+                                                (12, 2, 16384, 16, False), (2_000_000, 20, 4096, 16, True)])
+def test_rw_plain_probe_leaves_values(fa, O, torch_gpu, n, D, grid, unroll, nt):
+    """fa_diag_rw_plain (the sync legs' copy_ceiling_independent): every slot is read and written back where
+    it lies, x * 1 -- every client buffer keeps its bits (full strides, the strided tail and a buffer smaller
+    than one stride), so the bench's sync parity check after it sees the slots as they were."""
+    torch = torch_gpu
+    clients = [filled(fa, torch, n, False, 57, k) for k in range(D)]
+    before = [c.clone() for c in clients]
+    s = torch.cuda.Stream()
+    for _ in range(2):
+        fa.diag_rw_plain(clients, n, grid=grid, unroll=unroll, nt=nt, stream=s)
+    s.synchronize()
+    for a, b in zip(clients, before):
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+    with pytest.raises(fa.FaError):
+        fa.diag_rw_plain(clients, n, grid=grid, unroll=12, stream=s)  # unroll 8 or 16 only
+
+
 def test_context_misuse(fa, O, torch_gpu):
     """Misuse of a context is an error code, never a wrong result: gather pieces that do not add up to
     the bucket, a slot out of range, a finalize into pieces of the wrong total; redefining a bucket
