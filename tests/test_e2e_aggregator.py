@@ -98,6 +98,7 @@ def _large_parts(d, bf16=False):
     (True, False, ["--layout", "rs", "--rs-chunks", "3"]),  # RCCL reduce-scatter layout (one GPU: a copy)
     (True, False, ["--rx-concurrency", "2"]),           # 6 owners at once, 2 large receipts received at a time
     (False, False, ["--rx-concurrency", "0"]),          # no receive gate
+    (True, False, ["--crc", "host"]),                   # reply CRC-32s from the host (default: the GPU's)
 ])
 def test_multi_mb_parts_concurrent_owners(torch_gpu, tmp_path, pinned, sequential, extra):
     """D=6 owners sending at once (or one after another) multi-MB parts: pinned zero-copy ingest
