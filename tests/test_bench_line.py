@@ -153,3 +153,31 @@ def test_cpu_baseline_cores_spread_over_ccds(monkeypatch):
     assert bench.compact_cpus([0, 1, 2, 3, 8, 16, 17]) == "0-3,8,16-17"
     s = bench.spread([0.5, 0.25, 1.0], 2**30)
     assert s == {"min": 1.0, "median": 2.0, "max": 4.0, "reps": 3}
+
+
+def test_round6_full_record_compacts_to_its_printed_line():
+    """The round's final-tree run (r06s25): the line the bench printed is compact_line of the full record it
+    wrote beside it, within the bound, with the sync legs' copy-ceiling fraction and the C2 end-to-end keys."""
+    import bench
+    with open(os.path.join(ROOT, "profiles", "r06s25_bench_full.json")) as f:
+        full = json.load(f)
+    with open(os.path.join(ROOT, "profiles", "r06s25_bench_line.json")) as f:
+        printed = json.load(f)
+    got = _check(full, bench)
+    assert json.loads(json.dumps(bench.compact_line(full, printed["full_record"]))) == printed
+    assert "frac_copy_ind" in got["secondary"]["sync_c2"] and "e2e_fedavg_tail_ms" in got["secondary"]["round_c2"]
+
+
+def test_timed_loop_refuses_a_non_stream():
+    """timed_loop records HIP events on the stream it is given; anything else (a bool once reached it and
+    crashed inside the HIP runtime, r06s11-s20) is a TypeError before any launch."""
+    import pytest
+    import bench
+
+    class NoLaunch:
+        def launch(self, step, stream):
+            raise AssertionError("launched")
+
+    for bad in (True, False, None, 0):
+        with pytest.raises(TypeError):
+            bench.timed_loop(None, NoLaunch(), 1, 0, bad, None, lambda: None)
